@@ -1,0 +1,868 @@
+/*
+ * ccdec_oracle.c -- CPU restatement of the Cool-chic fixed-point decoder.
+ *
+ * TEST INFRASTRUCTURE ONLY (see ccdec_oracle.h).  Written from the reference's
+ * behaviour, one function per reference stage; every function cites the
+ * reference file:line it restates.  Planes are kept unpadded; the reference's
+ * padded frame_memory is replaced by explicit border rules (zero / replicate).
+ *
+ * Build with -fwrapv: the reference accumulates in int32 and relies on
+ * two's-complement wrap.
+ */
+#include "ccdec_oracle.h"
+
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+#include <time.h>
+
+#define ARM_PREC 8
+#define UPS_PREC 12
+#define SYN_PREC 12
+
+static double now_s(void)
+{
+    struct timespec ts;
+    clock_gettime(CLOCK_MONOTONIC, &ts);
+    return ts.tv_sec + 1e-9 * ts.tv_nsec;
+}
+
+/* ------------------------------------------------------------------------- */
+/* CABAC (HEVC/VVC binary arithmetic decoder + VVC dual-rate model).           */
+/* TDecBinCoderCABAC.h:58-121, TDecBinCoderCABAC.cpp:64-178, Contexts.h:84-176 */
+/* ------------------------------------------------------------------------- */
+
+typedef struct {
+    const uint8_t *buf;
+    size_t len, pos;
+    uint32_t range, value;
+    int32_t bits_needed;
+} bac_t;
+
+typedef struct { uint16_t s0, s1; uint8_t rate; } model_t;
+
+#define MASK0 0x7FE0u /* 10-bit estimate, Contexts.h:47 */
+#define MASK1 0x7FFEu /* 14-bit estimate, Contexts.h:48 */
+
+static const uint8_t k_lps_renorm[32] = { /* Contexts.cpp:45-55 */
+    6, 5, 4, 4, 3, 3, 3, 3, 2, 2, 2, 2, 2, 2, 2, 2,
+    1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1};
+
+static uint32_t rd(bac_t *c)
+{
+    /* InputBitstream::readByte (BitStream.h:175); past-the-end reads yield 0. */
+    uint32_t v = c->pos < c->len ? c->buf[c->pos] : 0u;
+    c->pos++;
+    return v;
+}
+
+static void model_init(model_t *m, int idx)
+{
+    m->s0 = (uint16_t)((idx << 8) & MASK0);
+    m->s1 = (uint16_t)((idx << 8) & MASK1);
+    m->rate = 8; /* DWS */
+}
+
+static unsigned model_state(const model_t *m) { return ((unsigned)(m->s0 + m->s1) >> 8) & 0xFF; }
+
+static void model_update(model_t *m, unsigned bin)
+{
+    int r0 = m->rate >> 4, r1 = m->rate & 15;
+    m->s0 = (uint16_t)(m->s0 - ((m->s0 >> r0) & MASK0));
+    m->s1 = (uint16_t)(m->s1 - ((m->s1 >> r1) & MASK1));
+    if (bin) {
+        m->s0 = (uint16_t)(m->s0 + ((0x7FFFu >> r0) & MASK0));
+        m->s1 = (uint16_t)(m->s1 + ((0x7FFFu >> r1) & MASK1));
+    }
+}
+
+static void bac_start(bac_t *c, const uint8_t *buf, size_t len)
+{
+    c->buf = buf; c->len = len; c->pos = 0;
+    c->range = 510;
+    c->value = rd(c) << 8;
+    c->value |= rd(c);
+    c->bits_needed = -8;
+}
+
+static unsigned bac_bin(bac_t *c, model_t *m, int update)
+{
+    unsigned st = model_state(m);
+    unsigned bin = st >> 7;
+    unsigned q = st & 0x80 ? st ^ 0xFF : st;
+    uint32_t lps = (((q >> 2) * (c->range >> 5)) >> 1) + 4;
+    c->range -= lps;
+    uint32_t scaled = c->range << 7;
+    if (c->value < scaled) {
+        if (c->range < 256) {
+            c->range <<= 1; c->value <<= 1; c->bits_needed += 1;
+            if (c->bits_needed >= 0) { c->value += rd(c) << c->bits_needed; c->bits_needed -= 8; }
+        }
+    } else {
+        int nb = k_lps_renorm[lps >> 3];
+        bin = 1 - bin;
+        c->value = (c->value - scaled) << nb;
+        c->range = lps << nb;
+        c->bits_needed += nb;
+        if (c->bits_needed >= 0) { c->value += rd(c) << c->bits_needed; c->bits_needed -= 8; }
+    }
+    if (update) model_update(m, bin);
+    return bin;
+}
+
+static unsigned bac_ep(bac_t *c)
+{
+    c->value += c->value;
+    if (++c->bits_needed >= 0) { c->value += rd(c); c->bits_needed = -8; }
+    uint32_t scaled = c->range << 7;
+    if (c->value >= scaled) { c->value -= scaled; return 1; }
+    return 0;
+}
+
+static unsigned bac_eps(bac_t *c, int n)
+{
+    unsigned bins = 0;
+    if (c->range == 256) { /* decodeAlignedBinsEP, TDecBinCoderCABAC.cpp:128-156 */
+        unsigned rem = (unsigned)n;
+        while (rem > 0) {
+            unsigned take = rem < 8 ? rem : 8;
+            unsigned nb = (c->value >> (15 - take)) & ((1u << take) - 1);
+            bins = (bins << take) | nb;
+            c->value = (c->value << take) & 0x7FFF;
+            rem -= take;
+            c->bits_needed += (int)take;
+            if (c->bits_needed >= 0) { c->value |= rd(c) << c->bits_needed; c->bits_needed -= 8; }
+        }
+        return bins;
+    }
+    unsigned rem = (unsigned)n;
+    while (rem > 8) {
+        c->value = (c->value << 8) + (rd(c) << (8 + c->bits_needed));
+        uint32_t scaled = c->range << 15;
+        for (int i = 0; i < 8; i++) {
+            bins += bins; scaled >>= 1;
+            if (c->value >= scaled) { bins++; c->value -= scaled; }
+        }
+        rem -= 8;
+    }
+    c->bits_needed += (int)rem;
+    c->value <<= rem;
+    if (c->bits_needed >= 0) { c->value += rd(c) << c->bits_needed; c->bits_needed -= 8; }
+    uint32_t scaled = c->range << (rem + 7);
+    for (unsigned i = 0; i < rem; i++) {
+        bins += bins; scaled >>= 1;
+        if (c->value >= scaled) { bins++; c->value -= scaled; }
+    }
+    return bins;
+}
+
+static int bac_expgolomb(bac_t *c, int k)
+{
+    int sym = 0;
+    unsigned bit = 1;
+    while (bit) { bit = bac_ep(c); sym += (int)(bit << k); k++; }
+    k--;
+    if (k > 0) sym += (int)bac_eps(c, k);
+    return sym;
+}
+
+/* ------------------------------------------------------------------------- */
+/* Static latent contexts and (mu, log_scale) -> context index.               */
+/* cc-contexts.h:20-48, cc-contexts.cpp:15-900                                */
+/* ------------------------------------------------------------------------- */
+
+static const uint8_t k_ctx_states[17 * 50 * 5] = {
+#include "../cool-chic_amd/csrc/ccmi_ctx_table.inc"
+};
+
+static void mu_sig_index(int32_t mu, int32_t log_sig, int *mu_round, int *mu_idx, int *sig_idx)
+{
+    int32_t r = mu >= 0 ? ((mu + 128) >> 8) << 8 : -(((-mu + 128) >> 8) << 8);
+    int32_t mi = (mu - r) * 16;
+    mi = mi >= 0 ? (mi + 128) >> 8 : -((-mi + 128) >> 8);
+    mi += 8;
+    int32_t ls = log_sig + 256; /* - SIG_LOG_MIN * ARM_SCALE, SIG_LOG_MIN = -1 */
+    int32_t si;
+    if (ls < 0) si = 0;
+    else {
+        si = (ls * 5 + 128) >> 8; /* N_SIGQ / (SIG_LOG_MAX_EXCL - SIG_LOG_MIN) = 5 */
+        if (si >= 50) si = 49;
+    }
+    *mu_round = r >> 8;
+    *mu_idx = mi;
+    *sig_idx = si;
+}
+
+/* cc-bac.h:192-231 decode_single, with static (never-updated) contexts. */
+static int32_t decode_value(bac_t *c, int mu_idx, int sig_idx)
+{
+    const uint8_t *s = &k_ctx_states[(mu_idx * 50 + sig_idx) * 5];
+    model_t m;
+    model_init(&m, s[0]);
+    if (!bac_bin(c, &m, 0)) return 0;
+    int v;
+    model_init(&m, s[1]);
+    if (!bac_bin(c, &m, 0)) v = 1;
+    else {
+        model_init(&m, s[2]);
+        if (!bac_bin(c, &m, 0)) v = 2;
+        else {
+            model_init(&m, s[3]);
+            if (!bac_bin(c, &m, 0)) v = 3;
+            else v = bac_expgolomb(c, 0) + 4;
+        }
+    }
+    model_init(&m, s[4]);
+    if (bac_bin(c, &m, 0)) v = -v;
+    return v;
+}
+
+/* ------------------------------------------------------------------------- */
+/* .cool parsing. cc-bitstream.cpp:58-84 (GOP), :140-234 (frame), :249-275    */
+/* ------------------------------------------------------------------------- */
+
+typedef struct { int n_out, ks, residual, relu; } syn_layer_t;
+typedef struct { int qw, qb, sw, sb, nw, nb; } lqi_t;
+
+typedef struct {
+    int h, w, bitdepth, frame_data_type, intra_period, p_period;
+    int dim_arm, n_hidden_arm;
+    int n_ups, ups_ks, n_pre, pre_ks;
+    int n_branches, n_syn;
+    syn_layer_t syn[16];
+    int flow_gain, ac_max_nn, ac_max_lat, sig_blk;
+    lqi_t arm, ups, synq;
+    int n_layers, n_grid;
+    int nft[CCO_MAX_LAYERS];
+    int nbytes_lat[CCO_MAX_LAYERS];
+    const uint8_t *arm_w, *arm_b, *ups_w, *ups_b, *syn_w, *syn_b, *lat[CCO_MAX_LAYERS];
+} hdr_t;
+
+typedef struct { const uint8_t *p; size_t n, pos; int err; } rdr_t;
+
+static int rdn(rdr_t *r, int nbytes)
+{
+    if (r->pos + (size_t)nbytes > r->n) { r->err = 1; return 0; }
+    int v = 0;
+    for (int i = 0; i < nbytes; i++) v = (v << 8) | r->p[r->pos++];
+    return v;
+}
+
+static const uint8_t *take(rdr_t *r, int nbytes)
+{
+    if (nbytes < 0 || r->pos + (size_t)nbytes > r->n) { r->err = 1; return NULL; }
+    const uint8_t *q = r->p + r->pos;
+    r->pos += (size_t)nbytes;
+    return q;
+}
+
+static int parse(const uint8_t *bs, size_t n, hdr_t *h)
+{
+    rdr_t r = {bs, n, 0, 0};
+    memset(h, 0, sizeof(*h));
+    rdn(&r, 2); /* n_bytes_header */
+    h->h = rdn(&r, 2);
+    h->w = rdn(&r, 2);
+    int raw = rdn(&r, 1);
+    h->bitdepth = (raw >> 4) + 8;
+    h->frame_data_type = raw & 0xF;
+    h->intra_period = rdn(&r, 1);
+    h->p_period = rdn(&r, 1);
+    /* frame header */
+    rdn(&r, 2); /* n_bytes_header */
+    rdn(&r, 1); /* display_index */
+    raw = rdn(&r, 1);
+    h->dim_arm = 8 * (raw >> 4);
+    h->n_hidden_arm = raw & 0xF;
+    raw = rdn(&r, 1);
+    h->n_ups = raw >> 4; h->ups_ks = raw & 0xF;
+    raw = rdn(&r, 1);
+    h->n_pre = raw >> 4; h->pre_ks = raw & 0xF;
+    h->n_branches = rdn(&r, 1);
+    h->n_syn = rdn(&r, 1);
+    if (h->n_syn > 16 || h->n_syn < 1) return 1;
+    for (int i = 0; i < h->n_syn; i++) {
+        h->syn[i].n_out = rdn(&r, 1);
+        h->syn[i].ks = rdn(&r, 1);
+        raw = rdn(&r, 1);
+        h->syn[i].residual = (raw >> 4) != 0;
+        h->syn[i].relu = (raw & 0xF) != 0;
+    }
+    h->flow_gain = rdn(&r, 1);
+    h->ac_max_nn = rdn(&r, 2);
+    h->ac_max_lat = rdn(&r, 2);
+    h->sig_blk = (signed char)rdn(&r, 1);
+    lqi_t *q[3] = {&h->arm, &h->ups, &h->synq};
+    for (int i = 0; i < 3; i++) {
+        q[i]->qw = rdn(&r, 1);
+        q[i]->qb = rdn(&r, 1);
+        if (q[i]->qb == 255) q[i]->qb = -1;
+    }
+    for (int i = 0; i < 3; i++) {
+        q[i]->sw = rdn(&r, 1);
+        q[i]->sb = q[i]->qb < 0 ? -1 : rdn(&r, 1);
+    }
+    for (int i = 0; i < 3; i++) {
+        q[i]->nw = rdn(&r, 2);
+        q[i]->nb = q[i]->qb < 0 ? -1 : rdn(&r, 2);
+    }
+    h->n_layers = rdn(&r, 1);
+    h->n_grid = rdn(&r, 1);
+    if (h->n_layers < 2 || h->n_layers > CCO_MAX_LAYERS || h->n_grid != h->n_layers) return 1;
+    for (int i = 0; i < h->n_layers; i++) h->nft[i] = rdn(&r, 1);
+    for (int i = 0; i < h->n_grid; i++) h->nbytes_lat[i] = rdn(&r, 3);
+    if (r.err) return 1;
+    h->arm_w = take(&r, h->arm.nw);
+    h->arm_b = take(&r, h->arm.nb < 0 ? 0 : h->arm.nb);
+    h->ups_w = take(&r, h->ups.nw);
+    h->ups_b = take(&r, h->ups.nb < 0 ? 0 : h->ups.nb);
+    h->syn_w = take(&r, h->synq.nw);
+    h->syn_b = take(&r, h->synq.nb < 0 ? 0 : h->synq.nb);
+    for (int i = 0; i < h->n_layers; i++) h->lat[i] = take(&r, h->nbytes_lat[i]);
+    if (r.err) return 1;
+    for (int i = 0; i < h->n_layers; i++) if (h->nft[i] != 1) return 1;
+    if (h->dim_arm != 8 && h->dim_arm != 16 && h->dim_arm != 24 && h->dim_arm != 32) return 1;
+    return 0;
+}
+
+/* ------------------------------------------------------------------------- */
+/* NN weights: Exp-Golomb magnitudes + EP sign, then << (precision - shift).  */
+/* cc-frame-decoder.cpp:157-199, shift tables :28-108                         */
+/* ------------------------------------------------------------------------- */
+
+static int read_weights(bac_t *c, int k, int n, int shift, int prec, int32_t *dst)
+{
+    if (prec < shift) return 1;
+    for (int i = 0; i < n; i++) {
+        int v = bac_expgolomb(c, k);
+        if (v != 0 && bac_ep(c)) v = -v;
+        dst[i] = (int32_t)((uint32_t)v << (prec - shift));
+    }
+    return 0;
+}
+
+/* decode_upsweights_qi: read (ks+1)/2 taps, mirror the first nw/2*2 onto the tail. */
+static int read_sym_kernel(bac_t *c, int k, int ks, int shift, int prec, int32_t *dst)
+{
+    int nw = (ks + 1) / 2;
+    if (read_weights(c, k, nw, shift, prec, dst)) return 1;
+    for (int i = 0; i < nw / 2 * 2; i++) dst[ks - 1 - i] = dst[i];
+    return 0;
+}
+
+typedef struct {
+    int d, nh;
+    int32_t w_hidden[4][32 * 32]; /* [out][in] as coded */
+    int32_t b_hidden[4][32];
+    int32_t w_out[2 * 32], b_out[2];
+    int32_t ups[CCO_MAX_LAYERS][16], pre[CCO_MAX_LAYERS][16];
+    int32_t blend[8];
+    int32_t *syn_w[8][16], *syn_b[8][16];
+} nets_t;
+
+static void free_nets(nets_t *nn)
+{
+    for (int b = 0; b < 8; b++)
+        for (int l = 0; l < 16; l++) { free(nn->syn_w[b][l]); free(nn->syn_b[b][l]); }
+}
+
+static int read_nets(const hdr_t *h, nets_t *nn)
+{
+    memset(nn, 0, sizeof(*nn));
+    bac_t cw, cb;
+    nn->d = h->dim_arm;
+    nn->nh = h->n_hidden_arm;
+    if (nn->nh > 4 || h->arm.qw > 8 || h->arm.qb < 0 || h->arm.qb > 16) return 1;
+    int ws = 8 - h->arm.qw, bsh = 16 - h->arm.qb;
+    bac_start(&cw, h->arm_w, (size_t)h->arm.nw);
+    bac_start(&cb, h->arm_b, (size_t)h->arm.nb);
+    int d = nn->d;
+    for (int l = 0; l < nn->nh; l++) {
+        if (read_weights(&cw, h->arm.sw, d * d, ws, ARM_PREC, nn->w_hidden[l])) return 1;
+        if (read_weights(&cb, h->arm.sb, d, bsh, 2 * ARM_PREC, nn->b_hidden[l])) return 1;
+    }
+    if (read_weights(&cw, h->arm.sw, 2 * d, ws, ARM_PREC, nn->w_out)) return 1;
+    if (read_weights(&cb, h->arm.sb, 2, bsh, 2 * ARM_PREC, nn->b_out)) return 1;
+
+    if (h->ups.qw > 12 || h->ups_ks > 16 || h->pre_ks > 16 || h->n_ups < 1 || h->n_pre < 1) return 1;
+    bac_start(&cw, h->ups_w, (size_t)h->ups.nw);
+    for (int l = 0; l < h->n_ups; l++)
+        if (read_sym_kernel(&cw, h->ups.sw, h->ups_ks, 12 - h->ups.qw, UPS_PREC, nn->ups[l])) return 1;
+    for (int l = 0; l < h->n_pre; l++)
+        if (read_sym_kernel(&cw, h->ups.sw, h->pre_ks, 12 - h->ups.qw, UPS_PREC, nn->pre[l])) return 1;
+
+    if (h->synq.qw > 12 || h->synq.qb < 0 || h->synq.qb > 24 || h->n_branches < 1 || h->n_branches > 8) return 1;
+    ws = 12 - h->synq.qw;
+    bsh = 24 - h->synq.qb;
+    bac_start(&cw, h->syn_w, (size_t)h->synq.nw);
+    bac_start(&cb, h->syn_b, (size_t)h->synq.nb);
+    if (h->n_branches > 1 && read_weights(&cw, h->synq.sw, h->n_branches, ws, SYN_PREC, nn->blend)) return 1;
+    for (int b = 0; b < h->n_branches; b++) {
+        int nin = h->n_layers;
+        for (int l = 0; l < h->n_syn; l++) {
+            const syn_layer_t *L = &h->syn[l];
+            int nw = nin * L->ks * L->ks * L->n_out;
+            nn->syn_w[b][l] = (int32_t *)malloc(sizeof(int32_t) * (size_t)(nw > 0 ? nw : 1));
+            nn->syn_b[b][l] = (int32_t *)malloc(sizeof(int32_t) * (size_t)(L->n_out > 0 ? L->n_out : 1));
+            if (read_weights(&cw, h->synq.sw, nw, ws, SYN_PREC, nn->syn_w[b][l])) return 1;
+            if (read_weights(&cb, h->synq.sb, L->n_out, bsh, 2 * SYN_PREC, nn->syn_b[b][l])) return 1;
+            nin = L->n_out;
+        }
+    }
+    return 0;
+}
+
+/* ------------------------------------------------------------------------- */
+/* ARM + CABAC latent decode, raster order.                                    */
+/* arm_cpu.cpp:18-106; contexts cc-frame-decoder.cpp:111-154; BACContext       */
+/* cc-bac.h:3-190; decode_latent_layer_bac_single cc-bac.h:234-253             */
+/* ------------------------------------------------------------------------- */
+
+/* (dy, dx) of the causal context pixels, in the reference's gather order. */
+static int ctx_offsets(int d, int *dy, int *dx)
+{
+    static const signed char o8[][2] = {{-3,0},{-2,0},{-1,-1},{-1,0},{-1,1},{0,-3},{0,-2},{0,-1}};
+    static const signed char o16[][2] = {{-3,0},{-3,1},{-2,-2},{-2,-1},{-2,0},{-2,1},{-2,2},
+        {-1,-3},{-1,-2},{-1,-1},{-1,0},{-1,1},{-1,2},{0,-3},{0,-2},{0,-1}};
+    static const signed char o24[][2] = {{-4,0},{-3,-2},{-3,-1},{-3,0},{-3,1},{-3,2},
+        {-2,-3},{-2,-2},{-2,-1},{-2,0},{-2,1},{-2,2},{-2,3},
+        {-1,-3},{-1,-2},{-1,-1},{-1,0},{-1,1},{-1,2},{-1,3},{0,-4},{0,-3},{0,-2},{0,-1}};
+    static const signed char o32[][2] = {{-4,-2},{-4,-1},{-4,0},{-4,1},
+        {-3,-3},{-3,-2},{-3,-1},{-3,0},{-3,1},{-3,2},{-3,3},
+        {-2,-3},{-2,-2},{-2,-1},{-2,0},{-2,1},{-2,2},{-2,3},{-2,4},
+        {-1,-4},{-1,-3},{-1,-2},{-1,-1},{-1,0},{-1,1},{-1,2},{-1,3},{-1,4},{0,-4},{0,-3},{0,-2},{0,-1}};
+    const signed char (*o)[2] = d == 8 ? o8 : d == 16 ? o16 : d == 24 ? o24 : d == 32 ? o32 : NULL;
+    if (!o) return 1;
+    for (int i = 0; i < d; i++) { dy[i] = o[i][0]; dx[i] = o[i][1]; }
+    return 0;
+}
+
+static int arm_decode_layer(const nets_t *nn, const uint8_t *bytes, size_t nbytes, int sig_blk,
+                            int h, int w, int32_t *plane)
+{
+    bac_t c;
+    bac_start(&c, bytes, nbytes);
+    /* BACContext::set_layer (cc-bac.h:24-130) */
+    int updated = sig_blk < 0;
+    int blk = sig_blk < 0 ? -sig_blk : sig_blk;
+    int shift = 0;
+    while ((1 << shift) < blk) shift++;
+    int mask = (1 << shift) - 1;
+    int nby = 1, nbx = 1;
+    if (blk > 0) { nby = (h + blk - 1) >> shift; nbx = (w + blk - 1) >> shift; }
+    uint8_t *sig = (uint8_t *)malloc((size_t)nby * nbx);
+    uint8_t *flat = (uint8_t *)calloc((size_t)nby * nbx, 1);
+    memset(sig, 1, (size_t)nby * nbx);
+    if (nby != 1 || nbx != 1) {
+        if (bac_ep(&c)) {
+            model_t m; model_init(&m, 65);
+            for (int i = 0; i < nby * nbx; i++) sig[i] = (uint8_t)(updated ? bac_bin(&c, &m, 1) : bac_ep(&c));
+        }
+        if (bac_ep(&c)) {
+            model_t m; model_init(&m, 65);
+            for (int i = 0; i < nby * nbx; i++)
+                if (sig[i]) flat[i] = (uint8_t)(updated ? bac_bin(&c, &m, 1) : bac_ep(&c));
+        }
+    }
+    int d = nn->d, dy[32], dx[32];
+    ctx_offsets(d, dy, dx);
+    int32_t a[32], b[32];
+    memset(plane, 0, sizeof(int32_t) * (size_t)h * w);
+    for (int y = 0; y < h; y++)
+        for (int x = 0; x < w; x++) {
+            int32_t *dst = &plane[y * w + x];
+            if (blk > 0) {
+                int bi = (y >> shift) * nbx + (x >> shift);
+                if (!sig[bi]) { *dst = 0; continue; }
+                if (flat[bi]) {
+                    if (x & mask) { *dst = dst[-1]; continue; }
+                    if (y & mask) { *dst = dst[-w]; continue; }
+                }
+            }
+            for (int i = 0; i < d; i++) {
+                int yy = y + dy[i], xx = x + dx[i];
+                a[i] = (yy >= 0 && xx >= 0 && xx < w) ? plane[yy * w + xx] : 0;
+            }
+            int32_t *in = a, *out = b;
+            for (int l = 0; l < nn->nh; l++) {
+                for (int o = 0; o < d; o++) {
+                    int32_t s = nn->b_hidden[l][o] + in[o] * 256; /* residual */
+                    for (int i = 0; i < d; i++) s += in[i] * nn->w_hidden[l][o * d + i];
+                    out[o] = s < 0 ? 0 : (s + 128) >> 8;
+                }
+                int32_t *t = in; in = out; out = t;
+            }
+            int32_t p[2];
+            for (int o = 0; o < 2; o++) {
+                int32_t s = nn->b_out[o];
+                for (int i = 0; i < d; i++) s += in[i] * nn->w_out[o * d + i];
+                p[o] = s < 0 ? -((-s + 128) >> 8) : (s + 128) >> 8;
+            }
+            int mr, mi, si;
+            mu_sig_index(p[0], p[1], &mr, &mi, &si);
+            *dst = (int32_t)((uint32_t)(mr + decode_value(&c, mi, si)) << ARM_PREC);
+        }
+    free(sig);
+    free(flat);
+    return 0;
+}
+
+/* ------------------------------------------------------------------------- */
+/* Upsampling, int32.  ups_refine_cpu.hpp:11-79, ups_upsample_cpu.hpp:12-91,   */
+/* driver run_ups cc-frame-decoder.cpp:572-679                                 */
+/* ------------------------------------------------------------------------- */
+
+static inline int32_t tshift(int32_t s, int p) { return s < 0 ? -((-s) >> p) : s >> p; }
+static inline int clampi(int v, int lo, int hi) { return v < lo ? lo : v > hi ? hi : v; }
+
+/* refine: separable ks-tap filter, zero padding, + residual; in at ARM_PREC, out at UPS_PREC */
+static void ups_refine(int ks, const int32_t *kw, const int32_t *in, int h, int w, int32_t *out)
+{
+    int pad = ks / 2;
+    int32_t *tmp = (int32_t *)malloc(sizeof(int32_t) * (size_t)h * w);
+    for (int y = 0; y < h; y++)
+        for (int x = 0; x < w; x++) {
+            int32_t s = 0;
+            for (int k = 0; k < ks; k++) {
+                int xx = x - pad + k;
+                if (xx >= 0 && xx < w) s += in[y * w + xx] * kw[k];
+            }
+            tmp[y * w + x] = tshift(s, ARM_PREC);
+        }
+    for (int y = 0; y < h; y++)
+        for (int x = 0; x < w; x++) {
+            int32_t s = 0;
+            for (int k = 0; k < ks; k++) {
+                int yy = y - pad + k;
+                if (yy >= 0 && yy < h) s += tmp[yy * w + x] * kw[k];
+            }
+            s += (int32_t)((uint32_t)in[y * w + x] << (UPS_PREC - ARM_PREC) << UPS_PREC);
+            out[y * w + x] = tshift(s, UPS_PREC);
+        }
+    free(tmp);
+}
+
+/* 2x upsample: polyphase split of the ksx2-tap kernel, replicate padding. */
+static void ups_up2(int ksx2, const int32_t *kw, const int32_t *in, int h, int w, int src_prec,
+                    int32_t *out, int ho, int wo)
+{
+    int ks = ksx2 / 2, pad = ks / 2;
+    int32_t *tmp = (int32_t *)malloc(sizeof(int32_t) * (size_t)h * 2 * w);
+    for (int y = 0; y < h; y++)
+        for (int x = 0; x < w; x++) {
+            int32_t se = 0, so = 0;
+            for (int k = 0; k < ks; k++) {
+                se += in[y * w + clampi(x - pad + k, 0, w - 1)] * kw[2 * k];
+                so += in[y * w + clampi(x - pad + 1 + k, 0, w - 1)] * kw[2 * k + 1];
+            }
+            tmp[y * 2 * w + 2 * x] = tshift(se, src_prec);
+            tmp[y * 2 * w + 2 * x + 1] = tshift(so, src_prec);
+        }
+    for (int j = 0; 2 * j < ho; j++)
+        for (int x = 0; x < wo; x++) {
+            int32_t se = 0, so = 0;
+            for (int k = 0; k < ks; k++) {
+                se += tmp[clampi(j - pad + k, 0, h - 1) * 2 * w + x] * kw[2 * k];
+                so += tmp[clampi(j - pad + 1 + k, 0, h - 1) * 2 * w + x] * kw[2 * k + 1];
+            }
+            out[(2 * j) * wo + x] = tshift(se, UPS_PREC);
+            if (2 * j + 1 < ho) out[(2 * j + 1) * wo + x] = tshift(so, UPS_PREC);
+        }
+    free(tmp);
+}
+
+static void run_ups(const hdr_t *h, const nets_t *nn, cco_frame *f, const int *zero_layer)
+{
+    int L = f->n_layers;
+    size_t npx = (size_t)f->h * f->w;
+    int32_t *cur = (int32_t *)malloc(sizeof(int32_t) * npx);
+    int32_t *nxt = (int32_t *)malloc(sizeof(int32_t) * npx);
+    for (int l = 0; l < L; l++) {
+        int32_t *dst = f->syn_in + (size_t)l * npx;
+        if (zero_layer[l]) { memset(dst, 0, sizeof(int32_t) * npx); continue; }
+        int pre = (L - 2 - l) % h->n_pre;
+        if (l == 0) { ups_refine(h->pre_ks, nn->pre[pre], f->lat[0], f->lh[0], f->lw[0], dst); continue; }
+        int prec;
+        if (l == L - 1) {
+            memcpy(cur, f->lat[l], sizeof(int32_t) * (size_t)f->lh[l] * f->lw[l]);
+            prec = ARM_PREC;
+        } else {
+            ups_refine(h->pre_ks, nn->pre[pre], f->lat[l], f->lh[l], f->lw[l], cur);
+            prec = UPS_PREC;
+        }
+        for (int t = l - 1; t >= 0; t--) {
+            int ul = (L - 2 - t) % h->n_ups;
+            int32_t *o = t == 0 ? dst : nxt;
+            ups_up2(h->ups_ks, nn->ups[ul], cur, f->lh[t + 1], f->lw[t + 1], prec, o, f->lh[t], f->lw[t]);
+            if (t > 0) { int32_t *tt = cur; cur = nxt; nxt = tt; }
+            prec = UPS_PREC;
+        }
+    }
+    free(cur);
+    free(nxt);
+}
+
+/* ------------------------------------------------------------------------- */
+/* Synthesis, int32 at 12-bit fixed point.                                     */
+/* syn_cpu.hpp:21-112 (generic conv), synfused_cpu.hpp:17-109 (fused 1x1 pair),*/
+/* synlb_cpu.hpp (3x3), synblend_cpu.hpp (branch blend),                       */
+/* run_syn_branch/run_syn cc-frame-decoder.cpp:773-1149                        */
+/* ------------------------------------------------------------------------- */
+
+static inline int32_t syn_act(int32_t s, int relu)
+{
+    if (s < 0) return relu ? 0 : -((-s) >> SYN_PREC);
+    return s >> SYN_PREC;
+}
+
+/* Fused 1x1 (nin -> nhid, ReLU) + 1x1 (nhid -> nout, linear).  The reference's
+ * fused kernel ignores both layers' residual/relu flags (synfused_cpu.hpp). */
+static void syn_fused(const int32_t *w0, const int32_t *b0, const int32_t *w1, const int32_t *b1,
+                      int nin, int nhid, int nout, const int32_t *in, int32_t *out, size_t npx)
+{
+    int32_t hid[256], v[64];
+    for (size_t p = 0; p < npx; p++) {
+        for (int i = 0; i < nin; i++) v[i] = in[(size_t)i * npx + p];
+        for (int j = 0; j < nhid; j++) {
+            int32_t s = b0[j];
+            for (int i = 0; i < nin; i++) s += v[i] * w0[j * nin + i];
+            hid[j] = s < 0 ? 0 : s >> SYN_PREC;
+        }
+        for (int o = 0; o < nout; o++) {
+            int32_t s = b1[o];
+            for (int j = 0; j < nhid; j++) s += hid[j] * w1[o * nhid + j];
+            out[(size_t)o * npx + p] = syn_act(s, 0);
+        }
+    }
+}
+
+/* generic ks x ks conv, replicate padding, optional residual (out-of-place semantics) */
+static void syn_conv(const int32_t *wt, const int32_t *bias, int ks, int nin, int nout, int residual, int relu,
+                     const int32_t *in, int h, int w, int32_t *out)
+{
+    int pad = ks / 2;
+    size_t npx = (size_t)h * w;
+    for (int y = 0; y < h; y++)
+        for (int x = 0; x < w; x++)
+            for (int o = 0; o < nout; o++) {
+                int32_t s = bias[o];
+                if (residual) s += (int32_t)((uint32_t)in[(size_t)o * npx + (size_t)y * w + x] << SYN_PREC);
+                const int32_t *k = wt + (size_t)o * nin * ks * ks;
+                for (int i = 0; i < nin; i++)
+                    for (int a = 0; a < ks; a++) {
+                        int yy = clampi(y - pad + a, 0, h - 1);
+                        for (int b = 0; b < ks; b++) {
+                            int xx = clampi(x - pad + b, 0, w - 1);
+                            s += in[(size_t)i * npx + (size_t)yy * w + xx] * *k++;
+                        }
+                    }
+                out[(size_t)o * npx + (size_t)y * w + x] = syn_act(s, relu);
+            }
+}
+
+static int run_branch(const hdr_t *h, const nets_t *nn, int b, const int32_t *in, int h_, int w_,
+                      int32_t **res, int *nres)
+{
+    size_t npx = (size_t)h_ * w_;
+    int maxp = h->n_layers;
+    for (int l = 0; l < h->n_syn; l++) if (h->syn[l].n_out > maxp) maxp = h->syn[l].n_out;
+    int32_t *A = (int32_t *)malloc(sizeof(int32_t) * npx * (size_t)maxp);
+    int32_t *B = (int32_t *)malloc(sizeof(int32_t) * npx * (size_t)maxp);
+    memcpy(A, in, sizeof(int32_t) * npx * (size_t)h->n_layers);
+    int nin = h->n_layers;
+    int fuse = h->n_syn >= 2 && h->syn[0].ks == 1 && h->syn[1].ks == 1; /* can_fuse :359-365 */
+    for (int l = 0; l < h->n_syn; l++) {
+        const syn_layer_t *L = &h->syn[l];
+        if (l == 0 && fuse) {
+            if (L->n_out > 256 || nin > 64) { free(A); free(B); return 1; }
+            syn_fused(nn->syn_w[b][0], nn->syn_b[b][0], nn->syn_w[b][1], nn->syn_b[b][1],
+                      nin, L->n_out, h->syn[1].n_out, A, B, npx);
+            nin = h->syn[1].n_out;
+            l++;
+        } else {
+            if (L->residual && L->n_out > nin) { free(A); free(B); return 1; }
+            syn_conv(nn->syn_w[b][l], nn->syn_b[b][l], L->ks, nin, L->n_out, L->residual, L->relu, A, h_, w_, B);
+            nin = L->n_out;
+        }
+        int32_t *t = A; A = B; B = t;
+    }
+    free(B);
+    *res = A;
+    *nres = nin;
+    return 0;
+}
+
+static inline int32_t clamp_unit(int32_t v) { return v < 0 ? 0 : v > (1 << SYN_PREC) ? (1 << SYN_PREC) : v; }
+
+static int run_syn(const hdr_t *h, const nets_t *nn, cco_frame *f)
+{
+    size_t npx = (size_t)f->h * f->w;
+    if (h->n_branches == 1) {
+        int32_t *r; int nr;
+        if (run_branch(h, nn, 0, f->syn_in, f->h, f->w, &r, &nr)) return 1;
+        f->syn_out = r;
+        f->n_out = nr;
+        return 0;
+    }
+    /* multi-branch: out = clamp(b0)*blend0 + clamp(b1)*blend1 (blend2), then += clamp(bk)*blendk */
+    int32_t *acc = NULL;
+    for (int b = 0; b < h->n_branches; b++) {
+        int32_t *r; int nr;
+        if (run_branch(h, nn, b, f->syn_in, f->h, f->w, &r, &nr)) { free(acc); return 1; }
+        if (b == 0) { acc = r; f->n_out = nr; continue; }
+        for (size_t i = 0; i < 3 * npx; i++) {
+            int32_t x0 = clamp_unit(r[i]);
+            if (b == 1) acc[i] = (clamp_unit(acc[i]) * nn->blend[0] + x0 * nn->blend[1]) >> SYN_PREC;
+            else acc[i] = acc[i] + ((x0 * nn->blend[b]) >> SYN_PREC);
+        }
+        free(r);
+    }
+    f->syn_out = acc;
+    return 0;
+}
+
+/* ------------------------------------------------------------------------- */
+/* Frame decode and outputs                                                    */
+/* ------------------------------------------------------------------------- */
+
+int cco_decode_frame_mem(const uint8_t *bs, size_t n, cco_frame *f)
+{
+    memset(f, 0, sizeof(*f));
+    hdr_t h;
+    if (parse(bs, n, &h)) return 1;
+    if (h.intra_period != 0) return 2; /* inter (P/B) frames: out of scope */
+    nets_t *nn = (nets_t *)malloc(sizeof(nets_t));
+    if (read_nets(&h, nn)) { free_nets(nn); free(nn); return 1; }
+    f->h = h.h; f->w = h.w;
+    f->frame_data_type = h.frame_data_type;
+    f->bitdepth = h.bitdepth;
+    f->n_layers = h.n_layers;
+    int zero[CCO_MAX_LAYERS] = {0};
+    double t0 = now_s();
+    for (int l = 0, hh = h.h, ww = h.w; l < h.n_layers; l++, hh = (hh + 1) / 2, ww = (ww + 1) / 2) {
+        f->lh[l] = hh; f->lw[l] = ww;
+        f->lat[l] = (int32_t *)calloc((size_t)hh * ww, sizeof(int32_t));
+        if (h.nbytes_lat[l] == 0) { zero[l] = 1; continue; }
+        arm_decode_layer(nn, h.lat[l], (size_t)h.nbytes_lat[l], h.sig_blk, hh, ww, f->lat[l]);
+    }
+    double t1 = now_s();
+    f->syn_in = (int32_t *)malloc(sizeof(int32_t) * (size_t)h.n_layers * h.h * h.w);
+    run_ups(&h, nn, f, zero);
+    double t2 = now_s();
+    int rc = run_syn(&h, nn, f);
+    double t3 = now_s();
+    f->t_arm = t1 - t0; f->t_ups = t2 - t1; f->t_syn = t3 - t2;
+    free_nets(nn);
+    free(nn);
+    return rc;
+}
+
+void cco_frame_free(cco_frame *f)
+{
+    for (int l = 0; l < CCO_MAX_LAYERS; l++) free(f->lat[l]);
+    free(f->syn_in);
+    free(f->syn_out);
+    memset(f, 0, sizeof(*f));
+}
+
+static inline int32_t to_sample(int32_t v, int maxv)
+{
+    int32_t s = (v * maxv + (1 << (SYN_PREC - 1))) >> SYN_PREC;
+    return s < 0 ? 0 : s > maxv ? maxv : s;
+}
+
+size_t cco_output_size(const cco_frame *f, int bd, int chroma, int is_yuv)
+{
+    size_t bps = bd <= 8 ? 1 : 2;
+    size_t npx = (size_t)f->h * f->w;
+    if (is_yuv && chroma == 420) return bps * (npx + 2 * (size_t)(f->h / 2) * (f->w / 2));
+    if (is_yuv) return bps * 3 * npx;
+    char hdr[64];
+    int hl = snprintf(hdr, sizeof hdr, "P6\n%d %d\n%d\n", f->w, f->h, (1 << bd) - 1);
+    return (size_t)hl + bps * 3 * npx;
+}
+
+/* ccdecapi.cpp:59-128 (PPM), :132-240 (420 8/10-bit), get_raw_444_* (444) */
+int cco_write_output(const cco_frame *f, int bd, int chroma, int is_yuv, uint8_t *dst)
+{
+    size_t npx = (size_t)f->h * f->w;
+    const int32_t *P = f->syn_out;
+    if (f->n_out < 3) return 1;
+    if (is_yuv) {
+        if (bd != 8 && bd != 10) return 1;
+        int maxv = (1 << bd) - 1;
+        uint16_t *d16 = (uint16_t *)dst;
+        size_t k = 0;
+        for (int c = 0; c < 3; c++) {
+            int sub = chroma == 420 && c > 0;
+            int hh = sub ? f->h / 2 : f->h, ww = sub ? f->w / 2 : f->w;
+            for (int y = 0; y < hh; y++)
+                for (int x = 0; x < ww; x++) {
+                    int32_t v = P[(size_t)c * npx + (size_t)(sub ? 2 * y : y) * f->w + (sub ? 2 * x : x)];
+                    int32_t s = to_sample(v, maxv);
+                    if (bd == 8) dst[k++] = (uint8_t)s;
+                    else d16[k++] = (uint16_t)s;
+                }
+        }
+        return 0;
+    }
+    int maxv = (1 << bd) - 1;
+    int hl = sprintf((char *)dst, "P6\n%d %d\n%d\n", f->w, f->h, maxv);
+    uint8_t *q = dst + hl;
+    for (size_t p = 0; p < npx; p++)
+        for (int c = 0; c < 3; c++) {
+            int32_t s = to_sample(P[(size_t)c * npx + p], maxv);
+            if (bd <= 8) *q++ = (uint8_t)s;
+            else { *q++ = (uint8_t)(s >> 8); *q++ = (uint8_t)(s & 0xFF); }
+        }
+    return 0;
+}
+
+static int ends_with(const char *s, const char *suf)
+{
+    size_t a = strlen(s), b = strlen(suf);
+    return a >= b && strcmp(s + a - b, suf) == 0;
+}
+
+int cco_decode_file(const char *in_path, const char *out_path, int out_bd, int out_chroma, int verbosity)
+{
+    FILE *fi = fopen(in_path, "rb");
+    if (!fi) return 1;
+    fseek(fi, 0, SEEK_END);
+    long n = ftell(fi);
+    fseek(fi, 0, SEEK_SET);
+    uint8_t *buf = (uint8_t *)malloc((size_t)(n > 0 ? n : 1));
+    if (fread(buf, 1, (size_t)n, fi) != (size_t)n) { fclose(fi); free(buf); return 1; }
+    fclose(fi);
+    cco_frame f;
+    int rc = cco_decode_frame_mem(buf, (size_t)n, &f);
+    free(buf);
+    if (rc) { cco_frame_free(&f); return 1; }
+    if (out_bd == 0) out_bd = f.bitdepth;
+    if (out_chroma == 0) out_chroma = f.frame_data_type == 1 ? 420 : 444;
+    int is_yuv = out_path && ends_with(out_path, ".yuv");
+    if (verbosity >= 1)
+        printf("time: arm %g ups %g syn %g\n", f.t_arm, f.t_ups, f.t_syn);
+    if (out_path && out_path[0]) {
+        size_t sz = cco_output_size(&f, out_bd, out_chroma, is_yuv);
+        uint8_t *o = (uint8_t *)malloc(sz);
+        rc = cco_write_output(&f, out_bd, out_chroma, is_yuv, o);
+        if (!rc) {
+            FILE *fo = fopen(out_path, "wb");
+            if (!fo || fwrite(o, 1, sz, fo) != sz) rc = 1;
+            if (fo) fclose(fo);
+        }
+        free(o);
+    }
+    cco_frame_free(&f);
+    return rc ? 1 : 0;
+}
+
+#ifdef CCO_MAIN
+int main(int argc, char **argv)
+{
+    if (argc < 3) { fprintf(stderr, "usage: %s in.cool out.{yuv,ppm} [bitdepth] [chroma]\n", argv[0]); return 1; }
+    int bd = argc > 3 ? atoi(argv[3]) : 0, ch = argc > 4 ? atoi(argv[4]) : 0;
+    return cco_decode_file(argv[1], argv[2], bd, ch, 1);
+}
+#endif

@@ -1,0 +1,53 @@
+/*
+ * ccdec_oracle.h -- CPU restatement of the Cool-chic fixed-point bitstream
+ * decoder (path B).  TEST INFRASTRUCTURE ONLY: this code is the parity checker
+ * for the HIP decoder in cool-chic_amd/csrc.  Only tests/, __graft_entry__.smoke()
+ * and bench.py's cpu_baseline leg may load it.  The product never links it.
+ *
+ * Parity pinned against: the reference decoder's own outputs on the shipped
+ * .cool bitstreams (md5 lists in tests/golden/ref_md5.json, produced by the
+ * reference ccdec built from /root/reference sources by oracle/Makefile).
+ */
+#ifndef CCDEC_ORACLE_H
+#define CCDEC_ORACLE_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define CCO_MAX_LAYERS 8
+
+typedef struct cco_frame {
+    int h, w;                 /* image size */
+    int frame_data_type;      /* 0 rgb, 1 yuv420, 2 yuv444 (GOP header) */
+    int bitdepth;             /* GOP header bitdepth */
+    int n_layers;             /* latent resolutions */
+    int lh[CCO_MAX_LAYERS], lw[CCO_MAX_LAYERS];
+    int32_t *lat[CCO_MAX_LAYERS]; /* ARM-decoded latents, value << ARM_PRECISION */
+    int32_t *syn_in;          /* n_layers x h x w, upsampled, precision 12 */
+    int n_out;                /* synthesis output planes (3 for intra) */
+    int32_t *syn_out;         /* n_out x h x w, precision 12 */
+    double t_arm, t_ups, t_syn; /* seconds spent per stage */
+} cco_frame;
+
+/* Decode the intra frame of an in-memory .cool stream.  Returns 0 on success,
+ * nonzero on parse failure / unsupported stream (never exits). */
+int cco_decode_frame_mem(const uint8_t *bs, size_t n, cco_frame *out);
+void cco_frame_free(cco_frame *f);
+
+/* Output conversions, as the reference CLI writes them
+ * (ccdecapi.cpp:59-128 ppm_out, :132-180 convert_444_420_8b, 444 raw). */
+size_t cco_output_size(const cco_frame *f, int out_bitdepth, int out_chroma, int is_yuv);
+int cco_write_output(const cco_frame *f, int out_bitdepth, int out_chroma, int is_yuv, uint8_t *dst);
+
+/* File-in / file-out, same contract as the reference cc_decode_cpu
+ * (ccdecapi_cpu.cpp:20-30): 0 on success, 1 on failure. */
+int cco_decode_file(const char *in_path, const char *out_path, int out_bitdepth, int out_chroma, int verbosity);
+
+#ifdef __cplusplus
+}
+#endif
+#endif
