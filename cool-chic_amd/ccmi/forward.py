@@ -1,0 +1,176 @@
+"""Path A (float forward) launchers: torch tensors in, torch tensors out.
+
+Each function validates shapes on the host (the kernels trust them), packs the
+arguments into the C structs of include/ccmi.h and enqueues the HIP kernels on the
+current torch stream.  All tensors must already live on the GPU.
+"""
+
+from __future__ import annotations
+
+import ctypes
+from typing import Sequence
+
+import torch
+
+from . import (ArmArgs, MAX_GRIDS, MAX_SYN_LAYERS, PostArgs, SynArgs, SynLayer, UpsArgs, check, lib, ptr,
+               require_cuda, stream_handle)
+
+
+def _grid_arrays(sizes: Sequence[tuple[int, int]]):
+    if not 1 <= len(sizes) <= MAX_GRIDS:
+        raise ValueError(f"1..{MAX_GRIDS} latent grids supported, got {len(sizes)}")
+    h = (ctypes.c_int * MAX_GRIDS)()
+    w = (ctypes.c_int * MAX_GRIDS)()
+    for i, (hh, ww) in enumerate(sizes):
+        h[i], w[i] = int(hh), int(ww)
+    return h, w
+
+
+def n_latents(sizes) -> int:
+    return sum(int(h) * int(w) for h, w in sizes)
+
+
+def arm_param_count(dim_arm: int, n_hidden: int) -> int:
+    return n_hidden * (dim_arm * dim_arm + dim_arm) + 2 * dim_arm + 2
+
+
+def pack_arm(layers: Sequence[tuple[torch.Tensor, torch.Tensor]]) -> torch.Tensor:
+    """[(W [out,in], b [out]) for each mlp linear] -> flat float32 (ccmi_arm_args.params order)."""
+    return torch.cat([t.reshape(-1).float() for wb in layers for t in wb])
+
+
+def pack_ups(ups: Sequence[torch.Tensor], pre: Sequence[torch.Tensor]) -> torch.Tensor:
+    """Full (already symmetric) 1-D kernels -> flat float32 (ccmi_ups_args.params order)."""
+    return torch.cat([k.reshape(-1).float() for k in list(ups) + list(pre)])
+
+
+def pack_syn(layers: Sequence[tuple[torch.Tensor, torch.Tensor]]) -> torch.Tensor:
+    return torch.cat([t.reshape(-1).float() for wb in layers for t in wb])
+
+
+def _as_batch(params: torch.Tensor) -> torch.Tensor:
+    return params.unsqueeze(0) if params.dim() == 1 else params
+
+
+def arm_forward(latent: torch.Tensor, sizes, params: torch.Tensor, dim_arm: int, n_hidden: int,
+                gain: float = 16.0, quantize: bool = True, want=("mu", "scale", "log_scale", "rate")) -> dict:
+    """latent [B, N] (or [N]) flat grids; params [B, P] (or [P]).  Returns dict of [B, N] tensors."""
+    squeeze = latent.dim() == 1
+    latent = latent.unsqueeze(0) if squeeze else latent
+    params = _as_batch(params)
+    require_cuda(latent, params)
+    B, N = latent.shape
+    if N != n_latents(sizes):
+        raise ValueError(f"latent has {N} values, grids hold {n_latents(sizes)}")
+    if params.shape[0] != B or params.shape[1] < arm_param_count(dim_arm, n_hidden):
+        raise ValueError("arm params: expected [B, >=%d]" % arm_param_count(dim_arm, n_hidden))
+    latent = latent.float().contiguous()
+    params = params.float().contiguous()
+    outs = {k: torch.empty(B, N, device=latent.device, dtype=torch.float32) for k in want}
+    h, w = _grid_arrays(sizes)
+    a = ArmArgs(latent=ptr(latent), latent_stride=N, n_grids=len(sizes), h=h, w=w, gain=float(gain),
+                quantize=int(bool(quantize)), dim_arm=dim_arm, n_hidden=n_hidden, params=ptr(params),
+                param_stride=params.shape[1], mu=ptr(outs.get("mu")), scale=ptr(outs.get("scale")),
+                log_scale=ptr(outs.get("log_scale")), rate=ptr(outs.get("rate")), out_stride=N, batch=B)
+    check(lib().ccmi_arm_forward_f32(a, stream_handle(latent.device)))
+    if squeeze:
+        outs = {k: v[0] for k, v in outs.items()}
+    return outs
+
+
+def ups_forward(latent: torch.Tensor, sizes, params: torch.Tensor, ups_k: int, n_ups: int, pre_k: int, n_pre: int,
+                gain: float = 16.0, quantize: bool = True) -> torch.Tensor:
+    """latent [B, N] flat grids -> [B, L, H, W] dense synthesis input."""
+    squeeze = latent.dim() == 1
+    latent = latent.unsqueeze(0) if squeeze else latent
+    params = _as_batch(params)
+    require_cuda(latent, params)
+    B, N = latent.shape
+    if N != n_latents(sizes):
+        raise ValueError(f"latent has {N} values, grids hold {n_latents(sizes)}")
+    if params.shape[0] != B or params.shape[1] < n_ups * ups_k + n_pre * pre_k:
+        raise ValueError("ups params: wrong shape")
+    latent = latent.float().contiguous()
+    params = params.float().contiguous()
+    L = len(sizes)
+    H, W = sizes[0]
+    out = torch.empty(B, L, H, W, device=latent.device, dtype=torch.float32)
+    h, w = _grid_arrays(sizes)
+    nws = lib().ccmi_ups_workspace_bytes(L, h, w, B)
+    ws = torch.empty(max(nws, 4), device=latent.device, dtype=torch.uint8)
+    a = UpsArgs(latent=ptr(latent), latent_stride=N, n_grids=L, h=h, w=w, gain=float(gain),
+                quantize=int(bool(quantize)), ups_k=ups_k, n_ups=n_ups, pre_k=pre_k, n_pre=n_pre,
+                params=ptr(params), param_stride=params.shape[1], out=ptr(out), out_stride=L * H * W,
+                workspace=ptr(ws), workspace_bytes=nws, batch=B)
+    check(lib().ccmi_ups_forward_f32(a, stream_handle(latent.device)))
+    return out[0] if squeeze else out
+
+
+def _syn_args(x, layers, params, out, B, C, H, W):
+    if len(layers) > MAX_SYN_LAYERS:
+        raise ValueError("too many synthesis layers")
+    arr = (SynLayer * MAX_SYN_LAYERS)()
+    for i, (n_out, ks, res, relu) in enumerate(layers):
+        arr[i] = SynLayer(int(n_out), int(ks), int(bool(res)), int(bool(relu)))
+    return SynArgs(in_=ptr(x), in_stride=C * H * W, c_in=C, h=H, w=W, n_layers=len(layers), layers=arr,
+                   params=ptr(params), param_stride=params.shape[1], out=ptr(out),
+                   out_stride=out.shape[1] * H * W, workspace=None, workspace_bytes=0, batch=B)
+
+
+def syn_param_count(c_in: int, layers) -> int:
+    n, c = 0, c_in
+    for n_out, ks, _, _ in layers:
+        n += n_out * c * ks * ks + n_out
+        c = n_out
+    return n
+
+
+def syn_forward(x: torch.Tensor, layers, params: torch.Tensor) -> torch.Tensor:
+    """x [B, C, H, W]; layers [(n_out, ks, residual, relu)]; params [B, P] -> [B, n_out_last, H, W]."""
+    squeeze = x.dim() == 3
+    x = x.unsqueeze(0) if squeeze else x
+    params = _as_batch(params)
+    require_cuda(x, params)
+    B, Cc, H, W = x.shape
+    if params.shape[0] != B or params.shape[1] < syn_param_count(Cc, layers):
+        raise ValueError("syn params: wrong shape")
+    x = x.float().contiguous()
+    params = params.float().contiguous()
+    out = torch.empty(B, int(layers[-1][0]), H, W, device=x.device, dtype=torch.float32)
+    a = _syn_args(x, layers, params, out, B, Cc, H, W)
+    nws = lib().ccmi_syn_workspace_bytes(a)
+    ws = None
+    if nws:
+        ws = torch.empty(nws, device=x.device, dtype=torch.uint8)
+        a.workspace, a.workspace_bytes = ptr(ws), nws
+    check(lib().ccmi_syn_forward_f32(a, stream_handle(x.device)))
+    return out[0] if squeeze else out
+
+
+def post_forward(x: torch.Tensor, bitdepth: int = 8, yuv420: bool = False) -> torch.Tensor:
+    """Eval post-processing of FrameEncoder.forward.  yuv420 -> flat [B, H*W + 2*(H/2)*(W/2)]."""
+    squeeze = x.dim() == 3
+    x = x.unsqueeze(0) if squeeze else x
+    require_cuda(x)
+    B, Cc, H, W = x.shape
+    if Cc != 3:
+        raise ValueError("post-processing expects 3 channels")
+    x = x.float().contiguous()
+    n = H * W + 2 * (H // 2) * (W // 2) if yuv420 else 3 * H * W
+    out = torch.empty(B, n, device=x.device, dtype=torch.float32)
+    a = PostArgs(in_=ptr(x), in_stride=3 * H * W, h=H, w=W, bitdepth=bitdepth, yuv420=int(bool(yuv420)),
+                 out=ptr(out), out_stride=n, batch=B)
+    check(lib().ccmi_post_f32(a, stream_handle(x.device)))
+    if not yuv420:
+        out = out.view(B, 3, H, W)
+    return out[0] if squeeze else out
+
+
+def split_420(flat: torch.Tensor, H: int, W: int) -> dict:
+    """Flat 420 output of post_forward -> {'y': [..,H,W], 'u','v': [..,H/2,W/2]} views."""
+    lead = flat.shape[:-1]
+    hc, wc = H // 2, W // 2
+    y = flat[..., : H * W].reshape(*lead, H, W)
+    u = flat[..., H * W: H * W + hc * wc].reshape(*lead, hc, wc)
+    v = flat[..., H * W + hc * wc:].reshape(*lead, hc, wc)
+    return {"y": y, "u": u, "v": v}

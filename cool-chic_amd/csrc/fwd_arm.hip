@@ -1,0 +1,193 @@
+// fwd_arm.hip -- path A ARM: causal context gather + MLP + Laplace rate, float32.
+//
+// Replaces, for every latent of every grid of every frame in one launch:
+//   quantize (quantizer.py:231-232, eval = torch.round(gain * y)),
+//   _get_neighbor (arm.py:308-352: zero pad 4, 9x9 unfold, index_select of the
+//                  causal context pixels, _get_non_zero_pixel_ctx_index arm.py:373-506),
+//   Arm.forward (arm.py:227-268: residual Linear+ReLU x n_hidden, Linear -> (mu, log_scale),
+//                scale = exp(clamp(log_scale - 4, -4.6, 5))),
+//   rate (coolchic.py:419-424 with _laplace_cdf arm.py:355-370).
+//
+// Layout: one workgroup (256 threads, 4 waves) owns an 8 x 64 tile of one grid of one
+// frame.  The quantised tile plus its causal halo (4 rows above, 4 columns either
+// side) is staged once in LDS; each thread evaluates the MLP for NL = 2 latents of the
+// same column, so every weight (wave-uniform, held in SGPRs via scalar loads) feeds two
+// FMAs.  LDS reads are lane-consecutive (conflict-free).  Grids of all resolutions
+// share one launch through a tile prefix table (no per-grid launches).
+#include "ccmi_internal.h"
+
+namespace {
+
+constexpr int kThreads = 256;
+constexpr int kTX = 64;
+constexpr int kRowsPerPass = kThreads / kTX; // 4
+constexpr int kNL = 2;                        // latents per thread
+constexpr int kTY = kRowsPerPass * kNL;       // 8
+constexpr int kHalo = 4;
+constexpr int kLW = kTX + 2 * kHalo;          // 72
+constexpr int kLH = kTY + kHalo;              // 12
+
+struct ArmGeom {
+    int n;
+    int h[CCMI_MAX_GRIDS], w[CCMI_MAX_GRIDS], off[CCMI_MAX_GRIDS];
+    int tiles_x[CCMI_MAX_GRIDS];
+    int tile_start[CCMI_MAX_GRIDS + 1];
+};
+
+// Context pixel offsets (dy, dx) in the reference's gather order: flattened 9x9
+// mask index k -> (k / 9 - 4, k % 9 - 4) for the indices of arm.py:373-506.
+template <int D>
+__device__ __forceinline__ void ctx_offset(int i, int &dy, int &dx)
+{
+    // clang-format off
+    constexpr signed char k8[8] = {13, 22, 30, 31, 32, 37, 38, 39};
+    constexpr signed char k16[16] = {13, 14, 20, 21, 22, 23, 24, 28, 29, 30, 31, 32, 33, 37, 38, 39};
+    constexpr signed char k24[24] = {4, 11, 12, 13, 14, 15, 19, 20, 21, 22, 23, 24, 25, 28, 29, 30, 31, 32, 33, 34,
+                                     36, 37, 38, 39};
+    constexpr signed char k32[32] = {2, 3, 4, 5, 10, 11, 12, 13, 14, 15, 16, 19, 20, 21, 22, 23, 24, 25, 26, 27,
+                                     28, 29, 30, 31, 32, 33, 34, 35, 36, 37, 38, 39};
+    // clang-format on
+    int k = D == 8 ? k8[i] : D == 16 ? k16[i] : D == 24 ? k24[i] : k32[i];
+    dy = k / 9 - 4;
+    dx = k % 9 - 4;
+}
+
+__device__ __forceinline__ float laplace_cdf(float x, float mu, float scale)
+{
+    float s = x - mu;
+    float sg = s > 0.f ? 1.f : (s < 0.f ? -1.f : 0.f);
+    return 0.5f - 0.5f * sg * expm1f(-fabsf(s) / scale);
+}
+
+template <int D>
+__global__ __launch_bounds__(kThreads) void arm_fwd_kernel(
+    const float *__restrict__ lat, int64_t lat_stride, ArmGeom g, float gain, int quantize, int nh,
+    const float *__restrict__ params, int64_t pstride, float *__restrict__ o_mu, float *__restrict__ o_scale,
+    float *__restrict__ o_log_scale, float *__restrict__ o_rate, int64_t ostride)
+{
+    __shared__ float tile[kLH][kLW];
+
+    const int b = blockIdx.y;
+    const int t = blockIdx.x;
+    int l = 0;
+#pragma unroll
+    for (int k = 1; k < CCMI_MAX_GRIDS; ++k)
+        if (k < g.n && t >= g.tile_start[k]) l = k;
+    const int lt = t - g.tile_start[l];
+    const int H = g.h[l], W = g.w[l];
+    const int y0 = (lt / g.tiles_x[l]) * kTY;
+    const int x0 = (lt % g.tiles_x[l]) * kTX;
+    const float *src = lat + (int64_t)b * lat_stride + g.off[l];
+
+    for (int i = threadIdx.x; i < kLH * kLW; i += kThreads) {
+        const int r = i / kLW, c = i - r * kLW;
+        const int y = y0 - kHalo + r, x = x0 - kHalo + c;
+        float v = 0.f;
+        if (y >= 0 && y < H && x >= 0 && x < W) {
+            v = src[y * W + x];
+            if (quantize) v = rintf(gain * v);
+        }
+        tile[r][c] = v;
+    }
+    __syncthreads();
+
+    const float *p = params + (int64_t)b * pstride;
+    const int cx = threadIdx.x % kTX;
+    const int cy0 = threadIdx.x / kTX;
+
+    float a[kNL][D];
+#pragma unroll
+    for (int n = 0; n < kNL; ++n) {
+        const int cy = cy0 + n * kRowsPerPass;
+#pragma unroll
+        for (int i = 0; i < D; ++i) {
+            int dy, dx;
+            ctx_offset<D>(i, dy, dx);
+            a[n][i] = tile[cy + kHalo + dy][cx + kHalo + dx];
+        }
+    }
+
+    for (int layer = 0; layer < nh; ++layer) {
+        const float *Wl = p + layer * (D * D + D);
+        const float *bl = Wl + D * D;
+        float o[kNL][D];
+#pragma unroll
+        for (int j = 0; j < D; ++j) {
+            const float bj = bl[j];
+#pragma unroll
+            for (int n = 0; n < kNL; ++n) {
+                float acc = 0.f;
+#pragma unroll
+                for (int i = 0; i < D; ++i) acc = fmaf(Wl[j * D + i], a[n][i], acc);
+                o[n][j] = fmaxf((acc + bj) + a[n][j], 0.f); // F.linear(x) + x, then ReLU
+            }
+        }
+#pragma unroll
+        for (int n = 0; n < kNL; ++n)
+#pragma unroll
+            for (int j = 0; j < D; ++j) a[n][j] = o[n][j];
+    }
+
+    const float *Wo = p + nh * (D * D + D);
+    const float b_mu = Wo[2 * D], b_ls = Wo[2 * D + 1];
+#pragma unroll
+    for (int n = 0; n < kNL; ++n) {
+        const int y = y0 + cy0 + n * kRowsPerPass, x = x0 + cx;
+        float m = 0.f, ls = 0.f;
+#pragma unroll
+        for (int i = 0; i < D; ++i) {
+            m = fmaf(Wo[i], a[n][i], m);
+            ls = fmaf(Wo[D + i], a[n][i], ls);
+        }
+        m += b_mu;
+        ls += b_ls;
+        if (y < H && x < W) {
+            const float sc = expf(fminf(fmaxf(ls - 4.f, -4.6f), 5.0f));
+            const float q = tile[cy0 + n * kRowsPerPass + kHalo][cx + kHalo];
+            const int64_t idx = (int64_t)b * ostride + g.off[l] + y * W + x;
+            if (o_mu) o_mu[idx] = m;
+            if (o_scale) o_scale[idx] = sc;
+            if (o_log_scale) o_log_scale[idx] = ls;
+            if (o_rate) {
+                const float pr = fmaxf(laplace_cdf(q + 0.5f, m, sc) - laplace_cdf(q - 0.5f, m, sc), 1.52587890625e-05f);
+                o_rate[idx] = -log2f(pr);
+            }
+        }
+    }
+}
+
+} // namespace
+
+int ccmi_launch_arm_f32(const ccmi_arm_args *a, hipStream_t s)
+{
+    ArmGeom g{};
+    g.n = a->n_grids;
+    int off = 0, tiles = 0;
+    for (int l = 0; l < a->n_grids; ++l) {
+        g.h[l] = a->h[l];
+        g.w[l] = a->w[l];
+        g.off[l] = off;
+        g.tiles_x[l] = ccmi_div_up(a->w[l], kTX);
+        g.tile_start[l] = tiles;
+        tiles += g.tiles_x[l] * ccmi_div_up(a->h[l], kTY);
+        off += a->h[l] * a->w[l];
+    }
+    g.tile_start[a->n_grids] = tiles;
+    if (a->latent_stride < off || (a->out_stride < off))
+        return ccmi_set_error(CCMI_ERR_ARG, "arm: stride smaller than the %d latents of a frame", off);
+    dim3 grid(tiles, a->batch);
+#define CCMI_ARM_LAUNCH(DD)                                                                                     \
+    hipLaunchKernelGGL(arm_fwd_kernel<DD>, grid, dim3(kThreads), 0, s, a->latent, a->latent_stride, g, a->gain, \
+                       a->quantize, a->n_hidden, a->params, a->param_stride, a->mu, a->scale, a->log_scale,     \
+                       a->rate, a->out_stride)
+    switch (a->dim_arm) {
+    case 8: CCMI_ARM_LAUNCH(8); break;
+    case 16: CCMI_ARM_LAUNCH(16); break;
+    case 24: CCMI_ARM_LAUNCH(24); break;
+    case 32: CCMI_ARM_LAUNCH(32); break;
+    default: return ccmi_set_error(CCMI_ERR_UNSUPPORTED, "arm: dim_arm must be 8, 16, 24 or 32 (got %d)", a->dim_arm);
+    }
+#undef CCMI_ARM_LAUNCH
+    CCMI_HIP_CHECK(hipGetLastError());
+    return CCMI_OK;
+}

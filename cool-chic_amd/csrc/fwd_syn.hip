@@ -1,0 +1,402 @@
+// fwd_syn.hip -- path A synthesis (Synthesis.forward), float32, plus frame post-processing.
+//
+// Reference: coolchic/enc/component/core/synthesis.py
+//   SynthesisConv2d.forward :69-84  -- replicate pad (ks-1)/2, conv2d + bias, (+ x if residual)
+//   Synthesis.forward      :264-277 -- layers in sequence, ReLU / identity after each.
+// Post-processing: FrameEncoder.forward eval branch, coolchic/enc/component/frame.py:175-183,
+//   convert_444_to_420 coolchic/enc/io/format/yuv.py:275-299 (nearest = even rows / cols).
+//
+// Fast path (every architecture made of a 1x1 "MLP" head followed by 3x3 layers with
+// <= 4 channels -- all the reference presets: hop, mop, lop, ...): ONE fused kernel per
+// launch.  A workgroup owns a 16 x 64 output tile.  Pass 0 evaluates the per-pixel MLP
+// (c_in -> hid -> c_mid, weights wave-uniform in SGPRs) on the tile plus a halo of one
+// pixel per 3x3 layer, and keeps its c_mid outputs in LDS; each 3x3 layer then shrinks
+// the region by one pixel, ping-ponging between two LDS images; the last layer writes
+// to HBM.  Replicate padding is reproduced by evaluating halo pixels at the clamped
+// image coordinate (a pointwise head commutes with clamping; a 3x3 layer reads its
+// input at clamp(clamp(g) + d)).  HBM traffic: c_in planes read once (+ halo), c_out
+// planes written once.
+//
+// Any other architecture runs the generic per-layer kernel (one launch per layer,
+// ping-pong through the caller's workspace).
+#include "ccmi_internal.h"
+
+namespace {
+
+constexpr int kThreads = 256;
+constexpr int kTY = 16, kTX = 64;
+constexpr int kMaxIn = 8;   // fused path: max synthesis input channels
+constexpr int kMaxMid = 4;  // fused path: max channels through the 3x3 layers
+constexpr int kMaxSp = 3;   // fused path: max number of 3x3 layers
+
+struct SpLayer {
+    int w_off, b_off; // offsets in the frame's parameter block
+    int residual, relu;
+};
+
+struct FusedArgs {
+    const float *in;
+    int64_t in_stride;
+    int cin, H, W;
+    int n_head;          // 1 or 2 1x1 layers
+    int w0_off, b0_off, relu0;
+    int w1_off, b1_off, relu1;
+    int n_sp;            // 3x3 layers after the head
+    SpLayer sp[kMaxSp];
+    const float *params;
+    int64_t pstride;
+    float *out;
+    int64_t out_stride;
+    int tiles_x;
+};
+
+__device__ __forceinline__ int clampi(int v, int hi) { return v < 0 ? 0 : (v > hi ? hi : v); }
+
+// HID: hidden width of a 2-layer head (0 for a 1-layer head c_in -> CMID).
+template <int HID, int CMID>
+__global__ __launch_bounds__(kThreads) void syn_fused_kernel(FusedArgs A)
+{
+    constexpr int kMaxRegion = (kTY + 2 * kMaxSp) * (kTX + 2 * kMaxSp);
+    __shared__ float s_buf[2][CMID][kMaxRegion];
+
+    const int b = blockIdx.y;
+    const int y0 = (blockIdx.x / A.tiles_x) * kTY;
+    const int x0 = (blockIdx.x % A.tiles_x) * kTX;
+    const float *prm = A.params + (int64_t)b * A.pstride;
+    const float *in = A.in + (int64_t)b * A.in_stride;
+    float *out = A.out + (int64_t)b * A.out_stride;
+    const int64_t plane = (int64_t)A.H * A.W;
+    const int halo = A.n_sp;
+
+    // ------------------------ pass 0: per-pixel 1x1 head ------------------------
+    {
+        const int rh = kTY + 2 * halo, rw = kTX + 2 * halo;
+        const float *w0 = prm + A.w0_off, *b0 = prm + A.b0_off;
+        const float *w1 = prm + A.w1_off, *b1 = prm + A.b1_off;
+        for (int i = threadIdx.x; i < rh * rw; i += kThreads) {
+            const int r = i / rw, c = i - r * rw;
+            const int gy = y0 - halo + r, gx = x0 - halo + c;
+            if (halo == 0 && (gy >= A.H || gx >= A.W)) continue;
+            const int64_t pix = (int64_t)clampi(gy, A.H - 1) * A.W + clampi(gx, A.W - 1);
+            float x[kMaxIn];
+#pragma unroll
+            for (int k = 0; k < kMaxIn; ++k) x[k] = k < A.cin ? in[k * plane + pix] : 0.f;
+            float o[CMID];
+            if constexpr (HID > 0) {
+                float hdn[HID];
+#pragma unroll
+                for (int j = 0; j < HID; ++j) {
+                    float acc = 0.f;
+#pragma unroll
+                    for (int k = 0; k < kMaxIn; ++k)
+                        if (k < A.cin) acc = fmaf(w0[j * A.cin + k], x[k], acc);
+                    acc += b0[j];
+                    hdn[j] = A.relu0 ? fmaxf(acc, 0.f) : acc;
+                }
+#pragma unroll
+                for (int m = 0; m < CMID; ++m) {
+                    float acc = 0.f;
+#pragma unroll
+                    for (int j = 0; j < HID; ++j) acc = fmaf(w1[m * HID + j], hdn[j], acc);
+                    acc += b1[m];
+                    o[m] = A.relu1 ? fmaxf(acc, 0.f) : acc;
+                }
+            } else {
+#pragma unroll
+                for (int m = 0; m < CMID; ++m) {
+                    float acc = 0.f;
+#pragma unroll
+                    for (int k = 0; k < kMaxIn; ++k)
+                        if (k < A.cin) acc = fmaf(w0[m * A.cin + k], x[k], acc);
+                    acc += b0[m];
+                    o[m] = A.relu0 ? fmaxf(acc, 0.f) : acc;
+                }
+            }
+            if (halo == 0) {
+#pragma unroll
+                for (int m = 0; m < CMID; ++m) out[m * plane + pix] = o[m];
+            } else {
+#pragma unroll
+                for (int m = 0; m < CMID; ++m) s_buf[0][m][i] = o[m];
+            }
+        }
+    }
+    if (halo == 0) return;
+
+    // ------------------------ 3x3 layers, replicate padding ------------------------
+    int cur = 0;
+    for (int s = 0; s < A.n_sp; ++s) {
+        __syncthreads();
+        const int hin = halo - s;          // halo of the input image of this layer
+        const int hout = hin - 1;          // halo of its output
+        const int iw = kTX + 2 * hin;
+        const int oh = kTY + 2 * hout, ow = kTX + 2 * hout;
+        const int oy = y0 - hin, ox = x0 - hin; // global coords of input-image (0,0)
+        const float *wt = prm + A.sp[s].w_off;
+        const float *bs = prm + A.sp[s].b_off;
+        const bool last = s == A.n_sp - 1;
+        for (int i = threadIdx.x; i < oh * ow; i += kThreads) {
+            const int r = i / ow, c = i - r * ow;
+            const int gy = y0 - hout + r, gx = x0 - hout + c;
+            if (last && (gy >= A.H || gx >= A.W)) continue;
+            const int cy = clampi(gy, A.H - 1), cx = clampi(gx, A.W - 1);
+            int ry[3], rx[3];
+#pragma unroll
+            for (int d = 0; d < 3; ++d) {
+                ry[d] = clampi(cy + d - 1, A.H - 1) - oy;
+                rx[d] = clampi(cx + d - 1, A.W - 1) - ox;
+            }
+            float acc[CMID];
+#pragma unroll
+            for (int m = 0; m < CMID; ++m) acc[m] = 0.f;
+#pragma unroll
+            for (int k = 0; k < CMID; ++k)
+#pragma unroll
+                for (int dy = 0; dy < 3; ++dy)
+#pragma unroll
+                    for (int dx = 0; dx < 3; ++dx) {
+                        const float v = s_buf[cur][k][ry[dy] * iw + rx[dx]];
+#pragma unroll
+                        for (int m = 0; m < CMID; ++m) acc[m] = fmaf(wt[((m * CMID + k) * 3 + dy) * 3 + dx], v, acc[m]);
+                    }
+#pragma unroll
+            for (int m = 0; m < CMID; ++m) {
+                float v = acc[m] + bs[m];
+                if (A.sp[s].residual) v += s_buf[cur][m][(cy - oy) * iw + (cx - ox)];
+                if (A.sp[s].relu) v = fmaxf(v, 0.f);
+                if (last)
+                    out[m * plane + (int64_t)gy * A.W + gx] = v;
+                else
+                    s_buf[cur ^ 1][m][i] = v;
+            }
+        }
+        cur ^= 1;
+    }
+}
+
+// Generic layer: any ks (odd), any channel counts; replicate padding.
+__global__ __launch_bounds__(kThreads) void syn_layer_kernel(const float *__restrict__ in, int64_t in_stride, int cin,
+                                                             int H, int W, const float *__restrict__ params,
+                                                             int64_t pstride, int w_off, int b_off, int nout, int ks,
+                                                             int residual, int relu, float *__restrict__ out,
+                                                             int64_t out_stride)
+{
+    const int b = blockIdx.y;
+    const int64_t plane = (int64_t)H * W;
+    const int64_t p = (int64_t)blockIdx.x * kThreads + threadIdx.x;
+    if (p >= plane) return;
+    const int y = (int)(p / W), x = (int)(p - (int64_t)y * W);
+    const float *src = in + (int64_t)b * in_stride;
+    float *dst = out + (int64_t)b * out_stride;
+    const float *wt = params + (int64_t)b * pstride + w_off;
+    const float *bs = params + (int64_t)b * pstride + b_off;
+    const int pad = ks / 2;
+    for (int m = 0; m < nout; ++m) {
+        float acc = 0.f;
+        for (int k = 0; k < cin; ++k)
+            for (int dy = 0; dy < ks; ++dy) {
+                const int yy = clampi(y + dy - pad, H - 1);
+                for (int dx = 0; dx < ks; ++dx) {
+                    const int xx = clampi(x + dx - pad, W - 1);
+                    acc = fmaf(wt[((m * cin + k) * ks + dy) * ks + dx], src[k * plane + (int64_t)yy * W + xx], acc);
+                }
+            }
+        float v = acc + bs[m];
+        if (residual) v += src[m * plane + p];
+        if (relu) v = fmaxf(v, 0.f);
+        dst[m * plane + p] = v;
+    }
+}
+
+__global__ __launch_bounds__(kThreads) void post_kernel(const float *__restrict__ in, int64_t in_stride, int H, int W,
+                                                        float qmax, int yuv420, float *__restrict__ out,
+                                                        int64_t out_stride)
+{
+    const int b = blockIdx.y;
+    const int64_t plane = (int64_t)H * W;
+    const int64_t p = (int64_t)blockIdx.x * kThreads + threadIdx.x;
+    if (p >= plane) return;
+    const float *src = in + (int64_t)b * in_stride;
+    float *dst = out + (int64_t)b * out_stride;
+    auto q = [qmax](float v) { return fminf(fmaxf(rintf(v * qmax) / qmax, 0.f), 1.f); };
+    dst[p] = q(src[p]);
+    const int y = (int)(p / W), x = (int)(p - (int64_t)y * W);
+    if (!yuv420) {
+        dst[plane + p] = q(src[plane + p]);
+        dst[2 * plane + p] = q(src[2 * plane + p]);
+    } else if (!(y & 1) && !(x & 1) && y / 2 < H / 2 && x / 2 < W / 2) {
+        const int64_t cp = (int64_t)(H / 2) * (W / 2);
+        const int64_t ci = (int64_t)(y / 2) * (W / 2) + x / 2;
+        dst[plane + ci] = q(src[plane + p]);
+        dst[plane + cp + ci] = q(src[2 * plane + p]);
+    }
+}
+
+struct Plan {
+    bool fused;
+    int hid, cmid;
+    FusedArgs fa;
+};
+
+// Offsets of each layer's weights / biases in a frame's parameter block.
+void layer_offsets(const ccmi_syn_args *a, int *w_off, int *b_off, int *cin_of, int64_t *total)
+{
+    int64_t o = 0;
+    int c = a->c_in;
+    for (int l = 0; l < a->n_layers; ++l) {
+        const ccmi_syn_layer &L = a->layers[l];
+        cin_of[l] = c;
+        w_off[l] = (int)o;
+        o += (int64_t)L.n_out * c * L.ks * L.ks;
+        b_off[l] = (int)o;
+        o += L.n_out;
+        c = L.n_out;
+    }
+    *total = o;
+}
+
+bool make_plan(const ccmi_syn_args *a, Plan *P)
+{
+    int w_off[CCMI_MAX_SYN_LAYERS], b_off[CCMI_MAX_SYN_LAYERS], cin_of[CCMI_MAX_SYN_LAYERS];
+    int64_t tot;
+    layer_offsets(a, w_off, b_off, cin_of, &tot);
+    P->fused = false;
+    const ccmi_syn_layer *L = a->layers;
+    int n_head = 0;
+    while (n_head < a->n_layers && n_head < 2 && L[n_head].ks == 1 && !L[n_head].residual) n_head++;
+    if (n_head == 0 || a->c_in > kMaxIn) return false;
+    const int cmid = L[n_head - 1].n_out;
+    if (cmid < 1 || cmid > kMaxMid) return false;
+    int hid = n_head == 2 ? L[0].n_out : 0;
+    if (n_head == 2 && hid != 8 && hid != 12 && hid != 16 && hid != 24 && hid != 32 && hid != 40 && hid != 48 &&
+        hid != 64)
+        return false;
+    const int n_sp = a->n_layers - n_head;
+    if (n_sp > kMaxSp) return false;
+    for (int l = n_head; l < a->n_layers; ++l)
+        if (L[l].ks != 3 || L[l].n_out != cmid) return false;
+    if (cmid != 3 && !(cmid == 4 && hid == 0)) return false; // instantiated shapes
+    FusedArgs &f = P->fa;
+    f = FusedArgs{};
+    f.cin = a->c_in;
+    f.H = a->h;
+    f.W = a->w;
+    f.n_head = n_head;
+    f.w0_off = w_off[0];
+    f.b0_off = b_off[0];
+    f.relu0 = L[0].relu;
+    if (n_head == 2) {
+        f.w1_off = w_off[1];
+        f.b1_off = b_off[1];
+        f.relu1 = L[1].relu;
+    }
+    f.n_sp = n_sp;
+    for (int s = 0; s < n_sp; ++s) {
+        f.sp[s].w_off = w_off[n_head + s];
+        f.sp[s].b_off = b_off[n_head + s];
+        f.sp[s].residual = L[n_head + s].residual;
+        f.sp[s].relu = L[n_head + s].relu;
+    }
+    P->fused = true;
+    P->hid = hid;
+    P->cmid = cmid;
+    return true;
+}
+
+template <int HID>
+void launch_fused_hid(dim3 grid, hipStream_t s, const FusedArgs &fa, int cmid)
+{
+    if (cmid == 3) hipLaunchKernelGGL((syn_fused_kernel<HID, 3>), grid, dim3(kThreads), 0, s, fa);
+}
+
+} // namespace
+
+extern "C" size_t ccmi_syn_workspace_bytes(const ccmi_syn_args *a)
+{
+    Plan P;
+    if (make_plan(a, &P)) return 0;
+    int maxc = a->c_in;
+    for (int l = 0; l < a->n_layers; ++l) maxc = a->layers[l].n_out > maxc ? a->layers[l].n_out : maxc;
+    return 2 * sizeof(float) * (size_t)maxc * a->h * a->w * (size_t)(a->batch > 0 ? a->batch : 0);
+}
+
+int ccmi_launch_syn_f32(const ccmi_syn_args *a, hipStream_t s)
+{
+    if (a->n_layers < 1 || a->n_layers > CCMI_MAX_SYN_LAYERS)
+        return ccmi_set_error(CCMI_ERR_ARG, "syn: n_layers must be in [1, %d]", CCMI_MAX_SYN_LAYERS);
+    int c = a->c_in;
+    for (int l = 0; l < a->n_layers; ++l) {
+        const ccmi_syn_layer &L = a->layers[l];
+        if (L.n_out < 1 || L.ks < 1 || L.ks % 2 == 0)
+            return ccmi_set_error(CCMI_ERR_ARG, "syn: layer %d has n_out=%d ks=%d (ks must be odd)", l, L.n_out, L.ks);
+        if (L.residual && L.n_out != c)
+            return ccmi_set_error(CCMI_ERR_ARG, "syn: residual layer %d needs n_out == n_in", l);
+        c = L.n_out;
+    }
+    Plan P;
+    if (make_plan(a, &P)) {
+        P.fa.in = a->in;
+        P.fa.in_stride = a->in_stride;
+        P.fa.params = a->params;
+        P.fa.pstride = a->param_stride;
+        P.fa.out = a->out;
+        P.fa.out_stride = a->out_stride;
+        P.fa.tiles_x = ccmi_div_up(a->w, kTX);
+        dim3 grid(P.fa.tiles_x * ccmi_div_up(a->h, kTY), a->batch);
+        switch (P.hid) {
+        case 0:
+            if (P.cmid == 3) hipLaunchKernelGGL((syn_fused_kernel<0, 3>), grid, dim3(kThreads), 0, s, P.fa);
+            else hipLaunchKernelGGL((syn_fused_kernel<0, 4>), grid, dim3(kThreads), 0, s, P.fa);
+            break;
+        case 8: launch_fused_hid<8>(grid, s, P.fa, P.cmid); break;
+        case 12: launch_fused_hid<12>(grid, s, P.fa, P.cmid); break;
+        case 16: launch_fused_hid<16>(grid, s, P.fa, P.cmid); break;
+        case 24: launch_fused_hid<24>(grid, s, P.fa, P.cmid); break;
+        case 32: launch_fused_hid<32>(grid, s, P.fa, P.cmid); break;
+        case 40: launch_fused_hid<40>(grid, s, P.fa, P.cmid); break;
+        case 48: launch_fused_hid<48>(grid, s, P.fa, P.cmid); break;
+        case 64: launch_fused_hid<64>(grid, s, P.fa, P.cmid); break;
+        }
+        CCMI_HIP_CHECK(hipGetLastError());
+        return CCMI_OK;
+    }
+    // generic path
+    const size_t need = ccmi_syn_workspace_bytes(a);
+    if (a->workspace == nullptr || a->workspace_bytes < need)
+        return ccmi_set_error(CCMI_ERR_ARG, "syn: workspace of %zu bytes needed for this architecture", need);
+    int w_off[CCMI_MAX_SYN_LAYERS], b_off[CCMI_MAX_SYN_LAYERS], cin_of[CCMI_MAX_SYN_LAYERS];
+    int64_t tot;
+    layer_offsets(a, w_off, b_off, cin_of, &tot);
+    int maxc = a->c_in;
+    for (int l = 0; l < a->n_layers; ++l) maxc = a->layers[l].n_out > maxc ? a->layers[l].n_out : maxc;
+    const int64_t buf_stride = (int64_t)maxc * a->h * a->w;
+    float *bufs[2] = {static_cast<float *>(a->workspace), static_cast<float *>(a->workspace) + buf_stride * a->batch};
+    const float *src = a->in;
+    int64_t src_stride = a->in_stride;
+    const int64_t plane = (int64_t)a->h * a->w;
+    dim3 grid((unsigned)((plane + kThreads - 1) / kThreads), a->batch);
+    for (int l = 0; l < a->n_layers; ++l) {
+        const bool last = l == a->n_layers - 1;
+        float *dst = last ? a->out : bufs[l & 1];
+        const int64_t dst_stride = last ? a->out_stride : buf_stride;
+        const ccmi_syn_layer &L = a->layers[l];
+        hipLaunchKernelGGL(syn_layer_kernel, grid, dim3(kThreads), 0, s, src, src_stride, cin_of[l], a->h, a->w,
+                           a->params, a->param_stride, w_off[l], b_off[l], L.n_out, L.ks, L.residual, L.relu, dst,
+                           dst_stride);
+        CCMI_HIP_CHECK(hipGetLastError());
+        src = dst;
+        src_stride = dst_stride;
+    }
+    return CCMI_OK;
+}
+
+int ccmi_launch_post_f32(const ccmi_post_args *a, hipStream_t s)
+{
+    if (a->bitdepth < 1 || a->bitdepth > 16) return ccmi_set_error(CCMI_ERR_ARG, "post: bitdepth %d", a->bitdepth);
+    const int64_t plane = (int64_t)a->h * a->w;
+    dim3 grid((unsigned)((plane + kThreads - 1) / kThreads), a->batch);
+    hipLaunchKernelGGL(post_kernel, grid, dim3(kThreads), 0, s, a->in, a->in_stride, a->h, a->w,
+                       (float)((1 << a->bitdepth) - 1), a->yuv420, a->out, a->out_stride);
+    CCMI_HIP_CHECK(hipGetLastError());
+    return CCMI_OK;
+}

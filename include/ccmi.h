@@ -1,0 +1,176 @@
+/*
+ * ccmi.h -- C ABI of libccmi, the MI355X (gfx950) implementation of Cool-chic's
+ * per-image decode / forward hot path.
+ *
+ * Every entry point takes plain pointers and sizes (no C++ or torch types), is
+ * reentrant (no globals; per-call state only) and never calls exit(): errors are
+ * returned as a CCMI_ERR_* code with a message in ccmi_last_error() (thread-local).
+ * Device pointers are caller-owned; kernels are enqueued on the caller's stream
+ * (a hipStream_t passed as void*, e.g. torch.cuda.current_stream().cuda_stream).
+ *
+ * Two forms of the hot path, mirroring the reference:
+ *   A. float forward  (coolchic/enc/component/coolchic.py:291-479): ARM probability
+ *      model + rate, upsampling, synthesis, frame post-processing;
+ *   B. fixed-point .cool bitstream decoder (coolchic/cpp/): CABAC + integer ARM,
+ *      integer upsampling, integer synthesis, bit-exact with the reference C decoder.
+ */
+#ifndef CCMI_H
+#define CCMI_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define CCMI_OK 0
+#define CCMI_ERR_ARG 1         /* invalid argument / shape */
+#define CCMI_ERR_HIP 2         /* HIP runtime error (no device, launch failure, ...) */
+#define CCMI_ERR_UNSUPPORTED 3 /* architecture or stream feature not implemented */
+#define CCMI_ERR_BITSTREAM 4   /* malformed .cool bitstream */
+#define CCMI_ERR_IO 5          /* file open / read / write failure */
+
+#define CCMI_MAX_GRIDS_PUBLIC 8
+#define CCMI_MAX_SYN_LAYERS 16
+
+/* Thread-local message for the last failing call on this thread. */
+const char *ccmi_last_error(void);
+/* ABI version (major*100 + minor). */
+int ccmi_version(void);
+/* Number of visible HIP devices (0 when none; never fails). */
+int ccmi_device_count(void);
+
+/* ------------------------------------------------------------------------- */
+/* Path A: float forward, batched over independent frames of the same size and */
+/* architecture.  Each frame has its own parameters (Cool-chic overfits one     */
+/* network per image).  Latents of one frame are the flat concatenation of its  */
+/* grids, grid l being h[l] x w[l] (coolchic.py:360-363).                        */
+/* ------------------------------------------------------------------------- */
+
+/* ARM: causal context gather + MLP + Laplace rate for every latent.
+ * Replaces _get_neighbor (arm.py:308-352), Arm.forward (arm.py:227-268) and the
+ * rate of CoolChicEncoder.forward (coolchic.py:395-424).
+ * params per frame, float32: for each hidden layer l < n_hidden: W_l [d][d] (out,in)
+ * then b_l [d]; then W_out [2][d], b_out [2]  (= arm.mlp state_dict order). */
+typedef struct ccmi_arm_args {
+    const float *latent;    /* [batch][latent_stride], N = sum h[l]*w[l] used */
+    int64_t latent_stride;
+    int n_grids;
+    int h[CCMI_MAX_GRIDS_PUBLIC];
+    int w[CCMI_MAX_GRIDS_PUBLIC];
+    float gain;             /* encoder gain (coolchic.py:91) */
+    int quantize;           /* 1: y = round(gain * latent) (eval quantizer); 0: latent used as is */
+    int dim_arm;            /* 8, 16, 24 or 32 */
+    int n_hidden;           /* 0..4 */
+    const float *params;
+    int64_t param_stride;
+    float *mu;              /* optional outputs [batch][out_stride] (NULL to skip) */
+    float *scale;
+    float *log_scale;
+    float *rate;            /* bits per latent, optional */
+    int64_t out_stride;
+    int batch;
+} ccmi_arm_args;
+int ccmi_arm_forward_f32(const ccmi_arm_args *args, void *stream);
+
+/* Upsampling: Upsampling.forward in eval mode (upsampling.py:476-506, separable
+ * paths :205-209 and :337-353).  params per frame, float32: n_ups kernels of ups_k
+ * taps (full symmetric kernels, conv_transpose2ds[i]), then n_pre kernels of
+ * pre_k taps (conv2ds[i]).  out: [batch][n_grids][H][W] with H,W = h[0],w[0]. */
+typedef struct ccmi_ups_args {
+    const float *latent;
+    int64_t latent_stride;
+    int n_grids;
+    int h[CCMI_MAX_GRIDS_PUBLIC];
+    int w[CCMI_MAX_GRIDS_PUBLIC];
+    float gain;
+    int quantize;
+    int ups_k;              /* even, >= 4 */
+    int n_ups;
+    int pre_k;              /* odd */
+    int n_pre;
+    const float *params;
+    int64_t param_stride;
+    float *out;
+    int64_t out_stride;
+    void *workspace;        /* device scratch of ccmi_ups_workspace_bytes() */
+    size_t workspace_bytes;
+    int batch;
+} ccmi_ups_args;
+size_t ccmi_ups_workspace_bytes(int n_grids, const int *h, const int *w, int batch);
+int ccmi_ups_forward_f32(const ccmi_ups_args *args, void *stream);
+
+/* Synthesis: Synthesis.forward (synthesis.py:264-277, SynthesisConv2d :69-84):
+ * conv layers with replicate padding, optional residual, optional ReLU.
+ * params per frame, float32, per layer: W [n_out][c_in][ks][ks] then b [n_out]. */
+typedef struct ccmi_syn_layer {
+    int n_out;
+    int ks;
+    int residual;
+    int relu;
+} ccmi_syn_layer;
+
+typedef struct ccmi_syn_args {
+    const float *in;        /* [batch][c_in][h][w] */
+    int64_t in_stride;
+    int c_in;
+    int h;
+    int w;
+    int n_layers;
+    ccmi_syn_layer layers[CCMI_MAX_SYN_LAYERS];
+    const float *params;
+    int64_t param_stride;
+    float *out;             /* [batch][n_out_last][h][w] */
+    int64_t out_stride;
+    void *workspace;        /* ccmi_syn_workspace_bytes(); may be NULL for fused architectures */
+    size_t workspace_bytes;
+    int batch;
+} ccmi_syn_args;
+size_t ccmi_syn_workspace_bytes(const ccmi_syn_args *args);
+int ccmi_syn_forward_f32(const ccmi_syn_args *args, void *stream);
+
+/* Frame post-processing of FrameEncoder.forward in eval mode (frame.py:175-183):
+ * x -> clamp(round(x * (2^bitdepth-1)) / (2^bitdepth-1), 0, 1), optionally 444->420
+ * nearest (yuv.py:275-299).  out420: Y [h][w] then U, V [h/2][w/2] per frame;
+ * out444: [3][h][w] per frame. */
+typedef struct ccmi_post_args {
+    const float *in;        /* [batch][3][h][w] raw synthesis output */
+    int64_t in_stride;
+    int h;
+    int w;
+    int bitdepth;
+    int yuv420;
+    float *out;
+    int64_t out_stride;
+    int batch;
+} ccmi_post_args;
+int ccmi_post_f32(const ccmi_post_args *args, void *stream);
+
+/* ------------------------------------------------------------------------- */
+/* Path B: fixed-point .cool decoder, bit-exact with coolchic/cpp.             */
+/* ------------------------------------------------------------------------- */
+
+/* Same contract as the reference pybind cc_decode_cpu(in, out, bitdepth, chroma,
+ * verbosity) (ccdecapi_cpu.cpp:20-30, ccdecapi.cpp:673-857): 0 on success, 1 on
+ * failure; bitdepth/chroma 0 = take from the header; output format by extension
+ * (.yuv -> planar 420/444, otherwise PPM).  Runs on HIP device `device`. */
+int ccmi_decode_file(const char *in_path, const char *out_path, int out_bitdepth,
+                     int out_chroma, int verbosity, int device);
+
+/* Throughput entry point: decode n independent in-memory .cool streams (intra
+ * frames) in one batched launch sequence.  out[i] receives the same bytes the
+ * reference writes for stream i (YUV if as_yuv, else PPM), out_caps[i] its
+ * capacity; out_sizes[i] (optional) the byte count written.  Host buffers. */
+int ccmi_decode_batch(const uint8_t *const *streams, const size_t *lens, int n,
+                      uint8_t *const *out, const size_t *out_caps, size_t *out_sizes,
+                      int out_bitdepth, int out_chroma, int as_yuv, void *stream);
+
+/* Byte size of the decoded output of one stream (header parse only). */
+int ccmi_decode_output_size(const uint8_t *stream, size_t len, int out_bitdepth,
+                            int out_chroma, int as_yuv, size_t *size);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* CCMI_H */

@@ -1,0 +1,169 @@
+"""Path A (float forward) parity.
+
+CPU tests pin the torch-fp32 oracle (oracle/forward_oracle.py) to the golden vectors
+produced by the reference implementation (tests/golden/forward_*.npz,
+tools/gen_golden_forward.py).  GPU tests run the HIP kernels of libccmi through the
+C ABI and compare them with the golden vectors and with the oracle.
+
+Tolerances (fp32 everywhere; summation order differs from PyTorch's conv/linear):
+  mu, log_scale, upsampling, synthesis: |err| <= 2e-5 * (1 + |ref|_max)
+  rate (bits): |err| <= 2e-3 per latent and |sum err| <= 1e-5 * sum  (Laplace CDF
+               differences amplify last-ulp differences of mu for improbable latents)
+  decoded 8-bit image: PSNR difference <= 1e-5 dB (north_star bar).
+"""
+
+import numpy as np
+import pytest
+import torch
+
+import forward_oracle as fo
+
+GOLDEN = fo.golden_files()
+assert GOLDEN, "tests/golden/forward_*.npz missing"
+
+
+def _tol(ref):
+    return 2e-5 * (1.0 + float(np.abs(ref).max()))
+
+
+def _lat(z, mp):
+    return [torch.from_numpy(z[f"lat{i}"]) for i in range(mp.n_grids)]
+
+
+# ----------------------------------------------------------------------------- CPU: oracle pinned
+
+
+@pytest.mark.parametrize("path", GOLDEN, ids=[p.stem for p in GOLDEN])
+def test_oracle_matches_reference_golden(path):
+    z = np.load(path)
+    mp = fo.ModelParams.from_npz(z)
+    r = fo.forward(mp, _lat(z, mp))
+    for k in ("mu", "scale", "log_scale", "rate", "ups", "syn"):
+        np.testing.assert_allclose(r[k].numpy(), z[k], rtol=0, atol=_tol(z[k]), err_msg=k)
+    for i, q in enumerate(r["q"]):
+        np.testing.assert_array_equal(q.numpy(), z[f"q{i}"])
+    np.testing.assert_allclose(fo.post(r["syn"]).numpy(), z["dec"], atol=1e-6)
+    d420 = fo.post(r["syn"], 8, True)
+    for k in "yuv":
+        np.testing.assert_allclose(d420[k].numpy(), z[f"dec420_{k}"], atol=1e-6)
+
+
+def test_context_offsets_match_c_decoder_table():
+    """The float path's 9x9 mask indices and the C decoder's stride offsets
+    (cc-frame-decoder.cpp:111-154) describe the same causal neighbourhoods."""
+    c16 = [(-3, 0), (-3, 1), (-2, -2), (-2, -1), (-2, 0), (-2, 1), (-2, 2), (-1, -3), (-1, -2), (-1, -1),
+           (-1, 0), (-1, 1), (-1, 2), (0, -3), (0, -2), (0, -1)]
+    assert [(k // 9 - 4, k % 9 - 4) for k in fo.CTX_INDEX[16]] == c16
+    for d, idx in fo.CTX_INDEX.items():
+        assert len(idx) == d and all(k < 40 for k in idx)  # strictly causal
+
+
+# ----------------------------------------------------------------------------- GPU: HIP kernels
+
+
+def _hip_forward(mp_list, lat_list, dev, quantize=True, want=("mu", "scale", "log_scale", "rate")):
+    from ccmi import forward as F
+    mp0 = mp_list[0]
+    lat = torch.stack([torch.cat([x.reshape(-1) for x in lats]) for lats in lat_list]).to(dev)
+    arm_p = torch.stack([F.pack_arm(mp.arm) for mp in mp_list]).to(dev)
+    ups_p = torch.stack([F.pack_ups(mp.ups_full(), mp.pre_full()) for mp in mp_list]).to(dev)
+    syn_p = torch.stack([F.pack_syn(mp.syn) for mp in mp_list]).to(dev)
+    a = F.arm_forward(lat, mp0.sizes, arm_p, mp0.dim_arm, mp0.n_hidden, mp0.gain, quantize, want)
+    u = F.ups_forward(lat, mp0.sizes, ups_p, mp0.ups_k, len(mp0.ups_half), mp0.pre_k, len(mp0.pre_half), mp0.gain,
+                      quantize)
+    s = F.syn_forward(u, mp0.layers, syn_p)
+    torch.cuda.synchronize()
+    return a, u, s
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("path", GOLDEN, ids=[p.stem for p in GOLDEN])
+def test_hip_forward_matches_reference_golden(path, gpu, ccmi_lib):
+    from ccmi import forward as F
+    z = np.load(path)
+    mp = fo.ModelParams.from_npz(z)
+    a, u, s = _hip_forward([mp], [_lat(z, mp)], gpu)
+    for k in ("mu", "log_scale", "scale"):
+        np.testing.assert_allclose(a[k][0].cpu().numpy(), z[k], rtol=0, atol=_tol(z[k]), err_msg=k)
+    r = a["rate"][0].cpu().numpy()
+    assert np.abs(r - z["rate"]).max() <= 2e-3
+    assert abs(r.sum() - z["rate"].sum()) <= 1e-5 * z["rate"].sum() + 1e-3
+    np.testing.assert_allclose(u[0].cpu().numpy(), z["ups"], rtol=0, atol=_tol(z["ups"]))
+    np.testing.assert_allclose(s[0].cpu().numpy(), z["syn"], rtol=0, atol=_tol(z["syn"]))
+    dec = F.post_forward(s, 8, False)[0].cpu().numpy()
+    assert np.mean(dec != z["dec"]) < 1e-3
+    d420 = F.split_420(F.post_forward(s, 8, True)[0], mp.H, mp.W)
+    for k in "yuv":
+        assert np.mean(d420[k].cpu().numpy() != z[f"dec420_{k}"]) < 1e-3
+
+
+def _psnr(x, t):
+    return float(10 * np.log10(1.0 / np.mean((x.astype(np.float64) - t) ** 2)))
+
+
+@pytest.mark.gpu
+def test_hip_psnr_within_1e5_db(gpu, ccmi_lib):
+    """north_star bar: decoded-image PSNR within 1e-5 dB of the reference's, same latents."""
+    from ccmi import forward as F
+    z = np.load([p for p in GOLDEN if "mop_120x208" in p.name][0])
+    mp = fo.ModelParams.from_npz(z)
+    _, _, s = _hip_forward([mp], [_lat(z, mp)], gpu)
+    dec = F.post_forward(s, 8, False)[0].cpu().numpy()
+    target = np.random.default_rng(0).random(dec.shape)
+    assert abs(_psnr(dec, target) - _psnr(z["dec"], target)) <= 1e-5
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("H,W,seed", [(720, 1280, 1), (37, 53, 2), (1, 1, 3), (2, 130, 4), (129, 3, 5)])
+def test_hip_forward_matches_oracle_random(H, W, seed, gpu, ccmi_lib):
+    mp = fo.ModelParams.random(H, W, seed=seed)
+    g = torch.Generator().manual_seed(seed)
+    lat = [0.5 * torch.randn(h, w, generator=g) for h, w in mp.sizes]
+    ref = fo.forward(mp, lat)
+    a, u, s = _hip_forward([mp], [lat], gpu)
+    np.testing.assert_allclose(a["mu"][0].cpu().numpy(), ref["mu"].numpy(), atol=_tol(ref["mu"].numpy()))
+    r = a["rate"][0].cpu().numpy()
+    assert np.abs(r - ref["rate"].numpy()).max() <= 2e-3
+    np.testing.assert_allclose(u[0].cpu().numpy(), ref["ups"].numpy(), atol=_tol(ref["ups"].numpy()))
+    np.testing.assert_allclose(s[0].cpu().numpy(), ref["syn"].numpy(), atol=_tol(ref["syn"].numpy()))
+
+
+@pytest.mark.gpu
+def test_hip_batch_of_frames_with_own_weights(gpu, ccmi_lib):
+    """A batch of independent frames, each with its own network, in one launch sequence."""
+    mps = [fo.ModelParams.random(96, 160, seed=10 + i) for i in range(3)]
+    lats = []
+    for i, mp in enumerate(mps):
+        g = torch.Generator().manual_seed(100 + i)
+        lats.append([0.5 * torch.randn(h, w, generator=g) for h, w in mp.sizes])
+    a, u, s = _hip_forward(mps, lats, gpu)
+    for i, (mp, lat) in enumerate(zip(mps, lats)):
+        ref = fo.forward(mp, lat)
+        np.testing.assert_allclose(s[i].cpu().numpy(), ref["syn"].numpy(), atol=_tol(ref["syn"].numpy()))
+        assert np.abs(a["rate"][i].cpu().numpy() - ref["rate"].numpy()).max() <= 2e-3
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("layers", [
+    "40-1-linear-relu|3-1-linear-none|3-3-residual-relu|3-3-residual-none",   # hop-like, other width
+    "3-1-linear-none|3-3-residual-relu",                                      # single-layer head
+    "16-1-linear-relu|3-1-linear-none",                                       # no 3x3
+    "9-1-linear-relu|6-3-linear-relu|3-5-linear-none",                        # generic path (ks 5)
+    "8-3-linear-relu|3-1-linear-none",                                        # spatial first -> generic
+])
+def test_hip_synthesis_architectures(layers, gpu, ccmi_lib):
+    from ccmi import forward as F
+    L = fo.parse_layers(layers)
+    mp = fo.ModelParams.random(45, 70, layers=L, seed=7)
+    x = torch.randn(7, 45, 70, generator=torch.Generator().manual_seed(3)) * 20
+    ref = fo.synthesis(x, L, mp.syn)
+    out = F.syn_forward(x.to(gpu), L, F.pack_syn(mp.syn).to(gpu))
+    np.testing.assert_allclose(out.cpu().numpy(), ref.numpy(), atol=_tol(ref.numpy()))
+
+
+@pytest.mark.gpu
+def test_hip_rejects_cpu_tensors(ccmi_lib):
+    from ccmi import forward as F
+    mp = fo.ModelParams.random(8, 8, n_grids=2)
+    with pytest.raises(ValueError):
+        F.syn_forward(torch.zeros(2, 8, 8), mp.layers, F.pack_syn(mp.syn))
