@@ -1,0 +1,258 @@
+"""Benchmark: decoded Mpixel/s per GPU of Cool-chic's forward/decode hot path
+(ARM probability model + rate, upsampling, synthesis, 420 post-processing) on
+synthetic 1280x720 frames, hop/c3x decoder architecture, float32.
+
+A step = one batch of `--batch` independent 720p frames (each with its own network,
+as Cool-chic overfits one per image) pushed through the libccmi HIP kernels, inputs
+resident in HBM.  With N GPUs (torchrun, one process per GPU) every rank decodes its
+own frames: weak scaling, no data-path collective; the step time is the max over
+ranks and `value` counts the pixels of all ranks.
+
+Prints ONE JSON line (rank 0).  Also reports:
+  roofline     -- the dominant kernel's algorithmic FLOP/s (HIP events on the launch
+                  stream) vs the FP32 peak, plus HBM traffic from the committed PMC
+                  profile (profiles/*pmc*.json) when present;
+  cpu_baseline -- the CPU oracle (torch fp32 restatement of the reference forward) on
+                  a bounded sample of the same workload, on this host's cores.
+"""
+
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+from pathlib import Path
+
+import torch
+
+ROOT = Path(__file__).resolve().parent
+sys.path.insert(0, str(ROOT / "cool-chic_amd"))
+sys.path.insert(0, str(ROOT / "oracle"))
+
+H, W = 720, 1280
+HOP = [(48, 1, False, True), (3, 1, False, False), (3, 3, True, True), (3, 3, True, False)]
+DIM_ARM, N_HIDDEN, N_GRIDS, GAIN = 16, 2, 7, 16.0
+PEAK_FP32_TFLOPS = 157.3  # MI355X FP32 (vector == f32-MFMA rate), MI355X_MICROARCH.md
+PEAK_HBM_GBS = 8000.0
+
+
+def sizes(h=H, w=W, n=N_GRIDS):
+    out = []
+    for _ in range(n):
+        out.append((h, w))
+        h, w = (h + 1) // 2, (w + 1) // 2
+    return out
+
+
+def flops_per_frame():
+    s = sizes()
+    n_lat = sum(h * w for h, w in s)
+    npx = H * W
+    d = DIM_ARM
+    arm_mac = n_lat * (N_HIDDEN * d * d + 2 * d)
+    syn_mac, c = 0, N_GRIDS
+    for n_out, ks, _, _ in HOP:
+        syn_mac += npx * n_out * c * ks * ks
+        c = n_out
+    # upsampling, polyphase: refine 2*7 taps per output, 2x upsample 2*4 taps per output
+    ups_mac = 0
+    for k in range(N_GRIDS - 1):  # destination level k receives (N_GRIDS-1-k) upsampled channels + 1 refined
+        hk, wk = s[k]
+        ups_mac += hk * wk * (14 + 8 * (N_GRIDS - 1 - k))
+    return {"arm": 2 * arm_mac, "ups": 2 * ups_mac, "syn": 2 * syn_mac, "n_lat": n_lat}
+
+
+def bytes_per_frame():
+    n_lat = sum(h * w for h, w in sizes())
+    npx = H * W
+    return {"arm": 4 * n_lat * 2,                       # read latents, write rate
+            "ups": 4 * (n_lat + N_GRIDS * npx),          # read latents, write dense synthesis input
+            "syn": 4 * (N_GRIDS * npx + 3 * npx),        # read dense input, write 3 planes
+            "post": 4 * (3 * npx + npx * 3 // 2)}
+
+
+def make_inputs(B, dev, seed):
+    import forward_oracle as fo
+    from ccmi import forward as F
+    g = torch.Generator().manual_seed(seed)
+    lat = 0.5 * torch.randn(B, sum(h * w for h, w in sizes()), generator=g)
+    mps = [fo.ModelParams.random(H, W, DIM_ARM, N_HIDDEN, HOP, N_GRIDS, seed=seed + i) for i in range(B)]
+    arm = torch.stack([F.pack_arm(m.arm) for m in mps])
+    ups = torch.stack([F.pack_ups(m.ups_full(), m.pre_full()) for m in mps])
+    syn = torch.stack([F.pack_syn(m.syn) for m in mps])
+    return {"lat": lat.to(dev), "arm": arm.to(dev), "ups": ups.to(dev), "syn": syn.to(dev), "mps": mps,
+            "lat_cpu": lat}
+
+
+class Pipeline:
+    """Preallocated buffers + direct C-ABI launches (no per-step allocation)."""
+
+    def __init__(self, inp, B, dev):
+        import ctypes
+        import ccmi
+        from ccmi import forward as F
+        self.L = ccmi.lib()
+        self.B = B
+        s = sizes()
+        n = sum(h * w for h, w in s)
+        self.rate = torch.empty(B, n, device=dev)
+        self.dense = torch.empty(B, N_GRIDS, H, W, device=dev)
+        self.syn = torch.empty(B, 3, H, W, device=dev)
+        self.yuv = torch.empty(B, H * W + 2 * (H // 2) * (W // 2), device=dev)
+        h, w = F._grid_arrays(s)
+        nws = self.L.ccmi_ups_workspace_bytes(N_GRIDS, h, w, B)
+        self.ws = torch.empty(nws, device=dev, dtype=torch.uint8)
+        p = ccmi.ptr
+        self.arm = ccmi.ArmArgs(latent=p(inp["lat"]), latent_stride=n, n_grids=N_GRIDS, h=h, w=w, gain=GAIN,
+                                quantize=1, dim_arm=DIM_ARM, n_hidden=N_HIDDEN, params=p(inp["arm"]),
+                                param_stride=inp["arm"].shape[1], mu=None, scale=None, log_scale=None,
+                                rate=p(self.rate), out_stride=n, batch=B)
+        self.ups = ccmi.UpsArgs(latent=p(inp["lat"]), latent_stride=n, n_grids=N_GRIDS, h=h, w=w, gain=GAIN,
+                                quantize=1, ups_k=8, n_ups=N_GRIDS - 1, pre_k=7, n_pre=N_GRIDS - 1,
+                                params=p(inp["ups"]), param_stride=inp["ups"].shape[1], out=p(self.dense),
+                                out_stride=N_GRIDS * H * W, workspace=p(self.ws), workspace_bytes=nws, batch=B)
+        self.synargs = F._syn_args(self.dense, HOP, inp["syn"], self.syn, B, N_GRIDS, H, W)
+        self.post = ccmi.PostArgs(in_=p(self.syn), in_stride=3 * H * W, h=H, w=W, bitdepth=8, yuv420=1,
+                                  out=p(self.yuv), out_stride=self.yuv.shape[1], batch=B)
+        self.byref = ctypes.byref
+        self.stream = torch.cuda.current_stream(dev)
+
+    def step(self, events=None):
+        import ccmi
+        L, s, br = self.L, self.stream.cuda_stream, self.byref
+        if events: events[0].record(self.stream)
+        ccmi.check(L.ccmi_arm_forward_f32(br(self.arm), s))
+        if events: events[1].record(self.stream)
+        ccmi.check(L.ccmi_ups_forward_f32(br(self.ups), s))
+        if events: events[2].record(self.stream)
+        ccmi.check(L.ccmi_syn_forward_f32(br(self.synargs), s))
+        if events: events[3].record(self.stream)
+        ccmi.check(L.ccmi_post_f32(br(self.post), s))
+        if events: events[4].record(self.stream)
+
+
+def cpu_baseline(inp, budget_s=12.0, max_frames=8):
+    """Oracle (torch fp32 CPU restatement of the reference forward) on whole 720p frames."""
+    import forward_oracle as fo
+    s = sizes()
+    frames, t0 = 0, time.perf_counter()
+    while frames < max_frames and (time.perf_counter() - t0) < budget_s:
+        i = frames % len(inp["mps"])
+        flat = inp["lat_cpu"][i]
+        lats, o = [], 0
+        for h, w in s:
+            lats.append(flat[o:o + h * w].view(h, w))
+            o += h * w
+        r = fo.forward(inp["mps"][i], lats)
+        fo.post(r["syn"], 8, True)
+        frames += 1
+    dt = time.perf_counter() - t0
+    return {"value": round(frames * H * W / dt / 1e6, 3), "unit": "Mpixel/s", "cores": torch.get_num_threads(),
+            "kind": "port",
+            "sample": f"{frames} synthetic 1280x720 hop frames, full float forward + 420 post "
+                      f"(oracle/forward_oracle.py, torch fp32 CPU, {torch.get_num_threads()} threads), {dt:.1f} s"}
+
+
+def pmc_traffic(stage: str):
+    """Per-launch HBM bytes of `stage` from the committed PMC summary, or None."""
+    for f in sorted((ROOT / "profiles").glob("*pmc*.json"), reverse=True):
+        try:
+            d = json.loads(f.read_text())
+            v = d.get("per_launch_hbm_bytes", {}).get(stage)
+            if v:
+                return float(v), f.name
+        except Exception:
+            pass
+    return None, None
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=50)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--batch", type=int, default=8, help="720p frames per step per GPU")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    dev = torch.device("cuda", local)
+    torch.cuda.set_device(dev)
+
+    B = args.batch
+    inp = make_inputs(B, dev, seed=1000 * rank + 1)
+    pipe = Pipeline(inp, B, dev)
+
+    for _ in range(args.warmup):
+        pipe.step()
+    torch.cuda.synchronize()
+
+    # per-stage HIP events over the timed region (recorded on the launch stream)
+    ev = [[torch.cuda.Event(enable_timing=True) for _ in range(5)] for _ in range(args.steps)]
+    if dist: dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for k in range(args.steps):
+        pipe.step(ev[k])
+    torch.cuda.synchronize()
+    t1 = time.perf_counter()
+    if dist: dist.barrier()
+    dt = t1 - t0
+    if dist:
+        t = torch.tensor([dt], device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        dt = float(t.item())
+
+    stage_ms = {n: sum(ev[k][i].elapsed_time(ev[k][i + 1]) for k in range(args.steps)) / args.steps
+                for i, n in enumerate(["arm", "ups", "syn", "post"])}
+    fl = flops_per_frame()
+    by = bytes_per_frame()
+    dom = max(("arm", "syn"), key=lambda n: stage_ms[n])
+    achieved = fl[dom] * B / (stage_ms[dom] * 1e-3) / 1e12
+    traffic, src = pmc_traffic(dom)
+
+    n_frames = B * args.steps * world
+    value = n_frames * H * W / dt / 1e6
+    res = {
+        "metric": "decoded Mpixel/s per GPU (Synth+ARM+upsample) @1280x720",
+        "value": round(value, 2),
+        "unit": "Mpixel/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(dt / args.steps * 1e3, 4),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "f32",
+        "data": "synthetic (seeded N(0,0.5) latents, random-init hop weights per frame)",
+        "config": {"workload": "1280x720 YUV420 8-bit frames, hop/c3x decoder (arm 16x2, syn 48-1/3-1/3-3r/3-3r, "
+                               "7 latent grids), float forward ARM+rate -> upsampling -> synthesis -> 420 post",
+                   "frames_per_step_per_gpu": B, "parallelism": f"image-parallel x{world}"},
+        "stage_ms_per_step": {k: round(v, 4) for k, v in stage_ms.items()},
+        "roofline": {"bound": "mfma", "kernel": dom, "achieved": round(achieved, 3), "peak": PEAK_FP32_TFLOPS,
+                     "unit": "TFLOP/s", "frac": round(achieved / PEAK_FP32_TFLOPS, 4),
+                     "traffic": traffic, "traffic_source": src,
+                     "algorithmic_flop_per_launch": fl[dom] * B,
+                     "algorithmic_bytes_per_launch": by[dom] * B,
+                     "note": "FP32 VALU-bound fused kernel; peak = FP32 vector rate (= f32 MFMA rate) on MI355X"},
+    }
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        res["cpu_baseline"] = cpu_baseline(inp)
+    if rank == 0:
+        print(json.dumps(res), flush=True)
+    if dist:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()
