@@ -133,7 +133,7 @@ class Pipeline:
         if events: events[4].record(self.stream)
 
 
-def cpu_baseline(inp, budget_s=12.0, max_frames=8):
+def cpu_baseline(inp, budget_s=12.0, max_frames=64):
     """Oracle (torch fp32 CPU restatement of the reference forward) on whole 720p frames."""
     import forward_oracle as fo
     s = sizes()

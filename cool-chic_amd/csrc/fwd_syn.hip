@@ -8,9 +8,9 @@
 //
 // Fast path (every architecture made of a 1x1 "MLP" head followed by 3x3 layers with
 // <= 4 channels -- all the reference presets: hop, mop, lop, ...): ONE fused kernel per
-// launch.  A workgroup owns a 16 x 64 output tile.  Pass 0 evaluates the per-pixel MLP
-// (c_in -> hid -> c_mid, weights wave-uniform in SGPRs) on the tile plus a halo of one
-// pixel per 3x3 layer, and keeps its c_mid outputs in LDS; each 3x3 layer then shrinks
+// launch.  A workgroup owns a 32 x 64 pixel window.  Pass 0 evaluates the per-pixel MLP
+// (c_in -> hid -> c_mid, weights wave-uniform in SGPRs) on the whole window (output tile
+// plus a halo of one pixel per 3x3 layer) and keeps its c_mid outputs in LDS; each 3x3 layer then shrinks
 // the region by one pixel, ping-ponging between two LDS images; the last layer writes
 // to HBM.  Replicate padding is reproduced by evaluating halo pixels at the clamped
 // image coordinate (a pointwise head commutes with clamping; a 3x3 layer reads its
@@ -24,7 +24,6 @@
 namespace {
 
 constexpr int kThreads = 256;
-constexpr int kTY = 16, kTX = 64;
 constexpr int kMaxIn = 8;   // fused path: max synthesis input channels
 constexpr int kMaxMid = 4;  // fused path: max channels through the 3x3 layers
 constexpr int kMaxSp = 3;   // fused path: max number of 3x3 layers
@@ -39,6 +38,7 @@ struct FusedArgs {
     int64_t in_stride;
     int cin, H, W;
     int n_head;          // 1 or 2 1x1 layers
+    int hid;             // hidden width of a 2-layer head
     int w0_off, b0_off, relu0;
     int w1_off, b1_off, relu1;
     int n_sp;            // 3x3 layers after the head
@@ -52,72 +52,104 @@ struct FusedArgs {
 
 __device__ __forceinline__ int clampi(int v, int hi) { return v < 0 ? 0 : (v > hi ? hi : v); }
 
-// HID: hidden width of a 2-layer head (0 for a 1-layer head c_in -> CMID).
-template <int HID, int CMID>
+// Fused head + 3x3 tail.  The workgroup's working region is a fixed 32 x 64 window
+// (2048 pixels, 8 per thread): the output tile is the window minus a halo of one pixel
+// per 3x3 layer.  All stages share the window's coordinate frame (pitch 64); stage t is
+// valid on rows/cols [t, 32-t) x [t, 64-t).  Thread (c = tid & 63, r0 = tid >> 6) owns
+// column c of rows r0, r0+4, ...; the head processes 4 rows per pass so each weight
+// (wave-uniform, scalar-loaded) feeds 4 FMAs, and hidden activations are consumed as
+// they are produced (never stored).
+constexpr int kRW = 64, kRH = 32, kRegion = kRW * kRH;
+constexpr int kRowsPerThread = kRH / (kThreads / kRW); // 8
+constexpr int kNP = 4;                                  // rows per head pass
+
+template <int CIN, int CMID>
 __global__ __launch_bounds__(kThreads) void syn_fused_kernel(FusedArgs A)
 {
-    constexpr int kMaxRegion = (kTY + 2 * kMaxSp) * (kTX + 2 * kMaxSp);
-    __shared__ float s_buf[2][CMID][kMaxRegion];
+    __shared__ float s_buf[2][CMID][kRegion];
 
     const int b = blockIdx.y;
-    const int y0 = (blockIdx.x / A.tiles_x) * kTY;
-    const int x0 = (blockIdx.x % A.tiles_x) * kTX;
+    const int halo = A.n_sp;
+    const int TX = kRW - 2 * halo, TY = kRH - 2 * halo;
+    const int y0 = (blockIdx.x / A.tiles_x) * TY;
+    const int x0 = (blockIdx.x % A.tiles_x) * TX;
+    const int oy = y0 - halo, ox = x0 - halo; // global coords of window (0,0)
     const float *prm = A.params + (int64_t)b * A.pstride;
     const float *in = A.in + (int64_t)b * A.in_stride;
     float *out = A.out + (int64_t)b * A.out_stride;
     const int64_t plane = (int64_t)A.H * A.W;
-    const int halo = A.n_sp;
+    const int c = threadIdx.x & (kRW - 1);
+    const int r0 = threadIdx.x >> 6;
+    const int gx = ox + c;
+    const int cxg = clampi(gx, A.W - 1);
 
     // ------------------------ pass 0: per-pixel 1x1 head ------------------------
-    {
-        const int rh = kTY + 2 * halo, rw = kTX + 2 * halo;
-        const float *w0 = prm + A.w0_off, *b0 = prm + A.b0_off;
-        const float *w1 = prm + A.w1_off, *b1 = prm + A.b1_off;
-        for (int i = threadIdx.x; i < rh * rw; i += kThreads) {
-            const int r = i / rw, c = i - r * rw;
-            const int gy = y0 - halo + r, gx = x0 - halo + c;
-            if (halo == 0 && (gy >= A.H || gx >= A.W)) continue;
-            const int64_t pix = (int64_t)clampi(gy, A.H - 1) * A.W + clampi(gx, A.W - 1);
-            float x[kMaxIn];
+    const float *w0 = prm + A.w0_off, *b0 = prm + A.b0_off;
+    const float *w1 = prm + A.w1_off, *b1 = prm + A.b1_off;
+    const int hid = A.n_head == 2 ? A.hid : 0;
 #pragma unroll
-            for (int k = 0; k < kMaxIn; ++k) x[k] = k < A.cin ? in[k * plane + pix] : 0.f;
-            float o[CMID];
-            if constexpr (HID > 0) {
-                float hdn[HID];
+    for (int g = 0; g < kRowsPerThread / kNP; ++g) {
+        float x[kNP][CIN];
+        float o[kNP][CMID];
 #pragma unroll
-                for (int j = 0; j < HID; ++j) {
+        for (int p = 0; p < kNP; ++p) {
+            const int r = r0 + 4 * (g * kNP + p);
+            const int64_t pix = (int64_t)clampi(oy + r, A.H - 1) * A.W + cxg;
+#pragma unroll
+            for (int k = 0; k < CIN; ++k) x[p][k] = in[k * plane + pix];
+#pragma unroll
+            for (int m = 0; m < CMID; ++m) o[p][m] = 0.f;
+        }
+        if (hid > 0) {
+            for (int j = 0; j < hid; ++j) {
+                const float *wj = w0 + j * CIN;
+                const float bj = b0[j];
+                float wm[CMID];
+#pragma unroll
+                for (int m = 0; m < CMID; ++m) wm[m] = w1[m * hid + j];
+#pragma unroll
+                for (int p = 0; p < kNP; ++p) {
                     float acc = 0.f;
 #pragma unroll
-                    for (int k = 0; k < kMaxIn; ++k)
-                        if (k < A.cin) acc = fmaf(w0[j * A.cin + k], x[k], acc);
-                    acc += b0[j];
-                    hdn[j] = A.relu0 ? fmaxf(acc, 0.f) : acc;
-                }
+                    for (int k = 0; k < CIN; ++k) acc = fmaf(wj[k], x[p][k], acc);
+                    acc += bj;
+                    if (A.relu0) acc = fmaxf(acc, 0.f);
 #pragma unroll
-                for (int m = 0; m < CMID; ++m) {
-                    float acc = 0.f;
-#pragma unroll
-                    for (int j = 0; j < HID; ++j) acc = fmaf(w1[m * HID + j], hdn[j], acc);
-                    acc += b1[m];
-                    o[m] = A.relu1 ? fmaxf(acc, 0.f) : acc;
-                }
-            } else {
-#pragma unroll
-                for (int m = 0; m < CMID; ++m) {
-                    float acc = 0.f;
-#pragma unroll
-                    for (int k = 0; k < kMaxIn; ++k)
-                        if (k < A.cin) acc = fmaf(w0[m * A.cin + k], x[k], acc);
-                    acc += b0[m];
-                    o[m] = A.relu0 ? fmaxf(acc, 0.f) : acc;
+                    for (int m = 0; m < CMID; ++m) o[p][m] = fmaf(wm[m], acc, o[p][m]);
                 }
             }
-            if (halo == 0) {
 #pragma unroll
-                for (int m = 0; m < CMID; ++m) out[m * plane + pix] = o[m];
+            for (int p = 0; p < kNP; ++p)
+#pragma unroll
+                for (int m = 0; m < CMID; ++m) {
+                    float v = o[p][m] + b1[m];
+                    o[p][m] = A.relu1 ? fmaxf(v, 0.f) : v;
+                }
+        } else {
+#pragma unroll
+            for (int m = 0; m < CMID; ++m) {
+                const float bm = b0[m];
+#pragma unroll
+                for (int p = 0; p < kNP; ++p) {
+                    float acc = 0.f;
+#pragma unroll
+                    for (int k = 0; k < CIN; ++k) acc = fmaf(w0[m * CIN + k], x[p][k], acc);
+                    acc += bm;
+                    o[p][m] = A.relu0 ? fmaxf(acc, 0.f) : acc;
+                }
+            }
+        }
+#pragma unroll
+        for (int p = 0; p < kNP; ++p) {
+            const int r = r0 + 4 * (g * kNP + p);
+            if (halo == 0) {
+                const int gy = oy + r;
+                if (gy < A.H && gx < A.W)
+#pragma unroll
+                    for (int m = 0; m < CMID; ++m) out[m * plane + (int64_t)gy * A.W + gx] = o[p][m];
             } else {
 #pragma unroll
-                for (int m = 0; m < CMID; ++m) s_buf[0][m][i] = o[m];
+                for (int m = 0; m < CMID; ++m) s_buf[0][m][r * kRW + c] = o[p][m];
             }
         }
     }
@@ -127,47 +159,45 @@ __global__ __launch_bounds__(kThreads) void syn_fused_kernel(FusedArgs A)
     int cur = 0;
     for (int s = 0; s < A.n_sp; ++s) {
         __syncthreads();
-        const int hin = halo - s;          // halo of the input image of this layer
-        const int hout = hin - 1;          // halo of its output
-        const int iw = kTX + 2 * hin;
-        const int oh = kTY + 2 * hout, ow = kTX + 2 * hout;
-        const int oy = y0 - hin, ox = x0 - hin; // global coords of input-image (0,0)
+        const int t = s + 1; // valid margin of this layer's output within the window
+        const bool last = s == A.n_sp - 1;
         const float *wt = prm + A.sp[s].w_off;
         const float *bs = prm + A.sp[s].b_off;
-        const bool last = s == A.n_sp - 1;
-        for (int i = threadIdx.x; i < oh * ow; i += kThreads) {
-            const int r = i / ow, c = i - r * ow;
-            const int gy = y0 - hout + r, gx = x0 - hout + c;
-            if (last && (gy >= A.H || gx >= A.W)) continue;
-            const int cy = clampi(gy, A.H - 1), cx = clampi(gx, A.W - 1);
-            int ry[3], rx[3];
+        const bool col_ok = c >= t && c < kRW - t;
+        int lx[3];
 #pragma unroll
-            for (int d = 0; d < 3; ++d) {
-                ry[d] = clampi(cy + d - 1, A.H - 1) - oy;
-                rx[d] = clampi(cx + d - 1, A.W - 1) - ox;
-            }
-            float acc[CMID];
+        for (int d = 0; d < 3; ++d) lx[d] = clampi(cxg + d - 1, A.W - 1) - ox;
+        for (int r = r0 + t; r < kRH - t; r += 4) {
+            const int gy = oy + r;
+            if (!col_ok || (last && (gy >= A.H || gx >= A.W))) continue;
+            const int cyg = clampi(gy, A.H - 1);
+            int ly[3];
 #pragma unroll
-            for (int m = 0; m < CMID; ++m) acc[m] = 0.f;
+            for (int d = 0; d < 3; ++d) ly[d] = (clampi(cyg + d - 1, A.H - 1) - oy) * kRW;
+            float nb[CMID][3][3];
 #pragma unroll
             for (int k = 0; k < CMID; ++k)
 #pragma unroll
                 for (int dy = 0; dy < 3; ++dy)
 #pragma unroll
-                    for (int dx = 0; dx < 3; ++dx) {
-                        const float v = s_buf[cur][k][ry[dy] * iw + rx[dx]];
-#pragma unroll
-                        for (int m = 0; m < CMID; ++m) acc[m] = fmaf(wt[((m * CMID + k) * 3 + dy) * 3 + dx], v, acc[m]);
-                    }
+                    for (int dx = 0; dx < 3; ++dx) nb[k][dy][dx] = s_buf[cur][k][ly[dy] + lx[dx]];
 #pragma unroll
             for (int m = 0; m < CMID; ++m) {
-                float v = acc[m] + bs[m];
-                if (A.sp[s].residual) v += s_buf[cur][m][(cy - oy) * iw + (cx - ox)];
+                float acc = 0.f;
+#pragma unroll
+                for (int k = 0; k < CMID; ++k)
+#pragma unroll
+                    for (int dy = 0; dy < 3; ++dy)
+#pragma unroll
+                        for (int dx = 0; dx < 3; ++dx)
+                            acc = fmaf(wt[((m * CMID + k) * 3 + dy) * 3 + dx], nb[k][dy][dx], acc);
+                float v = acc + bs[m];
+                if (A.sp[s].residual) v += nb[m][1][1]; // the input at the clamped centre
                 if (A.sp[s].relu) v = fmaxf(v, 0.f);
                 if (last)
                     out[m * plane + (int64_t)gy * A.W + gx] = v;
                 else
-                    s_buf[cur ^ 1][m][i] = v;
+                    s_buf[cur ^ 1][m][r * kRW + c] = v;
             }
         }
         cur ^= 1;
@@ -268,20 +298,18 @@ bool make_plan(const ccmi_syn_args *a, Plan *P)
     const int cmid = L[n_head - 1].n_out;
     if (cmid < 1 || cmid > kMaxMid) return false;
     int hid = n_head == 2 ? L[0].n_out : 0;
-    if (n_head == 2 && hid != 8 && hid != 12 && hid != 16 && hid != 24 && hid != 32 && hid != 40 && hid != 48 &&
-        hid != 64)
-        return false;
     const int n_sp = a->n_layers - n_head;
     if (n_sp > kMaxSp) return false;
     for (int l = n_head; l < a->n_layers; ++l)
         if (L[l].ks != 3 || L[l].n_out != cmid) return false;
-    if (cmid != 3 && !(cmid == 4 && hid == 0)) return false; // instantiated shapes
+    if (cmid != 3 && cmid != 4) return false; // instantiated shapes
     FusedArgs &f = P->fa;
     f = FusedArgs{};
     f.cin = a->c_in;
     f.H = a->h;
     f.W = a->w;
     f.n_head = n_head;
+    f.hid = hid;
     f.w0_off = w_off[0];
     f.b0_off = b_off[0];
     f.relu0 = L[0].relu;
@@ -303,10 +331,19 @@ bool make_plan(const ccmi_syn_args *a, Plan *P)
     return true;
 }
 
-template <int HID>
-void launch_fused_hid(dim3 grid, hipStream_t s, const FusedArgs &fa, int cmid)
+template <int CMID>
+void launch_fused(dim3 grid, hipStream_t s, const FusedArgs &fa)
 {
-    if (cmid == 3) hipLaunchKernelGGL((syn_fused_kernel<HID, 3>), grid, dim3(kThreads), 0, s, fa);
+    switch (fa.cin) {
+    case 1: hipLaunchKernelGGL((syn_fused_kernel<1, CMID>), grid, dim3(kThreads), 0, s, fa); break;
+    case 2: hipLaunchKernelGGL((syn_fused_kernel<2, CMID>), grid, dim3(kThreads), 0, s, fa); break;
+    case 3: hipLaunchKernelGGL((syn_fused_kernel<3, CMID>), grid, dim3(kThreads), 0, s, fa); break;
+    case 4: hipLaunchKernelGGL((syn_fused_kernel<4, CMID>), grid, dim3(kThreads), 0, s, fa); break;
+    case 5: hipLaunchKernelGGL((syn_fused_kernel<5, CMID>), grid, dim3(kThreads), 0, s, fa); break;
+    case 6: hipLaunchKernelGGL((syn_fused_kernel<6, CMID>), grid, dim3(kThreads), 0, s, fa); break;
+    case 7: hipLaunchKernelGGL((syn_fused_kernel<7, CMID>), grid, dim3(kThreads), 0, s, fa); break;
+    case 8: hipLaunchKernelGGL((syn_fused_kernel<8, CMID>), grid, dim3(kThreads), 0, s, fa); break;
+    }
 }
 
 } // namespace
@@ -341,22 +378,11 @@ int ccmi_launch_syn_f32(const ccmi_syn_args *a, hipStream_t s)
         P.fa.pstride = a->param_stride;
         P.fa.out = a->out;
         P.fa.out_stride = a->out_stride;
-        P.fa.tiles_x = ccmi_div_up(a->w, kTX);
-        dim3 grid(P.fa.tiles_x * ccmi_div_up(a->h, kTY), a->batch);
-        switch (P.hid) {
-        case 0:
-            if (P.cmid == 3) hipLaunchKernelGGL((syn_fused_kernel<0, 3>), grid, dim3(kThreads), 0, s, P.fa);
-            else hipLaunchKernelGGL((syn_fused_kernel<0, 4>), grid, dim3(kThreads), 0, s, P.fa);
-            break;
-        case 8: launch_fused_hid<8>(grid, s, P.fa, P.cmid); break;
-        case 12: launch_fused_hid<12>(grid, s, P.fa, P.cmid); break;
-        case 16: launch_fused_hid<16>(grid, s, P.fa, P.cmid); break;
-        case 24: launch_fused_hid<24>(grid, s, P.fa, P.cmid); break;
-        case 32: launch_fused_hid<32>(grid, s, P.fa, P.cmid); break;
-        case 40: launch_fused_hid<40>(grid, s, P.fa, P.cmid); break;
-        case 48: launch_fused_hid<48>(grid, s, P.fa, P.cmid); break;
-        case 64: launch_fused_hid<64>(grid, s, P.fa, P.cmid); break;
-        }
+        const int halo = P.fa.n_sp;
+        P.fa.tiles_x = ccmi_div_up(a->w, kRW - 2 * halo);
+        dim3 grid(P.fa.tiles_x * ccmi_div_up(a->h, kRH - 2 * halo), a->batch);
+        if (P.cmid == 3) launch_fused<3>(grid, s, P.fa);
+        else launch_fused<4>(grid, s, P.fa);
         CCMI_HIP_CHECK(hipGetLastError());
         return CCMI_OK;
     }
