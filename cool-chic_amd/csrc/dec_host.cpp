@@ -1,0 +1,559 @@
+// dec_host.cpp -- path B host side: .cool parsing, network weight decoding (CABAC
+// Exp-Golomb, tiny), device memory planning and the decode C-ABI entry points.
+//
+// Reference: cc-bitstream.cpp:58-275 (headers, chunking), cc-frame-decoder.cpp:157-353
+// (read_arm / read_ups / read_syn and the Q_STEP_*_SHIFT tables :28-108), ccdecapi.cpp
+// :673-857 (cc_decode_* driver, output formats).  All latent-layer decoding, upsampling,
+// synthesis and output conversion run on the GPU (dec_kernels.hip).
+#include <stdio.h>
+#include <string.h>
+
+#include <algorithm>
+#include <string>
+#include <vector>
+
+#include "ccmi_cabac.h"
+#include "dec_internal.h"
+
+namespace ccmi {
+
+namespace {
+
+struct Reader {
+    const uint8_t *p;
+    size_t n, pos;
+    bool err;
+    int u(int nb)
+    {
+        if (pos + (size_t)nb > n) {
+            err = true;
+            return 0;
+        }
+        int v = 0;
+        for (int i = 0; i < nb; ++i) v = (v << 8) | p[pos++];
+        return v;
+    }
+    const uint8_t *take(int nb)
+    {
+        if (nb < 0 || pos + (size_t)nb > n) {
+            err = true;
+            return nullptr;
+        }
+        const uint8_t *q = p + pos;
+        pos += (size_t)nb;
+        return q;
+    }
+};
+
+struct Lqi {
+    int qw, qb, sw, sb, nw, nb;
+};
+
+// Exp-Golomb magnitude + EP sign, then << (precision - q_step_shift)  (decode_weights_qi)
+bool read_weights(Cabac<HostBytes> &c, int k, int n, int shift, int prec, int32_t *dst)
+{
+    if (prec < shift) return false;
+    for (int i = 0; i < n; ++i) {
+        int32_t v = c.expgolomb(k);
+        if (v != 0 && c.ep()) v = -v;
+        dst[i] = (int32_t)((uint32_t)v << (prec - shift));
+    }
+    return true;
+}
+
+Cabac<HostBytes> cabac_on(const uint8_t *p, int n)
+{
+    Cabac<HostBytes> c;
+    c.src = HostBytes{p, (uint32_t)(n > 0 ? n : 0), 0};
+    c.start();
+    return c;
+}
+
+} // namespace
+
+int parse_and_decode_frame(const uint8_t *bs, size_t n, FrameHost &f)
+{
+    Reader r{bs, n, 0, false};
+    r.u(2);
+    f.h = r.u(2);
+    f.w = r.u(2);
+    int raw = r.u(1);
+    f.bitdepth = (raw >> 4) + 8;
+    f.frame_data_type = raw & 0xF;
+    f.intra_period = r.u(1);
+    r.u(1); // p_period
+    if (r.err || f.h < 1 || f.w < 1) return ccmi_set_error(CCMI_ERR_BITSTREAM, "truncated GOP header");
+    if (f.intra_period != 0)
+        return ccmi_set_error(CCMI_ERR_UNSUPPORTED, "inter (P/B) frames are outside the decoded hot path");
+    r.u(2); // frame header size
+    r.u(1); // display index
+    raw = r.u(1);
+    f.dim_arm = 8 * (raw >> 4);
+    f.n_hidden = raw & 0xF;
+    raw = r.u(1);
+    f.n_ups = raw >> 4;
+    f.ups_ks = raw & 0xF;
+    raw = r.u(1);
+    f.n_pre = raw >> 4;
+    f.pre_ks = raw & 0xF;
+    f.n_branches = r.u(1);
+    const int n_syn = r.u(1);
+    if (r.err || n_syn < 1 || n_syn > CCMI_MAX_SYN_LAYERS)
+        return ccmi_set_error(CCMI_ERR_BITSTREAM, "bad synthesis layer count %d", n_syn);
+    f.layers.resize(n_syn);
+    for (auto &L : f.layers) {
+        L.n_out = r.u(1);
+        L.ks = r.u(1);
+        raw = r.u(1);
+        L.residual = (raw >> 4) != 0;
+        L.relu = (raw & 0xF) != 0;
+    }
+    r.u(1); // flow gain
+    r.u(2); // ac_max_val_nn
+    r.u(2); // ac_max_val_latent
+    f.sig_blk = (signed char)r.u(1);
+    Lqi arm{}, ups{}, syn{};
+    Lqi *q[3] = {&arm, &ups, &syn};
+    for (auto *x : q) {
+        x->qw = r.u(1);
+        x->qb = r.u(1);
+        if (x->qb == 255) x->qb = -1;
+    }
+    for (auto *x : q) {
+        x->sw = r.u(1);
+        x->sb = x->qb < 0 ? -1 : r.u(1);
+    }
+    for (auto *x : q) {
+        x->nw = r.u(2);
+        x->nb = x->qb < 0 ? -1 : r.u(2);
+    }
+    f.n_layers = r.u(1);
+    const int n_grid = r.u(1);
+    if (r.err || f.n_layers < 2 || f.n_layers > CCMI_MAX_GRIDS || n_grid != f.n_layers)
+        return ccmi_set_error(CCMI_ERR_BITSTREAM, "bad latent layer count %d/%d", f.n_layers, n_grid);
+    for (int i = 0; i < f.n_layers; ++i)
+        if (r.u(1) != 1) return ccmi_set_error(CCMI_ERR_UNSUPPORTED, "only 1 feature per latent resolution");
+    for (int i = 0; i < f.n_layers; ++i) f.lat_n[i] = (uint32_t)r.u(3);
+    if (r.err) return ccmi_set_error(CCMI_ERR_BITSTREAM, "truncated frame header");
+    const uint8_t *arm_w = r.take(arm.nw), *arm_b = r.take(arm.nb < 0 ? 0 : arm.nb);
+    const uint8_t *ups_w = r.take(ups.nw);
+    r.take(ups.nb < 0 ? 0 : ups.nb);
+    const uint8_t *syn_w = r.take(syn.nw), *syn_b = r.take(syn.nb < 0 ? 0 : syn.nb);
+    for (int i = 0; i < f.n_layers; ++i) f.lat_bytes[i] = r.take((int)f.lat_n[i]);
+    if (r.err) return ccmi_set_error(CCMI_ERR_BITSTREAM, "truncated stream (payload shorter than the header says)");
+    for (int l = 0, hh = f.h, ww = f.w; l < f.n_layers; ++l, hh = (hh + 1) / 2, ww = (ww + 1) / 2) {
+        f.lh[l] = hh;
+        f.lw[l] = ww;
+    }
+
+    // ---- ARM (read_arm, cc-frame-decoder.cpp:201-258)
+    const int d = f.dim_arm;
+    if (d != 8 && d != 16 && d != 24 && d != 32) return ccmi_set_error(CCMI_ERR_UNSUPPORTED, "dim_arm %d", d);
+    if (f.n_hidden > 4) return ccmi_set_error(CCMI_ERR_UNSUPPORTED, "%d ARM hidden layers", f.n_hidden);
+    if (arm.qw > 8 || arm.qb < 0 || arm.qb > 16) return ccmi_set_error(CCMI_ERR_BITSTREAM, "ARM q-step index");
+    {
+        auto cw = cabac_on(arm_w, arm.nw), cb = cabac_on(arm_b, arm.nb);
+        const int ws = 8 - arm.qw, bsh = 16 - arm.qb;
+        f.arm.assign((size_t)f.n_hidden * (d * d + d) + 2 * d + 2, 0);
+        int32_t *p = f.arm.data();
+        for (int l = 0; l < f.n_hidden; ++l, p += d * d + d)
+            if (!read_weights(cw, arm.sw, d * d, ws, kArmPrec, p) || !read_weights(cb, arm.sb, d, bsh, 2 * kArmPrec, p + d * d))
+                return ccmi_set_error(CCMI_ERR_BITSTREAM, "ARM weights");
+        if (!read_weights(cw, arm.sw, 2 * d, ws, kArmPrec, p) || !read_weights(cb, arm.sb, 2, bsh, 2 * kArmPrec, p + 2 * d))
+            return ccmi_set_error(CCMI_ERR_BITSTREAM, "ARM weights");
+    }
+    // ---- upsampling (read_ups :261-300): half kernels mirrored (decode_upsweights_qi)
+    if (ups.qw > 12 || f.n_ups < 1 || f.n_pre < 1 || f.ups_ks < 2 || f.pre_ks < 1)
+        return ccmi_set_error(CCMI_ERR_BITSTREAM, "upsampling header");
+    {
+        auto cw = cabac_on(ups_w, ups.nw);
+        f.ups.assign((size_t)f.n_ups * f.ups_ks + (size_t)f.n_pre * f.pre_ks, 0);
+        int32_t *p = f.ups.data();
+        auto sym = [&](int ks) {
+            const int nw = (ks + 1) / 2;
+            if (!read_weights(cw, ups.sw, nw, 12 - ups.qw, kUpsPrec, p)) return false;
+            for (int i = 0; i < nw / 2 * 2; ++i) p[ks - 1 - i] = p[i];
+            p += ks;
+            return true;
+        };
+        for (int l = 0; l < f.n_ups; ++l)
+            if (!sym(f.ups_ks)) return ccmi_set_error(CCMI_ERR_BITSTREAM, "upsampling weights");
+        for (int l = 0; l < f.n_pre; ++l)
+            if (!sym(f.pre_ks)) return ccmi_set_error(CCMI_ERR_BITSTREAM, "upsampling weights");
+    }
+    // ---- synthesis (read_syn :302-353)
+    if (syn.qw > 12 || syn.qb < 0 || syn.qb > 24 || f.n_branches < 1 || f.n_branches > 8)
+        return ccmi_set_error(CCMI_ERR_BITSTREAM, "synthesis header");
+    {
+        auto cw = cabac_on(syn_w, syn.nw), cb = cabac_on(syn_b, syn.nb);
+        const int ws = 12 - syn.qw, bsh = 24 - syn.qb;
+        if (f.n_branches > 1) {
+            f.blend.assign(f.n_branches, 0);
+            if (!read_weights(cw, syn.sw, f.n_branches, ws, kSynPrec, f.blend.data()))
+                return ccmi_set_error(CCMI_ERR_BITSTREAM, "blend weights");
+        }
+        size_t per_branch = 0;
+        {
+            int c = f.n_layers;
+            for (auto &L : f.layers) {
+                if (L.n_out < 1 || L.ks < 1 || (L.ks & 1) == 0) return ccmi_set_error(CCMI_ERR_UNSUPPORTED, "syn layer ks %d", L.ks);
+                per_branch += (size_t)L.n_out * c * L.ks * L.ks + L.n_out;
+                c = L.n_out;
+            }
+        }
+        f.syn.assign(per_branch * f.n_branches, 0);
+        int32_t *p = f.syn.data();
+        for (int b = 0; b < f.n_branches; ++b) {
+            int c = f.n_layers;
+            for (auto &L : f.layers) {
+                const int nw = c * L.ks * L.ks * L.n_out;
+                if (!read_weights(cw, syn.sw, nw, ws, kSynPrec, p) || !read_weights(cb, syn.sb, L.n_out, bsh, 2 * kSynPrec, p + nw))
+                    return ccmi_set_error(CCMI_ERR_BITSTREAM, "synthesis weights");
+                p += nw + L.n_out;
+                c = L.n_out;
+            }
+        }
+    }
+    if (f.layers.back().n_out < 3) return ccmi_set_error(CCMI_ERR_UNSUPPORTED, "synthesis must output >= 3 planes");
+    return CCMI_OK;
+}
+
+} // namespace ccmi
+
+using namespace ccmi;
+
+namespace {
+
+enum OutKind { kYuv420 = 0, kYuv444 = 1, kPpm = 2 };
+
+struct OutFmt {
+    int kind, bitdepth;
+    size_t payload, header;
+    char hdr[48];
+};
+
+int out_format(const FrameHost &f, int out_bitdepth, int out_chroma, int as_yuv, OutFmt &o)
+{
+    o.bitdepth = out_bitdepth ? out_bitdepth : f.bitdepth;
+    const int chroma = out_chroma ? out_chroma : (f.frame_data_type == 1 ? 420 : 444);
+    const size_t bps = o.bitdepth <= 8 ? 1 : 2;
+    const size_t npx = (size_t)f.h * f.w;
+    o.header = 0;
+    if (as_yuv) {
+        if (o.bitdepth != 8 && o.bitdepth != 10)
+            return ccmi_set_error(CCMI_ERR_UNSUPPORTED, "YUV output bitdepth must be 8 or 10 (got %d)", o.bitdepth);
+        o.kind = chroma == 420 ? kYuv420 : kYuv444;
+        o.payload = bps * (o.kind == kYuv420 ? npx + 2 * (size_t)(f.h / 2) * (f.w / 2) : 3 * npx);
+    } else {
+        if (o.bitdepth < 1 || o.bitdepth > 16) return ccmi_set_error(CCMI_ERR_ARG, "PPM bitdepth %d", o.bitdepth);
+        o.kind = kPpm;
+        o.header = (size_t)snprintf(o.hdr, sizeof o.hdr, "P6\n%d %d\n%d\n", f.w, f.h, (1 << o.bitdepth) - 1);
+        o.payload = bps * 3 * npx;
+    }
+    return CCMI_OK;
+}
+
+size_t align_up(size_t v, size_t a) { return (v + a - 1) / a * a; }
+
+struct DevPlan {
+    size_t bytes_off[CCMI_MAX_GRIDS];
+    size_t arm_off, ups_off, syn_off, lat_off, ws_off, dense_off, synout_off, synws_off, out_off;
+    size_t lat_elems, ws_elems, dense_elems, synout_elems, synws_elems;
+};
+
+int decode_many(const uint8_t *const *streams, const size_t *lens, int n, uint8_t *const *outs, const size_t *caps,
+                size_t *sizes, int out_bitdepth, int out_chroma, int as_yuv, hipStream_t s)
+{
+    if (n < 1) return ccmi_set_error(CCMI_ERR_ARG, "decode: no streams");
+    std::vector<FrameHost> fr(n);
+    std::vector<OutFmt> of(n);
+    for (int i = 0; i < n; ++i) {
+        if (!streams[i]) return ccmi_set_error(CCMI_ERR_ARG, "decode: stream %d is NULL", i);
+        if (int rc = parse_and_decode_frame(streams[i], lens[i], fr[i])) {
+            std::string m = ccmi_last_error();
+            return ccmi_set_error(rc, "stream %d: %s", i, m.c_str());
+        }
+        if (int rc = out_format(fr[i], out_bitdepth, out_chroma, as_yuv, of[i])) return rc;
+        if (outs && caps && caps[i] < of[i].header + of[i].payload)
+            return ccmi_set_error(CCMI_ERR_ARG, "stream %d: output buffer of %zu bytes, need %zu", i, caps[i],
+                                  of[i].header + of[i].payload);
+        if (sizes) sizes[i] = of[i].header + of[i].payload;
+    }
+
+    // ---- plan one device allocation: constant part (bytes + weights, uploaded) then scratch
+    std::vector<DevPlan> pl(n);
+    size_t cst = 0;
+    for (int i = 0; i < n; ++i) {
+        FrameHost &f = fr[i];
+        DevPlan &p = pl[i];
+        for (int l = 0; l < f.n_layers; ++l) {
+            p.bytes_off[l] = cst;
+            cst += align_up(f.lat_n[l] + 64, 256);
+        }
+        p.arm_off = cst;
+        cst += align_up(f.arm.size() * 4, 256);
+        p.ups_off = cst;
+        cst += align_up(f.ups.size() * 4, 256);
+        p.syn_off = cst;
+        cst += align_up(f.syn.size() * 4, 256);
+    }
+    size_t tot = align_up(cst, 4096);
+    for (int i = 0; i < n; ++i) {
+        FrameHost &f = fr[i];
+        DevPlan &p = pl[i];
+        p.lat_elems = 0;
+        for (int l = 0; l < f.n_layers; ++l) p.lat_elems += (size_t)f.lh[l] * f.lw[l];
+        p.ws_elems = dec_ups_workspace_elems(f.lh, f.lw, f.n_layers);
+        p.dense_elems = (size_t)f.n_layers * f.h * f.w;
+        p.synout_elems = (size_t)f.layers.back().n_out * f.h * f.w * f.n_branches;
+        DecSynArgs sa{};
+        sa.c_in = f.n_layers;
+        sa.h = f.h;
+        sa.w = f.w;
+        sa.n_layers = (int)f.layers.size();
+        for (int l = 0; l < sa.n_layers; ++l) sa.layers[l] = f.layers[l];
+        p.synws_elems = dec_syn_workspace_elems(sa);
+        p.lat_off = tot;
+        tot += align_up(p.lat_elems * 4, 256);
+        p.ws_off = tot;
+        tot += align_up(p.ws_elems * 4 + 4, 256);
+        p.dense_off = tot;
+        tot += align_up(p.dense_elems * 4, 256);
+        p.synout_off = tot;
+        tot += align_up(p.synout_elems * 4, 256);
+        p.synws_off = tot;
+        tot += align_up(p.synws_elems * 4 + 4, 256);
+        p.out_off = tot;
+        tot += align_up(of[i].payload, 256);
+    }
+    const size_t desc_off = tot;
+    tot += align_up(sizeof(ArmStreamDesc) * (size_t)n * CCMI_MAX_GRIDS, 256);
+
+    std::vector<uint8_t> host(cst, 0);
+    for (int i = 0; i < n; ++i) {
+        FrameHost &f = fr[i];
+        DevPlan &p = pl[i];
+        for (int l = 0; l < f.n_layers; ++l)
+            if (f.lat_n[l]) memcpy(&host[p.bytes_off[l]], f.lat_bytes[l], f.lat_n[l]);
+        memcpy(&host[p.arm_off], f.arm.data(), f.arm.size() * 4);
+        memcpy(&host[p.ups_off], f.ups.data(), f.ups.size() * 4);
+        memcpy(&host[p.syn_off], f.syn.data(), f.syn.size() * 4);
+    }
+
+    uint8_t *dev = nullptr;
+    CCMI_HIP_CHECK(hipMalloc(&dev, tot));
+    struct Free {
+        uint8_t *p;
+        ~Free() { if (p) (void)hipFree(p); }
+    } guard{dev};
+    CCMI_HIP_CHECK(hipMemcpyAsync(dev, host.data(), cst, hipMemcpyHostToDevice, s));
+
+    // ---- ARM + CABAC: every non-empty latent layer of every frame, one launch per (d, nh)
+    std::vector<ArmStreamDesc> desc;
+    struct Key { int d, nh; };
+    std::vector<std::pair<Key, std::vector<ArmStreamDesc>>> groups;
+    int max_w = 0, max_blocks = 1;
+    for (int i = 0; i < n; ++i) {
+        FrameHost &f = fr[i];
+        DevPlan &p = pl[i];
+        int32_t *lat = reinterpret_cast<int32_t *>(dev + p.lat_off);
+        for (int l = 0; l < f.n_layers; ++l) {
+            int32_t *plane = lat;
+            lat += (size_t)f.lh[l] * f.lw[l];
+            if (f.lat_n[l] == 0) { // zero layer (cc-frame-decoder.cpp:479-484)
+                CCMI_HIP_CHECK(hipMemsetAsync(plane, 0, (size_t)f.lh[l] * f.lw[l] * 4, s));
+                continue;
+            }
+            ArmStreamDesc a{};
+            a.bytes = reinterpret_cast<const uint32_t *>(dev + p.bytes_off[l]);
+            a.nbytes = f.lat_n[l];
+            a.h = f.lh[l];
+            a.w = f.lw[l];
+            a.sig_blk = f.sig_blk;
+            a.d = f.dim_arm;
+            a.nh = f.n_hidden;
+            a.weights = reinterpret_cast<const int32_t *>(dev + p.arm_off);
+            a.out = plane;
+            max_w = std::max(max_w, a.w);
+            const int blk = std::abs(a.sig_blk);
+            if (blk > 0) {
+                int sh = 0;
+                while ((1 << sh) < blk) ++sh;
+                max_blocks = std::max(max_blocks, ((a.h + blk - 1) >> sh) * ((a.w + blk - 1) >> sh));
+            }
+            auto it = std::find_if(groups.begin(), groups.end(),
+                                   [&](auto &g) { return g.first.d == a.d && g.first.nh == a.nh; });
+            if (it == groups.end()) {
+                groups.push_back({Key{a.d, a.nh}, {}});
+                it = groups.end() - 1;
+            }
+            it->second.push_back(a);
+        }
+    }
+    size_t dpos = 0;
+    std::vector<ArmStreamDesc> all;
+    for (auto &g : groups) {
+        // longest streams first: they bound the launch
+        std::stable_sort(g.second.begin(), g.second.end(),
+                         [](const ArmStreamDesc &x, const ArmStreamDesc &y) { return x.h * x.w > y.h * y.w; });
+        all.insert(all.end(), g.second.begin(), g.second.end());
+    }
+    if (!all.empty()) {
+        CCMI_HIP_CHECK(hipMemcpyAsync(dev + desc_off, all.data(), all.size() * sizeof(ArmStreamDesc),
+                                      hipMemcpyHostToDevice, s));
+        for (auto &g : groups) {
+            const ArmStreamDesc *dd = reinterpret_cast<const ArmStreamDesc *>(dev + desc_off) + dpos;
+            if (int rc = launch_dec_arm(dd, (int)g.second.size(), max_w, max_blocks, g.first.d, g.first.nh, s)) return rc;
+            dpos += g.second.size();
+        }
+    }
+
+    // ---- per frame: upsampling, synthesis (+ blend), output bytes
+    for (int i = 0; i < n; ++i) {
+        FrameHost &f = fr[i];
+        DevPlan &p = pl[i];
+        DecUpsArgs ua{};
+        ua.lat = reinterpret_cast<const int32_t *>(dev + p.lat_off);
+        ua.n_layers = f.n_layers;
+        int off = 0;
+        for (int l = 0; l < f.n_layers; ++l) {
+            ua.lh[l] = f.lh[l];
+            ua.lw[l] = f.lw[l];
+            ua.off[l] = off;
+            off += f.lh[l] * f.lw[l];
+        }
+        ua.kernels = reinterpret_cast<const int32_t *>(dev + p.ups_off);
+        ua.ups_ks = f.ups_ks;
+        ua.n_ups = f.n_ups;
+        ua.pre_ks = f.pre_ks;
+        ua.n_pre = f.n_pre;
+        ua.workspace = reinterpret_cast<int32_t *>(dev + p.ws_off);
+        ua.out = reinterpret_cast<int32_t *>(dev + p.dense_off);
+        if (int rc = launch_dec_ups(ua, s)) return rc;
+
+        const int nout = f.layers.back().n_out;
+        const int64_t plane = (int64_t)f.h * f.w;
+        size_t per_branch = f.syn.size() / f.n_branches;
+        int32_t *synout = reinterpret_cast<int32_t *>(dev + p.synout_off);
+        for (int b = 0; b < f.n_branches; ++b) {
+            DecSynArgs sa{};
+            sa.in = ua.out;
+            sa.c_in = f.n_layers;
+            sa.h = f.h;
+            sa.w = f.w;
+            sa.n_layers = (int)f.layers.size();
+            for (int l = 0; l < sa.n_layers; ++l) sa.layers[l] = f.layers[l];
+            sa.params = reinterpret_cast<const int32_t *>(dev + p.syn_off) + per_branch * b;
+            sa.out = synout + (size_t)b * nout * plane;
+            sa.workspace = reinterpret_cast<int32_t *>(dev + p.synws_off);
+            if (int rc = launch_dec_syn(sa, s)) return rc;
+            if (b >= 1) // run_syn (cc-frame-decoder.cpp:1044-1149): blends on 3 planes
+                if (int rc = launch_dec_blend(synout, synout + (size_t)b * nout * plane, 3 * plane,
+                                              f.blend[0], f.blend[b], b == 1, s))
+                    return rc;
+        }
+        if (int rc = launch_dec_output(synout, f.h, f.w, of[i].bitdepth, of[i].kind, dev + p.out_off, s)) return rc;
+        if (outs) {
+            if (of[i].header) memcpy(outs[i], of[i].hdr, of[i].header);
+            CCMI_HIP_CHECK(hipMemcpyAsync(outs[i] + of[i].header, dev + p.out_off, of[i].payload,
+                                          hipMemcpyDeviceToHost, s));
+        }
+    }
+    CCMI_HIP_CHECK(hipStreamSynchronize(s));
+    return CCMI_OK;
+}
+
+} // namespace
+
+extern "C" int ccmi_decode_output_size(const uint8_t *stream, size_t len, int out_bitdepth, int out_chroma, int as_yuv,
+                                       size_t *size)
+{
+    if (!stream || !size) return ccmi_set_error(CCMI_ERR_ARG, "decode_output_size: null argument");
+    FrameHost f;
+    if (int rc = parse_and_decode_frame(stream, len, f)) return rc;
+    OutFmt o;
+    if (int rc = out_format(f, out_bitdepth, out_chroma, as_yuv, o)) return rc;
+    *size = o.header + o.payload;
+    return CCMI_OK;
+}
+
+extern "C" int ccmi_decode_batch(const uint8_t *const *streams, const size_t *lens, int n, uint8_t *const *out,
+                                 const size_t *out_caps, size_t *out_sizes, int out_bitdepth, int out_chroma,
+                                 int as_yuv, void *stream)
+{
+    if (!streams || !lens || !out || !out_caps) return ccmi_set_error(CCMI_ERR_ARG, "decode_batch: null argument");
+    return decode_many(streams, lens, n, out, out_caps, out_sizes, out_bitdepth, out_chroma, as_yuv,
+                       static_cast<hipStream_t>(stream));
+}
+
+static bool ends_with(const std::string &a, const char *b)
+{
+    const size_t n = strlen(b);
+    return a.size() >= n && a.compare(a.size() - n, n, b) == 0;
+}
+
+extern "C" int ccmi_decode_file(const char *in_path, const char *out_path, int out_bitdepth, int out_chroma,
+                                int verbosity, int device)
+{
+    if (!in_path) {
+        ccmi_set_error(CCMI_ERR_ARG, "decode: no input bitstream");
+        return 1;
+    }
+    FILE *fi = fopen(in_path, "rb");
+    if (!fi) {
+        ccmi_set_error(CCMI_ERR_IO, "cannot open %s for reading", in_path);
+        return 1;
+    }
+    std::vector<uint8_t> buf;
+    {
+        fseek(fi, 0, SEEK_END);
+        long n = ftell(fi);
+        fseek(fi, 0, SEEK_SET);
+        buf.resize(n > 0 ? (size_t)n : 0);
+        const bool ok = buf.empty() || fread(buf.data(), 1, buf.size(), fi) == buf.size();
+        fclose(fi);
+        if (!ok) {
+            ccmi_set_error(CCMI_ERR_IO, "cannot read %s", in_path);
+            return 1;
+        }
+    }
+    if (hipSetDevice(device) != hipSuccess) {
+        ccmi_set_error(CCMI_ERR_HIP, "hipSetDevice(%d) failed", device);
+        return 1;
+    }
+    const std::string out = out_path ? out_path : "";
+    const int as_yuv = ends_with(out, ".yuv");
+    size_t need = 0;
+    if (ccmi_decode_output_size(buf.data(), buf.size(), out_bitdepth, out_chroma, as_yuv, &need)) return 1;
+    std::vector<uint8_t> res(need);
+    const uint8_t *sp = buf.data();
+    const size_t ln = buf.size();
+    uint8_t *op = res.data();
+    size_t got = 0;
+    hipEvent_t e0, e1;
+    (void)hipEventCreate(&e0);
+    (void)hipEventCreate(&e1);
+    (void)hipEventRecord(e0, nullptr);
+    if (decode_many(&sp, &ln, 1, &op, &need, &got, out_bitdepth, out_chroma, as_yuv, nullptr)) return 1;
+    (void)hipEventRecord(e1, nullptr);
+    (void)hipEventSynchronize(e1);
+    float ms = 0;
+    (void)hipEventElapsedTime(&ms, e0, e1);
+    (void)hipEventDestroy(e0);
+    (void)hipEventDestroy(e1);
+    if (verbosity >= 1) printf("time: all %g\n", ms * 1e-3);
+    if (!out.empty()) {
+        FILE *fo = fopen(out.c_str(), "wb");
+        if (!fo) {
+            ccmi_set_error(CCMI_ERR_IO, "cannot open %s for writing", out.c_str());
+            return 1;
+        }
+        const bool ok = fwrite(res.data(), 1, got, fo) == got;
+        fclose(fo);
+        if (!ok) {
+            ccmi_set_error(CCMI_ERR_IO, "cannot write %s", out.c_str());
+            return 1;
+        }
+    }
+    return 0;
+}

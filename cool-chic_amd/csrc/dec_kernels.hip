@@ -1,0 +1,717 @@
+// dec_kernels.hip -- path B: HIP kernels of the bit-exact fixed-point .cool decoder.
+//
+// Compiled with -fwrapv: every accumulation is int32 with two's-complement wrap,
+// every right shift of a sum is the reference's truncation toward zero
+// (s < 0 ? -((-s) >> p) : s >> p) unless the reference rounds.
+//
+//  dec_arm_kernel   one wavefront per latent-layer CABAC stream (arm_cpu.cpp:18-106,
+//                   cc-bac.h:3-253): raster-order serial decode.  The CABAC state is
+//                   wave-uniform (scalar registers); lane o < d owns MLP neuron o; the
+//                   4 causal rows live in an LDS ring; same-row contexts come from
+//                   registers, so the only per-latent LDS traffic is the above-row
+//                   gather.  Many streams (7 per frame x frames) run concurrently.
+//  dec_ups_level    one launch per pyramid level (ups_refine_cpu.hpp:11-79,
+//                   ups_upsample_cpu.hpp:12-91): integer refine + 2x polyphase upsample
+//                   with the reference's per-pass truncations, LDS-tiled.
+//  dec_syn_fused    1x1+1x1 fused head (synfused_cpu.hpp:17-109 semantics) + 3x3 layers
+//                   (syn_cpu.hpp / synlb_cpu.hpp) with replicate padding, one launch.
+//  dec_syn_layer    generic per-layer integer conv (any ks / widths).
+//  dec_output       444 -> 420/444 8/10-bit or PPM payload (ccdecapi.cpp:59-240).
+#include "ccmi_cabac.h"
+#include "dec_internal.h"
+
+namespace ccmi {
+namespace {
+
+// ------------------------------------------------------------------ context table
+struct CtxPack {
+    uint32_t v[17 * 50 * 2];
+};
+constexpr uint8_t k_ctx_bytes[17 * 50 * 5] = {
+#include "ccmi_ctx_table.inc"
+};
+constexpr CtxPack make_ctx_pack()
+{
+    CtxPack p{};
+    for (int i = 0; i < 17 * 50; ++i) {
+        const uint8_t *s = &k_ctx_bytes[i * 5];
+        p.v[2 * i] = (uint32_t)s[0] | ((uint32_t)s[1] << 8) | ((uint32_t)s[2] << 16) | ((uint32_t)s[3] << 24);
+        p.v[2 * i + 1] = s[4];
+    }
+    return p;
+}
+__constant__ CtxPack c_ctx = make_ctx_pack();
+
+__device__ __forceinline__ int32_t tshift(int32_t s, int p) { return s < 0 ? -((-s) >> p) : s >> p; }
+__device__ __forceinline__ int clampi(int v, int hi) { return v < 0 ? 0 : (v > hi ? hi : v); }
+
+// ------------------------------------------------------------------ device byte source
+struct DevBytes {
+    const uint32_t *p;
+    uint32_t nwords, pos, wi, cur;
+    __device__ __forceinline__ uint32_t next()
+    {
+        const uint32_t i = pos >> 2;
+        if (i != wi) {
+            wi = i;
+            cur = i < nwords ? p[i] : 0u;
+        }
+        const uint32_t b = (cur >> ((pos & 3u) * 8u)) & 0xFFu;
+        ++pos;
+        return b;
+    }
+};
+
+// Sum of v over each DPP row of 16 lanes; the result is valid in lane 15 of the row.
+__device__ __forceinline__ int row_sum16(int v)
+{
+    v += __builtin_amdgcn_update_dpp(0, v, 0x111, 0xF, 0xF, true); // row_shr:1
+    v += __builtin_amdgcn_update_dpp(0, v, 0x112, 0xF, 0xF, true); // row_shr:2
+    v += __builtin_amdgcn_update_dpp(0, v, 0x114, 0xF, 0xF, true); // row_shr:4
+    v += __builtin_amdgcn_update_dpp(0, v, 0x118, 0xF, 0xF, true); // row_shr:8
+    return v;
+}
+
+// Context pixel (dy, dx) of context index i (cc-frame-decoder.cpp:111-154 order).
+template <int D>
+__device__ __forceinline__ void ctx_dydx(int i, int &dy, int &dx)
+{
+    // flattened 9x9 mask index k -> (k/9 - 4, k%9 - 4); same neighbourhoods as the C stride tables
+    constexpr signed char k8[8] = {13, 22, 30, 31, 32, 37, 38, 39};
+    constexpr signed char k16[16] = {13, 14, 20, 21, 22, 23, 24, 28, 29, 30, 31, 32, 33, 37, 38, 39};
+    constexpr signed char k24[24] = {4, 11, 12, 13, 14, 15, 19, 20, 21, 22, 23, 24, 25, 28, 29, 30, 31, 32, 33, 34,
+                                     36, 37, 38, 39};
+    constexpr signed char k32[32] = {2, 3, 4, 5, 10, 11, 12, 13, 14, 15, 16, 19, 20, 21, 22, 23, 24, 25, 26, 27,
+                                     28, 29, 30, 31, 32, 33, 34, 35, 36, 37, 38, 39};
+    int k = 40;
+    if (i < D) k = D == 8 ? k8[i] : D == 16 ? k16[i] : D == 24 ? k24[i] : k32[i];
+    dy = k / 9 - 4;
+    dx = k % 9 - 4;
+}
+
+constexpr int kRing = 5;   // rows y-4 .. y
+constexpr int kPad = 4;    // zero columns either side of a ring row
+
+template <int D, int NH>
+__global__ __launch_bounds__(64) void dec_arm_kernel(const ArmStreamDesc *__restrict__ streams, int pitch)
+{
+    extern __shared__ int32_t smem[];
+    int32_t *ring = smem;                                     // kRing x pitch
+    uint8_t *bmap = reinterpret_cast<uint8_t *>(smem + kRing * pitch); // block sig/flat map
+
+    const ArmStreamDesc S = streams[blockIdx.x];
+    const int lane = threadIdx.x;
+    const int h = S.h, w = S.w;
+
+    for (int i = lane; i < kRing * pitch; i += 64) ring[i] = 0;
+
+    // ---- weights: lane owns neuron o = lane % D (lanes >= D duplicate, masked in sums)
+    const int o = lane % D;
+    int32_t Wh[NH > 0 ? NH : 1][D], Bh[NH > 0 ? NH : 1];
+#pragma unroll
+    for (int l = 0; l < NH; ++l) {
+        const int32_t *base = S.weights + l * (D * D + D);
+#pragma unroll
+        for (int i = 0; i < D; ++i) Wh[l][i] = base[o * D + i];
+        Bh[l] = base[D * D + o];
+    }
+    const int32_t *ob = S.weights + NH * (D * D + D);
+    const int32_t Wo0 = lane < D ? ob[o] : 0, Wo1 = lane < D ? ob[D + o] : 0;
+    const int32_t bo0 = ob[2 * D], bo1 = ob[2 * D + 1];
+
+    // ---- CABAC start + block significance / flat maps (BACContext::set_layer)
+    Cabac<DevBytes> cab;
+    cab.src.p = S.bytes;
+    cab.src.nwords = (S.nbytes + 3) >> 2;
+    cab.src.pos = 0;
+    cab.src.wi = 0xFFFFFFFFu;
+    cab.src.cur = 0;
+    cab.start();
+    const int updated = S.sig_blk < 0;
+    const int blk = S.sig_blk < 0 ? -S.sig_blk : S.sig_blk;
+    int shift = 0;
+    while ((1 << shift) < blk) ++shift;
+    const int mask = (1 << shift) - 1;
+    int nby = 1, nbx = 1;
+    if (blk > 0) {
+        nby = (h + blk - 1) >> shift;
+        nbx = (w + blk - 1) >> shift;
+    }
+    const int nblk = nby * nbx;
+    for (int i = lane; i < nblk; i += 64) bmap[i] = 1; // bit0 sig, bit1 flat
+    __syncthreads();
+    if (nblk > 1) {
+        if (cab.ep()) {
+            Model m;
+            m.init(65);
+            for (int i = 0; i < nblk; ++i) {
+                const uint32_t b = updated ? cab.bin_adaptive(m) : cab.ep();
+                if (lane == 0) bmap[i] = (uint8_t)b;
+            }
+        }
+        __syncthreads();
+        if (cab.ep()) {
+            Model m;
+            m.init(65);
+            for (int i = 0; i < nblk; ++i) {
+                const int sig = __builtin_amdgcn_readfirstlane((int)bmap[i]);
+                if (sig) {
+                    const uint32_t f = updated ? cab.bin_adaptive(m) : cab.ep();
+                    if (lane == 0) bmap[i] = (uint8_t)(sig | (f << 1));
+                }
+            }
+        }
+    }
+    __syncthreads();
+
+    // ---- context geometry of this lane (context index = o)
+    int cdy, cdx;
+    ctx_dydx<D>(o, cdy, cdx);
+    const bool same_row = cdy == 0;
+
+    for (int y = 0; y < h; ++y) {
+        int32_t *row = ring + (y % kRing) * pitch + kPad;
+        const int32_t *up = ring + ((y + kRing - 1) % kRing) * pitch + kPad;
+        const int32_t *crow = ring + ((y + cdy + kRing) % kRing) * pitch + kPad + cdx;
+        int32_t r1 = 0, r2 = 0, r3 = 0, r4 = 0; // decoded values at x-1 .. x-4 (this row)
+        const int brow = blk > 0 ? (y >> shift) * nbx : 0;
+        for (int x = 0; x < w; ++x) {
+            int32_t v;
+            const int bm = blk > 0 ? __builtin_amdgcn_readfirstlane((int)bmap[brow + (x >> shift)]) : 1;
+            if (!(bm & 1)) {
+                v = 0;
+            } else if ((bm & 2) && (x & mask)) {
+                v = r1;
+            } else if ((bm & 2) && (y & mask)) {
+                v = __builtin_amdgcn_readfirstlane(up[x]);
+            } else {
+                int32_t a;
+                if (same_row) a = cdx == -1 ? r1 : cdx == -2 ? r2 : cdx == -3 ? r3 : r4;
+                else a = crow[x];
+#pragma unroll
+                for (int l = 0; l < NH; ++l) {
+                    int32_t acc = Bh[l] + a * 256; // residual
+#pragma unroll
+                    for (int i = 0; i < D; ++i) acc += Wh[l][i] * __builtin_amdgcn_readlane(a, i);
+                    a = acc < 0 ? 0 : (acc + 128) >> 8;
+                }
+                int32_t s0 = row_sum16(Wo0 * a), s1 = row_sum16(Wo1 * a);
+                int32_t m0 = __builtin_amdgcn_readlane(s0, 15), m1 = __builtin_amdgcn_readlane(s1, 15);
+                if (D > 16) {
+                    m0 += __builtin_amdgcn_readlane(s0, 31);
+                    m1 += __builtin_amdgcn_readlane(s1, 31);
+                }
+                m0 += bo0;
+                m1 += bo1;
+                const int32_t mu = m0 < 0 ? -((-m0 + 128) >> 8) : (m0 + 128) >> 8;
+                const int32_t ls = m1 < 0 ? -((-m1 + 128) >> 8) : (m1 + 128) >> 8;
+                // get_val_mu_indicies (cc-contexts.h:20-48)
+                const int32_t mr = mu >= 0 ? ((mu + 128) >> 8) << 8 : -(((-mu + 128) >> 8) << 8);
+                int32_t mi = (mu - mr) * 16;
+                mi = (mi >= 0 ? (mi + 128) >> 8 : -((-mi + 128) >> 8)) + 8;
+                const int32_t lsp = ls + 256;
+                int32_t si = lsp < 0 ? 0 : (lsp * 5 + 128) >> 8;
+                si = si > 49 ? 49 : si;
+                const uint32_t ci = (uint32_t)(mi * 50 + si) * 2u;
+                const uint32_t st = c_ctx.v[ci], stp = c_ctx.v[ci + 1];
+                // decode_single (cc-bac.h:192-231)
+                int32_t val = 0;
+                if (cab.bin_static(st & 0xFF)) {
+                    if (!cab.bin_static((st >> 8) & 0xFF)) val = 1;
+                    else if (!cab.bin_static((st >> 16) & 0xFF)) val = 2;
+                    else if (!cab.bin_static(st >> 24)) val = 3;
+                    else val = cab.expgolomb(0) + 4;
+                    if (cab.bin_static(stp)) val = -val;
+                }
+                v = (int32_t)((uint32_t)((mr >> 8) + val) << kArmPrec);
+            }
+            r4 = r3;
+            r3 = r2;
+            r2 = r1;
+            r1 = v;
+            if (lane == 0) row[x] = v;
+        }
+        __syncthreads();
+        int32_t *dst = S.out + (int64_t)y * w;
+        for (int x = lane; x < w; x += 64) dst[x] = row[x];
+        __syncthreads();
+    }
+}
+
+// ------------------------------------------------------------------ upsampling (integer)
+constexpr int kThreads = 256;
+constexpr int kTY = 16, kTX = 64;
+constexpr int kMaxKs = 16;
+
+struct DecLevel {
+    const int32_t *src;      // level-k stack (or the raw coarsest latent plane)
+    int C, hs, ws, src_prec;
+    const int32_t *ref;      // latent plane of level k-1 (ARM precision)
+    int32_t *dst;            // level k-1 stack: C + 1 channels
+    int hd, wd;
+    const int32_t *kup;      // ksx2 taps
+    int ksx2;
+    const int32_t *kpre;     // ks taps
+    int ks;
+    int tiles_x;
+};
+
+__global__ __launch_bounds__(kThreads) void dec_ups_level(DecLevel A)
+{
+    __shared__ int32_t s_in[(kTY + kMaxKs) * (kTX + kMaxKs)];
+    __shared__ int32_t s_tmp[(kTY + kMaxKs) * kTX];
+    const int y0 = (blockIdx.x / A.tiles_x) * kTY;
+    const int x0 = (blockIdx.x % A.tiles_x) * kTX;
+    const int tid = threadIdx.x;
+    const int64_t dplane = (int64_t)A.hd * A.wd;
+
+    // refine (ups_refine_cpu.hpp): zero padding, two passes with truncation, residual
+    {
+        const int pad = A.ks / 2;
+        const int rh = kTY + 2 * pad, rw = kTX + 2 * pad, pitch = kTX + kMaxKs;
+        for (int i = tid; i < rh * rw; i += kThreads) {
+            const int r = i / rw, c = i - r * rw;
+            const int y = y0 - pad + r, x = x0 - pad + c;
+            s_in[r * pitch + c] = (y >= 0 && y < A.hd && x >= 0 && x < A.wd) ? A.ref[y * A.wd + x] : 0;
+        }
+        __syncthreads();
+        for (int i = tid; i < rh * kTX; i += kThreads) {
+            const int r = i / kTX, c = i - r * kTX;
+            const int y = y0 - pad + r;
+            int32_t acc = 0;
+            for (int k = 0; k < A.ks; ++k) acc += s_in[r * pitch + c + k] * A.kpre[k];
+            // rows outside the plane are the zero padding of the vertical pass
+            s_tmp[r * kTX + c] = (y >= 0 && y < A.hd) ? tshift(acc, kArmPrec) : 0;
+        }
+        __syncthreads();
+        for (int i = tid; i < kTY * kTX; i += kThreads) {
+            const int r = i / kTX, c = i - r * kTX;
+            const int y = y0 + r, x = x0 + c;
+            if (y < A.hd && x < A.wd) {
+                int32_t acc = 0;
+                for (int k = 0; k < A.ks; ++k) acc += s_tmp[(r + k) * kTX + c] * A.kpre[k];
+                acc += (int32_t)((uint32_t)s_in[(r + pad) * pitch + c + pad] << (kUpsPrec - kArmPrec) << kUpsPrec);
+                A.dst[(int64_t)y * A.wd + x] = tshift(acc, kUpsPrec);
+            }
+        }
+        __syncthreads();
+    }
+
+    // 2x upsample of every source channel (ups_upsample_cpu.hpp): replicate padding,
+    // horizontal pass >> src_prec into tmp (2*ws wide), vertical pass >> 12.
+    const int ks = A.ksx2 / 2, pad = ks / 2;
+    const int sy0 = y0 / 2 - pad, sx0 = x0 / 2 - pad;
+    const int sh = kTY / 2 + ks, sw = kTX / 2 + ks, pitch = kTX / 2 + kMaxKs;
+    for (int c = 0; c < A.C; ++c) {
+        const int32_t *sp = A.src + (int64_t)c * A.hs * A.ws;
+        for (int i = tid; i < sh * sw; i += kThreads) {
+            const int r = i / sw, cc = i - r * sw;
+            s_in[r * pitch + cc] = sp[clampi(sy0 + r, A.hs - 1) * A.ws + clampi(sx0 + cc, A.ws - 1)];
+        }
+        __syncthreads();
+        for (int i = tid; i < sh * kTX; i += kThreads) {
+            const int r = i / kTX, cc = i - r * kTX;
+            const int X = x0 + cc, xs = X >> 1, ph = X & 1;
+            int32_t acc = 0;
+            for (int k = 0; k < ks; ++k) acc += s_in[r * pitch + (xs - pad + ph + k - sx0)] * A.kup[2 * k + ph];
+            s_tmp[r * kTX + cc] = tshift(acc, A.src_prec);
+        }
+        __syncthreads();
+        for (int i = tid; i < kTY * kTX; i += kThreads) {
+            const int r = i / kTX, cc = i - r * kTX;
+            const int Y = y0 + r, X = x0 + cc;
+            if (Y < A.hd && X < A.wd) {
+                const int ys = Y >> 1, ph = Y & 1;
+                int32_t acc = 0;
+                for (int k = 0; k < ks; ++k) acc += s_tmp[(ys - pad + ph + k - sy0) * kTX + cc] * A.kup[2 * k + ph];
+                A.dst[(int64_t)(c + 1) * dplane + (int64_t)Y * A.wd + X] = tshift(acc, kUpsPrec);
+            }
+        }
+        __syncthreads();
+    }
+}
+
+// ------------------------------------------------------------------ synthesis (integer)
+constexpr int kRW = 64, kRH = 32, kRegion = kRW * kRH;
+constexpr int kMaxSp = 3;
+
+struct DecSynFused {
+    const int32_t *in;
+    int cin, H, W;
+    int hid;                // fused head width (always ReLU), output linear (synfused semantics)
+    const int32_t *w0, *b0, *w1, *b1;
+    int n_sp;
+    const int32_t *wsp[kMaxSp], *bsp[kMaxSp];
+    int res[kMaxSp], relu[kMaxSp];
+    int32_t *out;
+    int tiles_x;
+};
+
+template <int CIN, int CMID>
+__global__ __launch_bounds__(kThreads) void dec_syn_fused(DecSynFused A)
+{
+    __shared__ int32_t s_buf[2][CMID][kRegion];
+    const int halo = A.n_sp;
+    const int TX = kRW - 2 * halo, TY = kRH - 2 * halo;
+    const int y0 = (blockIdx.x / A.tiles_x) * TY, x0 = (blockIdx.x % A.tiles_x) * TX;
+    const int oy = y0 - halo, ox = x0 - halo;
+    const int64_t plane = (int64_t)A.H * A.W;
+    const int c = threadIdx.x & (kRW - 1), r0 = threadIdx.x >> 6;
+    const int gx = ox + c, cxg = clampi(gx, A.W - 1);
+
+    for (int r = r0; r < kRH; r += 4) {
+        const int64_t pix = (int64_t)clampi(oy + r, A.H - 1) * A.W + cxg;
+        int32_t x[CIN];
+#pragma unroll
+        for (int k = 0; k < CIN; ++k) x[k] = A.in[k * plane + pix];
+        int32_t o[CMID];
+#pragma unroll
+        for (int m = 0; m < CMID; ++m) o[m] = A.b1[m];
+        for (int j = 0; j < A.hid; ++j) {
+            int32_t acc = A.b0[j];
+#pragma unroll
+            for (int k = 0; k < CIN; ++k) acc += x[k] * A.w0[j * CIN + k];
+            acc = acc < 0 ? 0 : acc >> kSynPrec;
+#pragma unroll
+            for (int m = 0; m < CMID; ++m) o[m] += acc * A.w1[m * A.hid + j];
+        }
+        const int gy = oy + r;
+#pragma unroll
+        for (int m = 0; m < CMID; ++m) {
+            const int32_t v = tshift(o[m], kSynPrec);
+            if (halo == 0) {
+                if (gy < A.H && gx < A.W) A.out[m * plane + (int64_t)gy * A.W + gx] = v;
+            } else {
+                s_buf[0][m][r * kRW + c] = v;
+            }
+        }
+    }
+    if (halo == 0) return;
+
+    int cur = 0;
+    for (int s = 0; s < A.n_sp; ++s) {
+        __syncthreads();
+        const int t = s + 1;
+        const bool last = s == A.n_sp - 1;
+        const int32_t *wt = A.wsp[s], *bs = A.bsp[s];
+        const bool col_ok = c >= t && c < kRW - t;
+        int lx[3];
+#pragma unroll
+        for (int d = 0; d < 3; ++d) lx[d] = clampi(cxg + d - 1, A.W - 1) - ox;
+        for (int r = r0 + t; r < kRH - t; r += 4) {
+            const int gy = oy + r;
+            if (!col_ok || (last && (gy >= A.H || gx >= A.W))) continue;
+            const int cyg = clampi(gy, A.H - 1);
+            int ly[3];
+#pragma unroll
+            for (int d = 0; d < 3; ++d) ly[d] = (clampi(cyg + d - 1, A.H - 1) - oy) * kRW;
+            int32_t nb[CMID][3][3];
+#pragma unroll
+            for (int k = 0; k < CMID; ++k)
+#pragma unroll
+                for (int dy = 0; dy < 3; ++dy)
+#pragma unroll
+                    for (int dx = 0; dx < 3; ++dx) nb[k][dy][dx] = s_buf[cur][k][ly[dy] + lx[dx]];
+#pragma unroll
+            for (int m = 0; m < CMID; ++m) {
+                int32_t acc = bs[m];
+                if (A.res[s]) acc += (int32_t)((uint32_t)nb[m][1][1] << kSynPrec);
+#pragma unroll
+                for (int k = 0; k < CMID; ++k)
+#pragma unroll
+                    for (int dy = 0; dy < 3; ++dy)
+#pragma unroll
+                        for (int dx = 0; dx < 3; ++dx) acc += nb[k][dy][dx] * wt[((m * CMID + k) * 3 + dy) * 3 + dx];
+                const int32_t v = acc < 0 ? (A.relu[s] ? 0 : -((-acc) >> kSynPrec)) : acc >> kSynPrec;
+                if (last)
+                    A.out[m * plane + (int64_t)gy * A.W + gx] = v;
+                else
+                    s_buf[cur ^ 1][m][r * kRW + c] = v;
+            }
+        }
+        cur ^= 1;
+    }
+}
+
+// generic integer conv layer (syn_cpu.hpp semantics, out-of-place, replicate padding).
+// fused_hidden > 0: this launch is the fused 1x1 pair with that hidden width.
+__global__ __launch_bounds__(kThreads) void dec_syn_layer(const int32_t *__restrict__ in, int cin, int H, int W,
+                                                          const int32_t *__restrict__ wt,
+                                                          const int32_t *__restrict__ bs, int nout, int ks,
+                                                          int residual, int relu, int32_t *__restrict__ out)
+{
+    const int64_t plane = (int64_t)H * W;
+    const int64_t p = (int64_t)blockIdx.x * kThreads + threadIdx.x;
+    if (p >= plane) return;
+    const int y = (int)(p / W), x = (int)(p - (int64_t)y * W);
+    const int pad = ks / 2;
+    for (int m = 0; m < nout; ++m) {
+        int32_t acc = bs[m];
+        if (residual) acc += (int32_t)((uint32_t)in[m * plane + p] << kSynPrec);
+        for (int k = 0; k < cin; ++k)
+            for (int dy = 0; dy < ks; ++dy) {
+                const int yy = clampi(y + dy - pad, H - 1);
+                for (int dx = 0; dx < ks; ++dx)
+                    acc += in[k * plane + (int64_t)yy * W + clampi(x + dx - pad, W - 1)] *
+                           wt[((m * cin + k) * ks + dy) * ks + dx];
+            }
+        out[m * plane + p] = acc < 0 ? (relu ? 0 : -((-acc) >> kSynPrec)) : acc >> kSynPrec;
+    }
+}
+
+__global__ __launch_bounds__(kThreads) void dec_syn_fused_generic(const int32_t *__restrict__ in, int cin, int64_t plane,
+                                                                  const int32_t *__restrict__ w0,
+                                                                  const int32_t *__restrict__ b0, int hid,
+                                                                  const int32_t *__restrict__ w1,
+                                                                  const int32_t *__restrict__ b1, int nout,
+                                                                  int32_t *__restrict__ out)
+{
+    const int64_t p = (int64_t)blockIdx.x * kThreads + threadIdx.x;
+    if (p >= plane) return;
+    for (int m = 0; m < nout; ++m) {
+        int32_t o = b1[m];
+        for (int j = 0; j < hid; ++j) {
+            int32_t acc = b0[j];
+            for (int k = 0; k < cin; ++k) acc += in[k * plane + p] * w0[j * cin + k];
+            acc = acc < 0 ? 0 : acc >> kSynPrec;
+            o += acc * w1[m * hid + j];
+        }
+        out[m * plane + p] = tshift(o, kSynPrec);
+    }
+}
+
+__global__ __launch_bounds__(kThreads) void dec_blend_kernel(int32_t *acc, const int32_t *x, int64_t n, int32_t b_acc,
+                                                             int32_t b_x, int first)
+{
+    const int64_t i = (int64_t)blockIdx.x * kThreads + threadIdx.x;
+    if (i >= n) return;
+    auto cl = [](int32_t v) { return v < 0 ? 0 : (v > (1 << kSynPrec) ? (1 << kSynPrec) : v); };
+    const int32_t x0 = cl(x[i]);
+    if (first) acc[i] = (cl(acc[i]) * b_acc + x0 * b_x) >> kSynPrec;
+    else acc[i] = acc[i] + ((x0 * b_x) >> kSynPrec);
+}
+
+// ------------------------------------------------------------------ output bytes
+__global__ __launch_bounds__(kThreads) void dec_output_kernel(const int32_t *__restrict__ syn, int H, int W, int maxv,
+                                                              int kind, int bps, uint8_t *__restrict__ dst)
+{
+    const int64_t plane = (int64_t)H * W;
+    const int64_t p = (int64_t)blockIdx.x * kThreads + threadIdx.x;
+    if (p >= plane) return;
+    auto smp = [maxv](int32_t v) {
+        int32_t s = (v * maxv + (1 << (kSynPrec - 1))) >> kSynPrec;
+        return s < 0 ? 0 : (s > maxv ? maxv : s);
+    };
+    auto put = [&](int64_t idx, int32_t s, bool big_endian) {
+        if (bps == 1) dst[idx] = (uint8_t)s;
+        else if (big_endian) { dst[2 * idx] = (uint8_t)(s >> 8); dst[2 * idx + 1] = (uint8_t)s; }
+        else { dst[2 * idx] = (uint8_t)s; dst[2 * idx + 1] = (uint8_t)(s >> 8); }
+    };
+    const int y = (int)(p / W), x = (int)(p - (int64_t)y * W);
+    if (kind == 2) { // PPM: interleaved RGB, 16-bit big endian
+        for (int c = 0; c < 3; ++c) put(3 * p + c, smp(syn[c * plane + p]), true);
+        return;
+    }
+    put(p, smp(syn[p]), false);
+    if (kind == 1) {
+        put(plane + p, smp(syn[plane + p]), false);
+        put(2 * plane + p, smp(syn[2 * plane + p]), false);
+    } else if (!(y & 1) && !(x & 1) && (y >> 1) < H / 2 && (x >> 1) < W / 2) {
+        const int64_t cp = (int64_t)(H / 2) * (W / 2), ci = (int64_t)(y >> 1) * (W / 2) + (x >> 1);
+        put(plane + ci, smp(syn[plane + p]), false);
+        put(plane + cp + ci, smp(syn[2 * plane + p]), false);
+    }
+}
+
+} // namespace
+
+// ------------------------------------------------------------------ launchers
+int launch_dec_arm(const ArmStreamDesc *d_streams, int n_streams, int max_w, int max_blocks, int d, int nh,
+                         hipStream_t s)
+{
+    const int pitch = max_w + 2 * kPad;
+    const size_t lds = sizeof(int32_t) * kRing * pitch + ((size_t)max_blocks + 16);
+    if (lds > 160 * 1024) return ccmi_set_error(CCMI_ERR_UNSUPPORTED, "dec: latent width %d too large for LDS ring", max_w);
+#define CCMI_ARM_CASE(DD, NN)                                                                                   \
+    if (d == DD && nh == NN) {                                                                                  \
+        hipLaunchKernelGGL((dec_arm_kernel<DD, NN>), dim3(n_streams), dim3(64), lds, s, d_streams, pitch);      \
+        CCMI_HIP_CHECK(hipGetLastError());                                                                      \
+        return CCMI_OK;                                                                                         \
+    }
+#define CCMI_ARM_D(DD) CCMI_ARM_CASE(DD, 0) CCMI_ARM_CASE(DD, 1) CCMI_ARM_CASE(DD, 2) CCMI_ARM_CASE(DD, 3) CCMI_ARM_CASE(DD, 4)
+    CCMI_ARM_D(8)
+    CCMI_ARM_D(16)
+    CCMI_ARM_D(24)
+    CCMI_ARM_D(32)
+#undef CCMI_ARM_D
+#undef CCMI_ARM_CASE
+    return ccmi_set_error(CCMI_ERR_UNSUPPORTED, "dec: ARM with d=%d, %d hidden layers not supported", d, nh);
+}
+
+size_t dec_ups_workspace_elems(const int *lh, const int *lw, int L)
+{
+    size_t n = 0;
+    for (int k = 1; k <= L - 2; ++k) n += (size_t)(L - k) * lh[k] * lw[k];
+    return n;
+}
+
+int launch_dec_ups(const DecUpsArgs &a, hipStream_t s)
+{
+    const int L = a.n_layers;
+    if (a.ups_ks < 2 || a.ups_ks > kMaxKs || a.pre_ks < 1 || a.pre_ks > kMaxKs - 1)
+        return ccmi_set_error(CCMI_ERR_UNSUPPORTED, "dec: upsampling kernel sizes %d/%d", a.ups_ks, a.pre_ks);
+    int32_t *stack[CCMI_MAX_GRIDS] = {};
+    int32_t *ws = a.workspace;
+    for (int k = 1; k <= L - 2; ++k) {
+        stack[k] = ws;
+        ws += (size_t)(L - k) * a.lh[k] * a.lw[k];
+    }
+    for (int step = 0; step < L - 1; ++step) {
+        const int k = L - 1 - step;
+        DecLevel A{};
+        A.src = k == L - 1 ? a.lat + a.off[k] : stack[k];
+        A.C = L - k;
+        A.hs = a.lh[k];
+        A.ws = a.lw[k];
+        A.src_prec = k == L - 1 ? kArmPrec : kUpsPrec;
+        A.ref = a.lat + a.off[k - 1];
+        A.dst = k - 1 == 0 ? a.out : stack[k - 1];
+        A.hd = a.lh[k - 1];
+        A.wd = a.lw[k - 1];
+        // reference indices: ups layer (L-2-target)%n_ups, preconcat (L-2-layer)%n_pre; target = layer = k-1
+        A.kup = a.kernels + ((L - 2 - (k - 1)) % a.n_ups) * a.ups_ks;
+        A.ksx2 = a.ups_ks;
+        A.kpre = a.kernels + a.n_ups * a.ups_ks + ((L - 2 - (k - 1)) % a.n_pre) * a.pre_ks;
+        A.ks = a.pre_ks;
+        A.tiles_x = ccmi_div_up(A.wd, kTX);
+        hipLaunchKernelGGL(dec_ups_level, dim3(A.tiles_x * ccmi_div_up(A.hd, kTY)), dim3(kThreads), 0, s, A);
+        CCMI_HIP_CHECK(hipGetLastError());
+    }
+    return CCMI_OK;
+}
+
+static int syn_maxc(const DecSynArgs &a)
+{
+    int m = a.c_in;
+    for (int l = 0; l < a.n_layers; ++l) m = a.layers[l].n_out > m ? a.layers[l].n_out : m;
+    return m;
+}
+
+static bool syn_fast(const DecSynArgs &a, int *cmid)
+{
+    if (a.n_layers < 2 || a.layers[0].ks != 1 || a.layers[1].ks != 1) return false;
+    if (a.c_in < 1 || a.c_in > 8) return false;
+    const int cm = a.layers[1].n_out;
+    if (cm != 3) return false;
+    if (a.n_layers - 2 > kMaxSp) return false;
+    for (int l = 2; l < a.n_layers; ++l)
+        if (a.layers[l].ks != 3 || a.layers[l].n_out != cm) return false;
+    *cmid = cm;
+    return true;
+}
+
+size_t dec_syn_workspace_elems(const DecSynArgs &a)
+{
+    int cm;
+    if (syn_fast(a, &cm)) return 0;
+    return 2 * (size_t)syn_maxc(a) * a.h * a.w;
+}
+
+int launch_dec_syn(const DecSynArgs &a, hipStream_t s)
+{
+    // weight offsets (per layer W then b)
+    const int32_t *wp[CCMI_MAX_SYN_LAYERS], *bp[CCMI_MAX_SYN_LAYERS];
+    int cin_of[CCMI_MAX_SYN_LAYERS];
+    {
+        const int32_t *q = a.params;
+        int c = a.c_in;
+        for (int l = 0; l < a.n_layers; ++l) {
+            cin_of[l] = c;
+            wp[l] = q;
+            q += (size_t)a.layers[l].n_out * c * a.layers[l].ks * a.layers[l].ks;
+            bp[l] = q;
+            q += a.layers[l].n_out;
+            c = a.layers[l].n_out;
+        }
+    }
+    int cm;
+    if (syn_fast(a, &cm)) {
+        DecSynFused F{};
+        F.in = a.in;
+        F.cin = a.c_in;
+        F.H = a.h;
+        F.W = a.w;
+        F.hid = a.layers[0].n_out;
+        F.w0 = wp[0];
+        F.b0 = bp[0];
+        F.w1 = wp[1];
+        F.b1 = bp[1];
+        F.n_sp = a.n_layers - 2;
+        for (int i = 0; i < F.n_sp; ++i) {
+            F.wsp[i] = wp[2 + i];
+            F.bsp[i] = bp[2 + i];
+            F.res[i] = a.layers[2 + i].residual;
+            F.relu[i] = a.layers[2 + i].relu;
+        }
+        F.out = a.out;
+        const int halo = F.n_sp;
+        F.tiles_x = ccmi_div_up(a.w, kRW - 2 * halo);
+        dim3 grid(F.tiles_x * ccmi_div_up(a.h, kRH - 2 * halo));
+        switch (a.c_in) {
+        case 1: hipLaunchKernelGGL((dec_syn_fused<1, 3>), grid, dim3(kThreads), 0, s, F); break;
+        case 2: hipLaunchKernelGGL((dec_syn_fused<2, 3>), grid, dim3(kThreads), 0, s, F); break;
+        case 3: hipLaunchKernelGGL((dec_syn_fused<3, 3>), grid, dim3(kThreads), 0, s, F); break;
+        case 4: hipLaunchKernelGGL((dec_syn_fused<4, 3>), grid, dim3(kThreads), 0, s, F); break;
+        case 5: hipLaunchKernelGGL((dec_syn_fused<5, 3>), grid, dim3(kThreads), 0, s, F); break;
+        case 6: hipLaunchKernelGGL((dec_syn_fused<6, 3>), grid, dim3(kThreads), 0, s, F); break;
+        case 7: hipLaunchKernelGGL((dec_syn_fused<7, 3>), grid, dim3(kThreads), 0, s, F); break;
+        default: hipLaunchKernelGGL((dec_syn_fused<8, 3>), grid, dim3(kThreads), 0, s, F); break;
+        }
+        CCMI_HIP_CHECK(hipGetLastError());
+        return CCMI_OK;
+    }
+    // generic: the reference fuses the first two layers whenever both are 1x1 (can_fuse)
+    const int64_t plane = (int64_t)a.h * a.w;
+    const int maxc = syn_maxc(a);
+    int32_t *bufs[2] = {a.workspace, a.workspace + (size_t)maxc * plane};
+    const int32_t *src = a.in;
+    dim3 grid((unsigned)((plane + kThreads - 1) / kThreads));
+    int l = 0, k = 0;
+    while (l < a.n_layers) {
+        const bool fused = l == 0 && a.n_layers >= 2 && a.layers[0].ks == 1 && a.layers[1].ks == 1;
+        const int last_layer = fused ? 1 : l;
+        int32_t *dst = last_layer == a.n_layers - 1 ? a.out : bufs[k & 1];
+        if (fused) {
+            hipLaunchKernelGGL(dec_syn_fused_generic, grid, dim3(kThreads), 0, s, src, cin_of[0], plane, wp[0], bp[0],
+                               a.layers[0].n_out, wp[1], bp[1], a.layers[1].n_out, dst);
+        } else {
+            const SynLayerDesc &L = a.layers[l];
+            hipLaunchKernelGGL(dec_syn_layer, grid, dim3(kThreads), 0, s, src, cin_of[l], a.h, a.w, wp[l], bp[l],
+                               L.n_out, L.ks, L.residual, L.relu, dst);
+        }
+        CCMI_HIP_CHECK(hipGetLastError());
+        src = dst;
+        l = last_layer + 1;
+        ++k;
+    }
+    return CCMI_OK;
+}
+
+int launch_dec_blend(int32_t *acc, const int32_t *x, int64_t n, int32_t b_acc, int32_t b_x, int first, hipStream_t s)
+{
+    hipLaunchKernelGGL(dec_blend_kernel, dim3((unsigned)((n + kThreads - 1) / kThreads)), dim3(kThreads), 0, s, acc, x,
+                       n, b_acc, b_x, first);
+    CCMI_HIP_CHECK(hipGetLastError());
+    return CCMI_OK;
+}
+
+int launch_dec_output(const int32_t *syn, int h, int w, int bitdepth, int kind, uint8_t *dst, hipStream_t s)
+{
+    const int64_t plane = (int64_t)h * w;
+    hipLaunchKernelGGL(dec_output_kernel, dim3((unsigned)((plane + kThreads - 1) / kThreads)), dim3(kThreads), 0, s,
+                       syn, h, w, (1 << bitdepth) - 1, kind, bitdepth <= 8 ? 1 : 2, dst);
+    CCMI_HIP_CHECK(hipGetLastError());
+    return CCMI_OK;
+}
+
+} // namespace ccmi
