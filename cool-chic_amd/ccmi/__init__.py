@@ -23,7 +23,7 @@ OK, ERR_ARG, ERR_HIP, ERR_UNSUPPORTED, ERR_BITSTREAM, ERR_IO = range(6)
 # Public symbols of include/ccmi.h (checked by tests/test_abi.py).
 EXPORTED = [
     "ccmi_last_error", "ccmi_version", "ccmi_device_count",
-    "ccmi_arm_forward_f32", "ccmi_ups_workspace_bytes", "ccmi_ups_forward_f32",
+    "ccmi_arm_forward_f32", "ccmi_arm_context_f32", "ccmi_arm_mlp_f32", "ccmi_ups_workspace_bytes", "ccmi_ups_forward_f32",
     "ccmi_syn_workspace_bytes", "ccmi_syn_forward_f32", "ccmi_post_f32",
     "ccmi_decode_file", "ccmi_decode_batch", "ccmi_decode_output_size",
 ]
@@ -101,6 +101,11 @@ def lib() -> C.CDLL:
         f = getattr(L, name)
         f.argtypes = [C.POINTER(st), C.c_void_p]
         f.restype = C.c_int
+    L.ccmi_arm_context_f32.argtypes = [C.c_void_p, C.c_int, C.c_int, C.c_int, C.c_int, C.c_void_p, C.c_void_p]
+    L.ccmi_arm_context_f32.restype = C.c_int
+    L.ccmi_arm_mlp_f32.argtypes = [C.c_void_p, C.c_int64, C.c_int, C.c_int, C.c_void_p, C.c_void_p, C.c_void_p,
+                                   C.c_void_p, C.c_void_p]
+    L.ccmi_arm_mlp_f32.restype = C.c_int
     L.ccmi_ups_workspace_bytes.argtypes = [C.c_int, C.POINTER(C.c_int), C.POINTER(C.c_int), C.c_int]
     L.ccmi_ups_workspace_bytes.restype = C.c_size_t
     L.ccmi_syn_workspace_bytes.argtypes = [C.POINTER(SynArgs)]

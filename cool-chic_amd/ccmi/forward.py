@@ -48,8 +48,13 @@ def pack_syn(layers: Sequence[tuple[torch.Tensor, torch.Tensor]]) -> torch.Tenso
     return torch.cat([t.reshape(-1).float() for wb in layers for t in wb])
 
 
-def _as_batch(params: torch.Tensor) -> torch.Tensor:
-    return params.unsqueeze(0) if params.dim() == 1 else params
+def _as_batch(params: torch.Tensor, B: int):
+    """[P] -> shared by every frame (stride 0); [B, P] -> one parameter block per frame."""
+    if params.dim() == 1:
+        return params.unsqueeze(0), 0
+    if params.shape[0] != B:
+        raise ValueError(f"params: expected {B} parameter rows, got {params.shape[0]}")
+    return params, params.shape[1]
 
 
 def arm_forward(latent: torch.Tensor, sizes, params: torch.Tensor, dim_arm: int, n_hidden: int,
@@ -57,12 +62,12 @@ def arm_forward(latent: torch.Tensor, sizes, params: torch.Tensor, dim_arm: int,
     """latent [B, N] (or [N]) flat grids; params [B, P] (or [P]).  Returns dict of [B, N] tensors."""
     squeeze = latent.dim() == 1
     latent = latent.unsqueeze(0) if squeeze else latent
-    params = _as_batch(params)
-    require_cuda(latent, params)
     B, N = latent.shape
+    params, pstride = _as_batch(params, B)
+    require_cuda(latent, params)
     if N != n_latents(sizes):
         raise ValueError(f"latent has {N} values, grids hold {n_latents(sizes)}")
-    if params.shape[0] != B or params.shape[1] < arm_param_count(dim_arm, n_hidden):
+    if params.shape[1] < arm_param_count(dim_arm, n_hidden):
         raise ValueError("arm params: expected [B, >=%d]" % arm_param_count(dim_arm, n_hidden))
     latent = latent.float().contiguous()
     params = params.float().contiguous()
@@ -70,7 +75,7 @@ def arm_forward(latent: torch.Tensor, sizes, params: torch.Tensor, dim_arm: int,
     h, w = _grid_arrays(sizes)
     a = ArmArgs(latent=ptr(latent), latent_stride=N, n_grids=len(sizes), h=h, w=w, gain=float(gain),
                 quantize=int(bool(quantize)), dim_arm=dim_arm, n_hidden=n_hidden, params=ptr(params),
-                param_stride=params.shape[1], mu=ptr(outs.get("mu")), scale=ptr(outs.get("scale")),
+                param_stride=pstride, mu=ptr(outs.get("mu")), scale=ptr(outs.get("scale")),
                 log_scale=ptr(outs.get("log_scale")), rate=ptr(outs.get("rate")), out_stride=N, batch=B)
     check(lib().ccmi_arm_forward_f32(a, stream_handle(latent.device)))
     if squeeze:
@@ -83,12 +88,12 @@ def ups_forward(latent: torch.Tensor, sizes, params: torch.Tensor, ups_k: int, n
     """latent [B, N] flat grids -> [B, L, H, W] dense synthesis input."""
     squeeze = latent.dim() == 1
     latent = latent.unsqueeze(0) if squeeze else latent
-    params = _as_batch(params)
-    require_cuda(latent, params)
     B, N = latent.shape
+    params, pstride = _as_batch(params, B)
+    require_cuda(latent, params)
     if N != n_latents(sizes):
         raise ValueError(f"latent has {N} values, grids hold {n_latents(sizes)}")
-    if params.shape[0] != B or params.shape[1] < n_ups * ups_k + n_pre * pre_k:
+    if params.shape[1] < n_ups * ups_k + n_pre * pre_k:
         raise ValueError("ups params: wrong shape")
     latent = latent.float().contiguous()
     params = params.float().contiguous()
@@ -100,20 +105,20 @@ def ups_forward(latent: torch.Tensor, sizes, params: torch.Tensor, ups_k: int, n
     ws = torch.empty(max(nws, 4), device=latent.device, dtype=torch.uint8)
     a = UpsArgs(latent=ptr(latent), latent_stride=N, n_grids=L, h=h, w=w, gain=float(gain),
                 quantize=int(bool(quantize)), ups_k=ups_k, n_ups=n_ups, pre_k=pre_k, n_pre=n_pre,
-                params=ptr(params), param_stride=params.shape[1], out=ptr(out), out_stride=L * H * W,
+                params=ptr(params), param_stride=pstride, out=ptr(out), out_stride=L * H * W,
                 workspace=ptr(ws), workspace_bytes=nws, batch=B)
     check(lib().ccmi_ups_forward_f32(a, stream_handle(latent.device)))
     return out[0] if squeeze else out
 
 
-def _syn_args(x, layers, params, out, B, C, H, W):
+def _syn_args(x, layers, params, out, B, C, H, W, pstride=None):
     if len(layers) > MAX_SYN_LAYERS:
         raise ValueError("too many synthesis layers")
     arr = (SynLayer * MAX_SYN_LAYERS)()
     for i, (n_out, ks, res, relu) in enumerate(layers):
         arr[i] = SynLayer(int(n_out), int(ks), int(bool(res)), int(bool(relu)))
     return SynArgs(in_=ptr(x), in_stride=C * H * W, c_in=C, h=H, w=W, n_layers=len(layers), layers=arr,
-                   params=ptr(params), param_stride=params.shape[1], out=ptr(out),
+                   params=ptr(params), param_stride=params.shape[1] if pstride is None else pstride, out=ptr(out),
                    out_stride=out.shape[1] * H * W, workspace=None, workspace_bytes=0, batch=B)
 
 
@@ -129,15 +134,15 @@ def syn_forward(x: torch.Tensor, layers, params: torch.Tensor) -> torch.Tensor:
     """x [B, C, H, W]; layers [(n_out, ks, residual, relu)]; params [B, P] -> [B, n_out_last, H, W]."""
     squeeze = x.dim() == 3
     x = x.unsqueeze(0) if squeeze else x
-    params = _as_batch(params)
-    require_cuda(x, params)
     B, Cc, H, W = x.shape
-    if params.shape[0] != B or params.shape[1] < syn_param_count(Cc, layers):
+    params, pstride = _as_batch(params, B)
+    require_cuda(x, params)
+    if params.shape[1] < syn_param_count(Cc, layers):
         raise ValueError("syn params: wrong shape")
     x = x.float().contiguous()
     params = params.float().contiguous()
     out = torch.empty(B, int(layers[-1][0]), H, W, device=x.device, dtype=torch.float32)
-    a = _syn_args(x, layers, params, out, B, Cc, H, W)
+    a = _syn_args(x, layers, params, out, B, Cc, H, W, pstride)
     nws = lib().ccmi_syn_workspace_bytes(a)
     ws = None
     if nws:
@@ -174,3 +179,28 @@ def split_420(flat: torch.Tensor, H: int, W: int) -> dict:
     u = flat[..., H * W: H * W + hc * wc].reshape(*lead, hc, wc)
     v = flat[..., H * W + hc * wc:].reshape(*lead, hc, wc)
     return {"y": y, "u": u, "v": v}
+
+
+def arm_context(grid: torch.Tensor, dim_arm: int) -> torch.Tensor:
+    """_get_neighbor on device: grid [B, H, W] (or [H, W]) -> [B, H*W, dim_arm]."""
+    squeeze = grid.dim() == 2
+    grid = grid.unsqueeze(0) if squeeze else grid
+    require_cuda(grid)
+    grid = grid.float().contiguous()
+    B, H, W = grid.shape
+    out = torch.empty(B, H * W, dim_arm, device=grid.device, dtype=torch.float32)
+    check(lib().ccmi_arm_context_f32(ptr(grid), B, H, W, dim_arm, ptr(out), stream_handle(grid.device)))
+    return out[0] if squeeze else out
+
+
+def arm_mlp(ctx: torch.Tensor, params: torch.Tensor, dim_arm: int, n_hidden: int):
+    """Arm.forward on device: contexts [..., M, dim_arm] -> (mu, scale, log_scale) [..., M]."""
+    require_cuda(ctx, params)
+    lead = ctx.shape[:-1]
+    flat = ctx.reshape(-1, dim_arm).float().contiguous()
+    params = params.float().contiguous()
+    m = flat.shape[0]
+    mu, sc, ls = (torch.empty(m, device=ctx.device, dtype=torch.float32) for _ in range(3))
+    check(lib().ccmi_arm_mlp_f32(ptr(flat), m, dim_arm, n_hidden, ptr(params), ptr(mu), ptr(sc), ptr(ls),
+                                 stream_handle(ctx.device)))
+    return mu.view(lead), sc.view(lead), ls.view(lead)

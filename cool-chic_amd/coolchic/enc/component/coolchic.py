@@ -1,0 +1,189 @@
+"""CoolChicEncoder (reference: coolchic/enc/component/coolchic.py).
+
+Same constructor parameters, sub-modules and state_dict layout as the reference.
+``forward`` in eval mode is the hot path, run entirely by libccmi HIP kernels:
+  quantise + ARM context + MLP + Laplace rate -> ccmi_arm_forward_f32 (one launch),
+  upsampling pyramid                           -> ccmi_ups_forward_f32 (one launch / level),
+  synthesis                                    -> ccmi_syn_forward_f32 (one fused launch).
+``forward_batch`` decodes many independent encoders (each with its own weights) of the
+same size and architecture in one launch sequence.
+"""
+
+import math
+from dataclasses import dataclass, field, fields
+from typing import Any, Dict, List, Optional, OrderedDict, Sequence, Tuple
+
+import torch
+from torch import Tensor, nn
+
+from ccmi import forward as _F
+from coolchic.enc.component.core.arm import Arm, _get_non_zero_pixel_ctx_index
+from coolchic.enc.component.core.synthesis import Synthesis
+from coolchic.enc.component.core.upsampling import Upsampling
+
+MAX_ARM_MASK_SIZE = 9
+
+
+@dataclass
+class CoolChicEncoderParameter:
+    """coolchic.py:55-124."""
+
+    layers_synthesis: List[str]
+    n_ft_per_res: List[int]
+    dim_arm: int = 24
+    n_hidden_layers_arm: int = 2
+    encoder_gain: int = 16
+    ups_k_size: int = 8
+    ups_preconcat_k_size: int = 7
+    latent_n_grids: int = field(init=False)
+    img_size: Optional[Tuple[int, int]] = field(init=False, default=None)
+
+    def __post_init__(self):
+        self.latent_n_grids = len(self.n_ft_per_res)
+
+    def set_image_size(self, img_size: Tuple[int, int]) -> None:
+        self.img_size = img_size
+
+    def pretty_string(self) -> str:
+        s = "CoolChicEncoderParameter value:\n-------------------------------\n"
+        for k in fields(self):
+            s += f"{k.name:<25}: {str(getattr(self, k.name)):<80}\n"
+        return s + "\n"
+
+
+@dataclass
+class CoolChicEncoderOutput:
+    raw_out: Tensor
+    rate: Tensor
+    additional_data: Dict[str, Any]
+
+
+class CoolChicLatentGrid(nn.Module):
+    """One latent resolution (coolchic.py:144-151)."""
+
+    def __init__(self, data: torch.Tensor):
+        super().__init__()
+        self.data = nn.Parameter(data, requires_grad=True)
+
+
+class CoolChicEncoder(nn.Module):
+    """coolchic.py:154-795 (decode-side forward)."""
+
+    def __init__(self, param: CoolChicEncoderParameter):
+        super().__init__()
+        self.param = param
+        assert param.img_size is not None, "call param.set_image_size((H, W)) first"
+        if any(c != 1 for c in param.n_ft_per_res):
+            raise NotImplementedError("n_ft_per_res must be all 1 (as the reference decoder requires)")
+        self.encoder_gains = param.encoder_gain
+        self.size_per_latent = []
+        self.latent_grids = nn.ModuleList()
+        for i in range(param.latent_n_grids):
+            h, w = [int(math.ceil(x / (2 ** i))) for x in param.img_size]
+            self.size_per_latent.append((1, param.n_ft_per_res[i], h, w))
+            self.latent_grids.append(CoolChicLatentGrid(torch.zeros(1, param.n_ft_per_res[i], h, w)))
+        self.synthesis = Synthesis(sum(s[1] for s in self.size_per_latent), param.layers_synthesis)
+        self.upsampling = Upsampling(param.ups_k_size, param.ups_preconcat_k_size, param.latent_n_grids - 1,
+                                     param.latent_n_grids - 1)
+        self.mask_size = MAX_ARM_MASK_SIZE
+        self.register_buffer("non_zero_pixel_ctx_index", _get_non_zero_pixel_ctx_index(param.dim_arm),
+                             persistent=False)
+        self.arm = Arm(param.dim_arm, param.n_hidden_layers_arm)
+        self.modules_to_send = ["arm", "upsampling", "synthesis"]
+
+    @property
+    def grid_sizes(self) -> List[Tuple[int, int]]:
+        return [(s[2], s[3]) for s in self.size_per_latent]
+
+    def flat_latent(self) -> Tensor:
+        B = self.latent_grids[0].data.shape[0]
+        return torch.cat([g.data.reshape(B, -1) for g in self.latent_grids], dim=1)
+
+    def forward(self, quantizer_noise_type: str = "kumaraswamy", quantizer_type: str = "softround",
+                soft_round_temperature: Optional[Tensor] = torch.tensor(0.3),
+                noise_parameter: Optional[Tensor] = torch.tensor(1.0), AC_MAX_VAL: int = -1,
+                flag_additional_outputs: bool = False) -> Tuple[Tensor, Tensor, Dict[str, Any]]:
+        """Eval forward (coolchic.py:291-479): returns raw synthesis output [B, C, H, W],
+        rate [B, N] in bits and the optional per-grid detail dictionary."""
+        if self.training:
+            raise NotImplementedError("training-mode forward (noisy / soft quantisers, autograd) is not "
+                                      "implemented on the HIP path yet; call .eval() for decoding")
+        return forward_batch([self], AC_MAX_VAL=AC_MAX_VAL, flag_additional_outputs=flag_additional_outputs)
+
+    # ---------------------------------------------------------------- parameters
+    def get_param(self) -> "OrderedDict[str, Tensor]":
+        return OrderedDict({k: v.detach().clone() for k, v in self.named_parameters()})
+
+    def set_param(self, param) -> None:
+        self.load_state_dict(param)
+
+    def initialize_latent_grids(self, zeros: bool = True, random_seed: Optional[int] = None) -> None:
+        g = None if zeros else torch.Generator().manual_seed(random_seed)
+        for i, lat in enumerate(self.latent_grids):
+            d = lat.data
+            self.latent_grids[i] = CoolChicLatentGrid(
+                torch.zeros_like(d) if zeros else 1e-2 * torch.randn(d.shape, generator=g))
+
+    def reinitialize_parameters(self) -> None:
+        self.arm.reinitialize_parameters()
+        self.upsampling.reinitialize_parameters()
+        self.synthesis.reinitialize_parameters()
+        self.initialize_latent_grids()
+
+
+def _check_same_arch(encs: Sequence[CoolChicEncoder]) -> None:
+    p0 = encs[0].param
+    for e in encs[1:]:
+        p = e.param
+        if (p.img_size, p.layers_synthesis, p.n_ft_per_res, p.dim_arm, p.n_hidden_layers_arm, p.ups_k_size,
+                p.ups_preconcat_k_size, p.encoder_gain) != (p0.img_size, p0.layers_synthesis, p0.n_ft_per_res,
+                                                            p0.dim_arm, p0.n_hidden_layers_arm, p0.ups_k_size,
+                                                            p0.ups_preconcat_k_size, p0.encoder_gain):
+            raise ValueError("forward_batch: all encoders must share image size and architecture")
+
+
+@torch.no_grad()
+def forward_batch(encs: Sequence[CoolChicEncoder], AC_MAX_VAL: int = -1, flag_additional_outputs: bool = False):
+    """Eval forward of several independent CoolChicEncoders (own weights each) in one HIP launch
+    sequence.  Returns (raw_out [B, C, H, W], rate [B, N], additional_data)."""
+    _check_same_arch(encs)
+    e0 = encs[0]
+    dev = e0.latent_grids[0].data.device
+    if dev.type != "cuda":
+        raise ValueError("CoolChicEncoder.forward runs on the GPU: move the module with .to('cuda')")
+    sizes = e0.grid_sizes
+    gain = float(e0.encoder_gains)
+    flat = torch.cat([e.flat_latent() for e in encs], dim=0).float().contiguous()
+    quantize = True
+    if AC_MAX_VAL != -1:  # bitstream-writing clamp (coolchic.py:374-377)
+        flat = torch.clamp(torch.round(flat * gain), -AC_MAX_VAL, AC_MAX_VAL + 1)
+        quantize = False
+    arm_p = torch.stack([e.arm.packed_params() for e in encs]).to(dev)
+    ups_p = torch.stack([e.upsampling.packed_params() for e in encs]).to(dev)
+    syn_p = torch.stack([e.synthesis.packed_params() for e in encs]).to(dev)
+    want = ("mu", "scale", "log_scale", "rate") if flag_additional_outputs else ("rate",)
+    a = _F.arm_forward(flat, sizes, arm_p, e0.param.dim_arm, e0.param.n_hidden_layers_arm, gain, quantize, want)
+    dense = e0.upsampling.forward_flat(flat, sizes, gain, quantize, params=ups_p)
+    raw = e0.synthesis.forward(dense, params=syn_p)
+    add: Dict[str, Any] = {}
+    if flag_additional_outputs:
+        if len(encs) > 1:
+            raise NotImplementedError("Batching is not yet supported for additional outputs.")
+        q = flat if not quantize else torch.round(flat * gain)
+        keys = ["detailed_sent_latent", "detailed_mu", "detailed_scale", "detailed_log_scale",
+                "detailed_rate_bit", "detailed_centered_latent"]
+        add = {k: [] for k in keys}
+        add["hpfilters"] = []
+        cnt = 0
+        for h, w in sizes:
+            sl = slice(cnt, cnt + h * w)
+            lat = q[:, sl].view(1, 1, h, w)
+            mu = a["mu"][:, sl].view(1, 1, h, w)
+            add["detailed_sent_latent"].append(lat)
+            add["detailed_mu"].append(mu)
+            add["detailed_scale"].append(a["scale"][:, sl].view(1, 1, h, w))
+            add["detailed_log_scale"].append(a["log_scale"][:, sl].view(1, 1, h, w))
+            add["detailed_rate_bit"].append(a["rate"][:, sl].view(1, 1, h, w))
+            add["detailed_centered_latent"].append(lat - mu)
+            cnt += h * w
+    return raw, a["rate"], add

@@ -1,0 +1,54 @@
+"""FrameEncoder (reference: coolchic/enc/component/frame.py), intra frames, eval forward.
+
+forward() = CoolChicEncoder.forward + the eval post-processing of frame.py:175-183
+(rounding to the output bitdepth, optional 444 -> 420 nearest, clamp), the latter in
+ccmi_post_f32.  Inter coding (warping, frame.py:165-170) is disabled in the reference
+and not part of this hot path.
+"""
+
+from dataclasses import dataclass, field
+from typing import Any, Dict, List, Optional, Union
+
+import torch
+from torch import Tensor, nn
+
+from ccmi import forward as _F
+from coolchic.enc.component.coolchic import CoolChicEncoder, CoolChicEncoderParameter
+
+
+@dataclass
+class FrameEncoderOutput:
+    decoded_image: Union[Tensor, Dict[str, Tensor]]
+    rate: Tensor
+    additional_data: Dict[str, Any] = field(default_factory=dict)
+
+
+class FrameEncoder(nn.Module):
+    def __init__(self, coolchic_encoder_param: CoolChicEncoderParameter, frame_type: str = "I",
+                 frame_data_type: str = "rgb", bitdepth: int = 8):
+        super().__init__()
+        if frame_type != "I":
+            raise NotImplementedError("only intra frames are part of the decode hot path")
+        self.coolchic_encoder_param = coolchic_encoder_param
+        self.frame_type = frame_type
+        self.frame_data_type = frame_data_type
+        self.bitdepth = bitdepth
+        self.coolchic_encoder = CoolChicEncoder(coolchic_encoder_param)
+
+    def forward(self, reference_frames: Optional[List[Tensor]] = None, quantizer_noise_type: str = "kumaraswamy",
+                quantizer_type: str = "softround", soft_round_temperature: Optional[float] = 0.3,
+                noise_parameter: Optional[float] = 1.0, AC_MAX_VAL: int = -1,
+                flag_additional_outputs: bool = False) -> FrameEncoderOutput:
+        raw, rate, add = self.coolchic_encoder.forward(quantizer_noise_type, quantizer_type, soft_round_temperature,
+                                                       noise_parameter, AC_MAX_VAL, flag_additional_outputs)
+        return FrameEncoderOutput(self.post_process(raw), rate, add if flag_additional_outputs else {})
+
+    def post_process(self, raw: Tensor):
+        if self.training:
+            raise NotImplementedError("training-mode frame forward")
+        H, W = raw.shape[-2:]
+        if self.frame_data_type == "yuv420":
+            out = _F.post_forward(raw, self.bitdepth, True)
+            d = _F.split_420(out, H, W)
+            return {k: v.unsqueeze(1) for k, v in d.items()}
+        return _F.post_forward(raw, self.bitdepth, False)

@@ -44,7 +44,7 @@ extern "C" int ccmi_arm_forward_f32(const ccmi_arm_args *a, void *stream)
     if (a->batch < 1) return ccmi_set_error(CCMI_ERR_ARG, "arm: batch must be >= 1");
     if (a->n_hidden < 0 || a->n_hidden > 4) return ccmi_set_error(CCMI_ERR_UNSUPPORTED, "arm: n_hidden must be in [0, 4]");
     const int64_t need = (int64_t)a->n_hidden * (a->dim_arm * a->dim_arm + a->dim_arm) + 2 * a->dim_arm + 2;
-    if (a->batch > 1 && a->param_stride < need) return ccmi_set_error(CCMI_ERR_ARG, "arm: param_stride < %lld", (long long)need);
+    if (a->param_stride != 0 && a->param_stride < need) return ccmi_set_error(CCMI_ERR_ARG, "arm: param_stride < %lld", (long long)need);
     if (!a->rate && !a->mu && !a->scale && !a->log_scale) return ccmi_set_error(CCMI_ERR_ARG, "arm: no output requested");
     return ccmi_launch_arm_f32(a, static_cast<hipStream_t>(stream));
 }

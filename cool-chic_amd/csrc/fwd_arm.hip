@@ -156,7 +156,97 @@ __global__ __launch_bounds__(kThreads) void arm_fwd_kernel(
     }
 }
 
+template <int D>
+__global__ __launch_bounds__(kThreads) void arm_context_kernel(const float *__restrict__ grid, int H, int W,
+                                                               float *__restrict__ out)
+{
+    const int b = blockIdx.y;
+    const int64_t p = (int64_t)blockIdx.x * kThreads + threadIdx.x;
+    if (p >= (int64_t)H * W) return;
+    const int y = (int)(p / W), x = (int)(p - (int64_t)y * W);
+    const float *g = grid + (int64_t)b * H * W;
+    float *o = out + ((int64_t)b * H * W + p) * D;
+#pragma unroll
+    for (int i = 0; i < D; ++i) {
+        int dy, dx;
+        ctx_offset<D>(i, dy, dx);
+        const int yy = y + dy, xx = x + dx;
+        o[i] = (yy >= 0 && xx >= 0 && xx < W) ? g[yy * W + xx] : 0.f;
+    }
+}
+
+template <int D>
+__global__ __launch_bounds__(kThreads) void arm_mlp_kernel(const float *__restrict__ ctx, int64_t M, int nh,
+                                                           const float *__restrict__ p, float *__restrict__ o_mu,
+                                                           float *__restrict__ o_scale, float *__restrict__ o_ls)
+{
+    const int64_t r = (int64_t)blockIdx.x * kThreads + threadIdx.x;
+    if (r >= M) return;
+    float a[D];
+#pragma unroll
+    for (int i = 0; i < D; ++i) a[i] = ctx[r * D + i];
+    for (int layer = 0; layer < nh; ++layer) {
+        const float *Wl = p + layer * (D * D + D);
+        float o[D];
+#pragma unroll
+        for (int j = 0; j < D; ++j) {
+            float acc = 0.f;
+#pragma unroll
+            for (int i = 0; i < D; ++i) acc = fmaf(Wl[j * D + i], a[i], acc);
+            o[j] = fmaxf((acc + Wl[D * D + j]) + a[j], 0.f);
+        }
+#pragma unroll
+        for (int j = 0; j < D; ++j) a[j] = o[j];
+    }
+    const float *Wo = p + nh * (D * D + D);
+    float m = 0.f, ls = 0.f;
+#pragma unroll
+    for (int i = 0; i < D; ++i) {
+        m = fmaf(Wo[i], a[i], m);
+        ls = fmaf(Wo[D + i], a[i], ls);
+    }
+    m += Wo[2 * D];
+    ls += Wo[2 * D + 1];
+    if (o_mu) o_mu[r] = m;
+    if (o_ls) o_ls[r] = ls;
+    if (o_scale) o_scale[r] = expf(fminf(fmaxf(ls - 4.f, -4.6f), 5.0f));
+}
+
 } // namespace
+
+extern "C" int ccmi_arm_context_f32(const float *grid, int batch, int h, int w, int dim_arm, float *out, void *stream)
+{
+    if (!grid || !out || batch < 1 || h < 1 || w < 1) return ccmi_set_error(CCMI_ERR_ARG, "arm_context: bad argument");
+    dim3 g((unsigned)(((int64_t)h * w + kThreads - 1) / kThreads), batch);
+    hipStream_t s = static_cast<hipStream_t>(stream);
+    switch (dim_arm) {
+    case 8: hipLaunchKernelGGL(arm_context_kernel<8>, g, dim3(kThreads), 0, s, grid, h, w, out); break;
+    case 16: hipLaunchKernelGGL(arm_context_kernel<16>, g, dim3(kThreads), 0, s, grid, h, w, out); break;
+    case 24: hipLaunchKernelGGL(arm_context_kernel<24>, g, dim3(kThreads), 0, s, grid, h, w, out); break;
+    case 32: hipLaunchKernelGGL(arm_context_kernel<32>, g, dim3(kThreads), 0, s, grid, h, w, out); break;
+    default: return ccmi_set_error(CCMI_ERR_UNSUPPORTED, "arm_context: dim_arm %d", dim_arm);
+    }
+    CCMI_HIP_CHECK(hipGetLastError());
+    return CCMI_OK;
+}
+
+extern "C" int ccmi_arm_mlp_f32(const float *ctx, int64_t m, int dim_arm, int n_hidden, const float *params, float *mu,
+                                float *scale, float *log_scale, void *stream)
+{
+    if (!ctx || !params || m < 0 || n_hidden < 0 || n_hidden > 4) return ccmi_set_error(CCMI_ERR_ARG, "arm_mlp: bad argument");
+    if (m == 0) return CCMI_OK;
+    dim3 g((unsigned)((m + kThreads - 1) / kThreads));
+    hipStream_t s = static_cast<hipStream_t>(stream);
+    switch (dim_arm) {
+    case 8: hipLaunchKernelGGL(arm_mlp_kernel<8>, g, dim3(kThreads), 0, s, ctx, m, n_hidden, params, mu, scale, log_scale); break;
+    case 16: hipLaunchKernelGGL(arm_mlp_kernel<16>, g, dim3(kThreads), 0, s, ctx, m, n_hidden, params, mu, scale, log_scale); break;
+    case 24: hipLaunchKernelGGL(arm_mlp_kernel<24>, g, dim3(kThreads), 0, s, ctx, m, n_hidden, params, mu, scale, log_scale); break;
+    case 32: hipLaunchKernelGGL(arm_mlp_kernel<32>, g, dim3(kThreads), 0, s, ctx, m, n_hidden, params, mu, scale, log_scale); break;
+    default: return ccmi_set_error(CCMI_ERR_UNSUPPORTED, "arm_mlp: dim_arm %d", dim_arm);
+    }
+    CCMI_HIP_CHECK(hipGetLastError());
+    return CCMI_OK;
+}
 
 int ccmi_launch_arm_f32(const ccmi_arm_args *a, hipStream_t s)
 {

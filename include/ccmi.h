@@ -74,6 +74,15 @@ typedef struct ccmi_arm_args {
 } ccmi_arm_args;
 int ccmi_arm_forward_f32(const ccmi_arm_args *args, void *stream);
 
+/* Standalone pieces of the ARM for API parity with the reference modules (the fused
+ * ccmi_arm_forward_f32 is what CoolChicEncoder.forward uses):
+ *  ccmi_arm_context_f32: _get_neighbor (arm.py:308-352), grids [batch][h][w] -> [batch][h*w][dim_arm]
+ *  ccmi_arm_mlp_f32:     Arm.forward (arm.py:227-268) on given contexts [m][dim_arm] -> mu, scale,
+ *                        log_scale [m] (any may be NULL); params as in ccmi_arm_args (one model). */
+int ccmi_arm_context_f32(const float *grid, int batch, int h, int w, int dim_arm, float *out, void *stream);
+int ccmi_arm_mlp_f32(const float *ctx, int64_t m, int dim_arm, int n_hidden, const float *params, float *mu,
+                     float *scale, float *log_scale, void *stream);
+
 /* Upsampling: Upsampling.forward in eval mode (upsampling.py:476-506, separable
  * paths :205-209 and :337-353).  params per frame, float32: n_ups kernels of ups_k
  * taps (full symmetric kernels, conv_transpose2ds[i]), then n_pre kernels of
