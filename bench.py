@@ -155,6 +155,61 @@ def cpu_baseline(inp, budget_s=12.0, max_frames=64):
                       f"(oracle/forward_oracle.py, torch fp32 CPU, {torch.get_num_threads()} threads), {dt:.1f} s"}
 
 
+def bench_bitexact_decode(reps: int):
+    """Path B: the bit-exact HIP decoder on the shipped 1280x720 class-E .cool streams
+    (15 files x reps frames per ccmi_decode_batch call), output bytes checked against the
+    reference decoder's md5 list."""
+    import hashlib
+    from ccmi import decode
+    md5 = json.loads((ROOT / "tests/golden/ref_md5.json").read_text())
+    files = sorted((ROOT / "tests/golden/cool").glob("E-*.cool"))
+    streams = [f.read_bytes() for f in files]
+    decode.decode_batch(streams[:2])
+    batch = streams * reps
+    t0 = time.perf_counter()
+    outs = decode.decode_batch(batch)
+    wall = time.perf_counter() - t0
+    tm = decode.last_timing()
+    exact = all(hashlib.md5(o).hexdigest() == md5["jvet/" + f.name]["md5"] for f, o in zip(files * reps, outs))
+    kern_s = (tm["arm_cabac"] + tm["ups_syn_out"]) / 1e3
+    n = len(batch)
+    return {"metric": "bit-exact .cool decode Mpixel/s (batch of independent 720p streams)",
+            "frames": n, "value_kernels": round(n * H * W / kern_s / 1e6, 2),
+            "value_wall_pcie_inclusive": round(n * H * W / wall / 1e6, 2), "unit": "Mpixel/s",
+            "stage_ms": {k: round(v, 3) for k, v in tm.items()}, "bit_exact_vs_reference_md5": exact,
+            "data": "15 shipped JVET class-E .cool bitstreams (results/image/jvet), repeated"}
+
+
+def cpu_decode_baseline(budget_s=10.0):
+    """The reference C decoder (oracle/_ref, built from /root/reference sources) -- or the C oracle
+    when that binary is absent -- decoding the class-E streams, one process per core."""
+    import subprocess
+    import tempfile
+    ref = ROOT / "oracle" / "_ref" / "ccdec_ref"
+    orc = ROOT / "oracle" / "_build" / "ccdec_oracle"
+    files = sorted((ROOT / "tests/golden/cool").glob("E-*.cool"))
+    ncores = max(1, min(16, os.cpu_count() or 1))
+    kind = "reference" if ref.exists() else "port"
+    with tempfile.TemporaryDirectory() as td:
+        def cmd(f, i):
+            out = f"{td}/o{i}.yuv"
+            return [str(ref), f"--input={f}", f"--output={out}", "--avx2"] if kind == "reference" else \
+                [str(orc), str(f), out]
+        frames, t0, k, procs = 0, time.perf_counter(), 0, []
+        while True:
+            while len(procs) < ncores and time.perf_counter() - t0 < budget_s:
+                procs.append(subprocess.Popen(cmd(files[k % len(files)], len(procs)), stdout=subprocess.DEVNULL))
+                k += 1
+            if not procs:
+                break
+            procs.pop(0).wait()
+            frames += 1
+        dt = time.perf_counter() - t0
+    return {"value": round(frames * H * W / dt / 1e6, 3), "unit": "Mpixel/s", "cores": ncores, "kind": kind,
+            "sample": f"{frames} decodes of the 15 class-E 720p streams, {ncores} concurrent single-threaded "
+                      f"processes ({'reference ccdec --avx2' if kind == 'reference' else 'C oracle'}), {dt:.1f} s"}
+
+
 def pmc_traffic(stage: str):
     """Per-launch HBM bytes of `stage` from the committed PMC summary, or None."""
     for f in sorted((ROOT / "profiles").glob("*pmc*.json"), reverse=True):
@@ -175,6 +230,7 @@ def main():
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--batch", type=int, default=8, help="720p frames per step per GPU")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--decode-reps", type=int, default=8, help="class-E stream copies for the bit-exact decode leg")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -248,6 +304,11 @@ def main():
     }
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         res["cpu_baseline"] = cpu_baseline(inp)
+    if rank == 0 and args.decode_reps > 0:
+        dec = bench_bitexact_decode(args.decode_reps)
+        if world == 1 and not args.no_cpu_baseline:
+            dec["cpu_baseline"] = cpu_decode_baseline()
+        res["bitexact_decode"] = dec
     if rank == 0:
         print(json.dumps(res), flush=True)
     if dist:

@@ -25,7 +25,7 @@ EXPORTED = [
     "ccmi_last_error", "ccmi_version", "ccmi_device_count",
     "ccmi_arm_forward_f32", "ccmi_arm_context_f32", "ccmi_arm_mlp_f32", "ccmi_ups_workspace_bytes", "ccmi_ups_forward_f32",
     "ccmi_syn_workspace_bytes", "ccmi_syn_forward_f32", "ccmi_post_f32",
-    "ccmi_decode_file", "ccmi_decode_batch", "ccmi_decode_output_size",
+    "ccmi_decode_file", "ccmi_decode_batch", "ccmi_decode_output_size", "ccmi_decode_last_timing",
 ]
 
 
@@ -90,6 +90,13 @@ def lib() -> C.CDLL:
     global _lib
     if _lib is not None:
         return _lib
+    # PyTorch-ROCm bundles its own libamdhip64.so.7 (same soname as /opt/rocm's).  Load torch
+    # first so that the process has ONE HIP runtime, shared by torch tensors / streams and
+    # libccmi; loading libccmi first would pull /opt/rocm's runtime under torch.
+    try:
+        import torch  # noqa: F401
+    except ImportError:
+        pass
     if not LIB_PATH.exists():
         raise CcmiUnavailable(f"{LIB_PATH} not built: run `make -C cool-chic_amd` (or __graft_entry__.build())")
     L = C.CDLL(str(LIB_PATH))
@@ -119,6 +126,8 @@ def lib() -> C.CDLL:
     L.ccmi_decode_output_size.argtypes = [C.c_void_p, C.c_size_t, C.c_int, C.c_int, C.c_int,
                                           C.POINTER(C.c_size_t)]
     L.ccmi_decode_output_size.restype = C.c_int
+    L.ccmi_decode_last_timing.argtypes = [C.POINTER(C.c_float)]
+    L.ccmi_decode_last_timing.restype = C.c_int
     _lib = L
     return L
 

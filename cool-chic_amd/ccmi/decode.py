@@ -44,4 +44,11 @@ def decode_batch(streams: Sequence[bytes], output_bitdepth: int = 0, output_chro
     return [o.raw[: got[i]] for i, o in enumerate(outs)]
 
 
-__all__ = ["decode_file", "decode_batch", "output_size", "CcmiError"]
+def last_timing() -> dict:
+    """Device stage times (ms) of this thread's last decode: upload, arm_cabac, ups_syn_out, download."""
+    ms = (C.c_float * 4)()
+    check(lib().ccmi_decode_last_timing(ms))
+    return dict(zip(("upload", "arm_cabac", "ups_syn_out", "download"), list(ms)))
+
+
+__all__ = ["last_timing", "decode_file", "decode_batch", "output_size", "CcmiError"]

@@ -261,6 +261,27 @@ struct DevPlan {
     size_t lat_elems, ws_elems, dense_elems, synout_elems, synws_elems;
 };
 
+thread_local float g_last_ms[4] = {0, 0, 0, 0};
+
+struct EventSet {
+    hipEvent_t e[5] = {};
+    bool ok = true;
+    EventSet()
+    {
+        for (auto &x : e)
+            if (hipEventCreate(&x) != hipSuccess) ok = false;
+    }
+    ~EventSet()
+    {
+        for (auto &x : e)
+            if (x) (void)hipEventDestroy(x);
+    }
+    void rec(int i, hipStream_t s)
+    {
+        if (ok) (void)hipEventRecord(e[i], s);
+    }
+};
+
 int decode_many(const uint8_t *const *streams, const size_t *lens, int n, uint8_t *const *outs, const size_t *caps,
                 size_t *sizes, int out_bitdepth, int out_chroma, int as_yuv, hipStream_t s)
 {
@@ -328,6 +349,11 @@ int decode_many(const uint8_t *const *streams, const size_t *lens, int n, uint8_
     }
     const size_t desc_off = tot;
     tot += align_up(sizeof(ArmStreamDesc) * (size_t)n * CCMI_MAX_GRIDS, 256);
+#if defined(CCMI_ARM_STAMPS)
+    const size_t dbg_off = tot;
+    tot += align_up(8 * 8 * (size_t)n * CCMI_MAX_GRIDS, 256);
+    size_t all_count = 0;
+#endif
 
     std::vector<uint8_t> host(cst, 0);
     for (int i = 0; i < n; ++i) {
@@ -346,6 +372,8 @@ int decode_many(const uint8_t *const *streams, const size_t *lens, int n, uint8_
         uint8_t *p;
         ~Free() { if (p) (void)hipFree(p); }
     } guard{dev};
+    EventSet ev;
+    ev.rec(0, s);
     CCMI_HIP_CHECK(hipMemcpyAsync(dev, host.data(), cst, hipMemcpyHostToDevice, s));
 
     // ---- ARM + CABAC: every non-empty latent layer of every frame, one launch per (d, nh)
@@ -373,6 +401,15 @@ int decode_many(const uint8_t *const *streams, const size_t *lens, int n, uint8_
             a.d = f.dim_arm;
             a.nh = f.n_hidden;
             a.weights = reinterpret_cast<const int32_t *>(dev + p.arm_off);
+            a.flags = 1;
+            a.dbg = nullptr;
+#if defined(CCMI_ARM_STAMPS)
+            a.dbg = reinterpret_cast<uint64_t *>(dev + dbg_off) + 8 * (desc.size() + all_count++);
+#endif
+            for (size_t k = 0; k < f.arm.size(); ++k) {
+                // biases sit between weight blocks; checking them too is conservative
+                if (f.arm[k] >= (1 << 23) || f.arm[k] < -(1 << 23)) a.flags = 0;
+            }
             a.out = plane;
             max_w = std::max(max_w, a.w);
             const int blk = std::abs(a.sig_blk);
@@ -398,9 +435,11 @@ int decode_many(const uint8_t *const *streams, const size_t *lens, int n, uint8_
                          [](const ArmStreamDesc &x, const ArmStreamDesc &y) { return x.h * x.w > y.h * y.w; });
         all.insert(all.end(), g.second.begin(), g.second.end());
     }
-    if (!all.empty()) {
+    if (!all.empty())
         CCMI_HIP_CHECK(hipMemcpyAsync(dev + desc_off, all.data(), all.size() * sizeof(ArmStreamDesc),
                                       hipMemcpyHostToDevice, s));
+    ev.rec(1, s);
+    if (!all.empty()) {
         for (auto &g : groups) {
             const ArmStreamDesc *dd = reinterpret_cast<const ArmStreamDesc *>(dev + desc_off) + dpos;
             if (int rc = launch_dec_arm(dd, (int)g.second.size(), max_w, max_blocks, g.first.d, g.first.nh, s)) return rc;
@@ -408,6 +447,7 @@ int decode_many(const uint8_t *const *streams, const size_t *lens, int n, uint8_
         }
     }
 
+    ev.rec(2, s);
     // ---- per frame: upsampling, synthesis (+ blend), output bytes
     for (int i = 0; i < n; ++i) {
         FrameHost &f = fr[i];
@@ -453,17 +493,42 @@ int decode_many(const uint8_t *const *streams, const size_t *lens, int n, uint8_
                     return rc;
         }
         if (int rc = launch_dec_output(synout, f.h, f.w, of[i].bitdepth, of[i].kind, dev + p.out_off, s)) return rc;
-        if (outs) {
-            if (of[i].header) memcpy(outs[i], of[i].hdr, of[i].header);
-            CCMI_HIP_CHECK(hipMemcpyAsync(outs[i] + of[i].header, dev + p.out_off, of[i].payload,
-                                          hipMemcpyDeviceToHost, s));
+    }
+    ev.rec(3, s);
+    for (int i = 0; i < n && outs; ++i) {
+        if (of[i].header) memcpy(outs[i], of[i].hdr, of[i].header);
+        CCMI_HIP_CHECK(hipMemcpyAsync(outs[i] + of[i].header, dev + pl[i].out_off, of[i].payload,
+                                      hipMemcpyDeviceToHost, s));
+    }
+    ev.rec(4, s);
+    CCMI_HIP_CHECK(hipStreamSynchronize(s));
+#if defined(CCMI_ARM_STAMPS)
+    {
+        std::vector<uint64_t> dbg(8 * all.size());
+        CCMI_HIP_CHECK(hipMemcpy(dbg.data(), dev + dbg_off, dbg.size() * 8, hipMemcpyDeviceToHost));
+        for (size_t j = 0; j < all.size(); ++j) {
+            const size_t k = (size_t)(reinterpret_cast<uint8_t *>(all[j].dbg) - (dev + dbg_off)) / 64;
+            fprintf(stderr, "STAMPS stream %zu (%dx%d): ctx %llu mlp %llu idx %llu cabac %llu coded %llu setup %llu loop %llu\n", k,
+                    all[j].h, all[j].w, (unsigned long long)dbg[8 * k], (unsigned long long)dbg[8 * k + 1],
+                    (unsigned long long)dbg[8 * k + 2], (unsigned long long)dbg[8 * k + 3],
+                    (unsigned long long)dbg[8 * k + 4], (unsigned long long)dbg[8 * k + 5],
+                    (unsigned long long)dbg[8 * k + 6]);
         }
     }
-    CCMI_HIP_CHECK(hipStreamSynchronize(s));
+#endif
+    if (ev.ok)
+        for (int k = 0; k < 4; ++k) (void)hipEventElapsedTime(&g_last_ms[k], ev.e[k], ev.e[k + 1]);
     return CCMI_OK;
 }
 
 } // namespace
+
+extern "C" int ccmi_decode_last_timing(float *ms4)
+{
+    if (!ms4) return ccmi_set_error(CCMI_ERR_ARG, "decode_last_timing: null argument");
+    for (int k = 0; k < 4; ++k) ms4[k] = g_last_ms[k];
+    return CCMI_OK;
+}
 
 extern "C" int ccmi_decode_output_size(const uint8_t *stream, size_t len, int out_bitdepth, int out_chroma, int as_yuv,
                                        size_t *size)

@@ -51,8 +51,10 @@ struct ArmStreamDesc {
     uint32_t nbytes;
     int h, w, sig_blk;
     int d, nh;
+    int flags;              // bit 0: every ARM weight fits in 24 signed bits
     const int32_t *weights; // device copy of FrameHost::arm
     int32_t *out;           // device h*w plane, value << kArmPrec
+    uint64_t *dbg;          // diagnostic builds only (CCMI_ARM_STAMPS): 8 counters per stream
 };
 
 // One launch for n_streams streams sharing (d, nh); max_w / max_blocks size the LDS

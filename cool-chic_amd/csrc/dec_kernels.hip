@@ -46,18 +46,32 @@ __device__ __forceinline__ int32_t tshift(int32_t s, int p) { return s < 0 ? -((
 __device__ __forceinline__ int clampi(int v, int hi) { return v < 0 ? 0 : (v > hi ? hi : v); }
 
 // ------------------------------------------------------------------ device byte source
+// The stream is read through a constant-address-space pointer so that the wave-uniform
+// word loads become scalar (SMEM) loads; the next word is prefetched one word ahead.
+typedef const __attribute__((address_space(4))) uint32_t *const_u32_ptr;
+
 struct DevBytes {
-    const uint32_t *p;
-    uint32_t nwords, pos, wi, cur;
+    const_u32_ptr p;
+    uint32_t nwords, pos, wi, cur, nxt;
+    __device__ __forceinline__ uint32_t ld(uint32_t i) const { return i < nwords ? p[i] : 0u; }
+    __device__ __forceinline__ void init(const uint32_t *base, uint32_t nbytes)
+    {
+        p = (const_u32_ptr)(size_t)base;
+        nwords = (nbytes + 3u) >> 2;
+        pos = 0;
+        wi = 0;
+        cur = ld(0);
+        nxt = ld(1);
+    }
     __device__ __forceinline__ uint32_t next()
     {
-        const uint32_t i = pos >> 2;
-        if (i != wi) {
-            wi = i;
-            cur = i < nwords ? p[i] : 0u;
-        }
         const uint32_t b = (cur >> ((pos & 3u) * 8u)) & 0xFFu;
         ++pos;
+        if ((pos & 3u) == 0) {
+            cur = nxt;
+            ++wi;
+            nxt = ld(wi + 1);
+        }
         return b;
     }
 };
@@ -92,17 +106,54 @@ __device__ __forceinline__ void ctx_dydx(int i, int &dy, int &dx)
 constexpr int kRing = 5;   // rows y-4 .. y
 constexpr int kPad = 4;    // zero columns either side of a ring row
 
+// int32 multiply with two's-complement wrap; the 24-bit form (v_mad_i32_i24, full rate)
+// is exact whenever both operands fit in 24 signed bits.
+template <bool F24>
+__device__ __forceinline__ int32_t imul(int32_t a, int32_t b)
+{
+    if constexpr (F24) return __mul24(a, b);
+    else return (int32_t)((uint32_t)a * (uint32_t)b);
+}
+
+// One residual hidden layer, lane o = neuron o: (b + 256 a_o + sum_i W[o][i] a_i), ReLU, round >> 8.
+template <int D, bool F24>
+__device__ __forceinline__ int32_t arm_hidden(const int32_t (&W)[D], int32_t bias, int32_t a)
+{
+    int32_t acc = bias + a * 256;
+#pragma unroll
+    for (int i = 0; i < D; ++i) acc += imul<F24>(W[i], __builtin_amdgcn_readlane(a, i));
+    return acc < 0 ? 0 : (acc + 128) >> 8;
+}
+
+#if defined(CCMI_ARM_STAMPS)
+// Diagnostic build only (make stamps): per-stream cycle totals of the decode segments.
+#define STAMP(var) const uint64_t var = __builtin_amdgcn_s_memtime()
+#define ACC(k, a, b) st_acc[k] += (b) - (a)
+#else
+#define STAMP(var)
+#define ACC(k, a, b)
+#endif
+
 template <int D, int NH>
 __global__ __launch_bounds__(64) void dec_arm_kernel(const ArmStreamDesc *__restrict__ streams, int pitch)
 {
+#if defined(CCMI_ARM_STAMPS)
+    uint64_t st_acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+#endif
     extern __shared__ int32_t smem[];
-    int32_t *ring = smem;                                     // kRing x pitch
+    int32_t *ring = smem;                                              // kRing x pitch
     uint8_t *bmap = reinterpret_cast<uint8_t *>(smem + kRing * pitch); // block sig/flat map
 
     const ArmStreamDesc S = streams[blockIdx.x];
     const int lane = threadIdx.x;
     const int h = S.h, w = S.w;
+    // weights fit in 24 signed bits (host check): hidden layers >= 2 and the output layer
+    // then use 24-bit multiplies (their inputs are ReLU-rounded sums, < 2^23 by construction)
+    const bool w24 = (S.flags & 1) != 0;
 
+#if defined(CCMI_ARM_STAMPS)
+    const uint64_t t_begin = __builtin_amdgcn_s_memtime();
+#endif
     for (int i = lane; i < kRing * pitch; i += 64) ring[i] = 0;
 
     // ---- weights: lane owns neuron o = lane % D (lanes >= D duplicate, masked in sums)
@@ -117,15 +168,12 @@ __global__ __launch_bounds__(64) void dec_arm_kernel(const ArmStreamDesc *__rest
     }
     const int32_t *ob = S.weights + NH * (D * D + D);
     const int32_t Wo0 = lane < D ? ob[o] : 0, Wo1 = lane < D ? ob[D + o] : 0;
-    const int32_t bo0 = ob[2 * D], bo1 = ob[2 * D + 1];
+    const int32_t bo0 = __builtin_amdgcn_readfirstlane(ob[2 * D]);
+    const int32_t bo1 = __builtin_amdgcn_readfirstlane(ob[2 * D + 1]);
 
-    // ---- CABAC start + block significance / flat maps (BACContext::set_layer)
+    // ---- CABAC start + block significance / flat maps (BACContext::set_layer, cc-bac.h:24-130)
     Cabac<DevBytes> cab;
-    cab.src.p = S.bytes;
-    cab.src.nwords = (S.nbytes + 3) >> 2;
-    cab.src.pos = 0;
-    cab.src.wi = 0xFFFFFFFFu;
-    cab.src.cur = 0;
+    cab.src.init(S.bytes, S.nbytes);
     cab.start();
     const int updated = S.sig_blk < 0;
     const int blk = S.sig_blk < 0 ? -S.sig_blk : S.sig_blk;
@@ -164,10 +212,15 @@ __global__ __launch_bounds__(64) void dec_arm_kernel(const ArmStreamDesc *__rest
     }
     __syncthreads();
 
+#if defined(CCMI_ARM_STAMPS)
+    st_acc[5] = __builtin_amdgcn_s_memtime() - t_begin; // setup incl. block maps
+    const uint64_t t_loop = __builtin_amdgcn_s_memtime();
+#endif
     // ---- context geometry of this lane (context index = o)
     int cdy, cdx;
     ctx_dydx<D>(o, cdy, cdx);
     const bool same_row = cdy == 0;
+    int big = 0; // uniform: a decoded |latent| >= 2^15 was seen -> contexts may exceed 24 bits
 
     for (int y = 0; y < h; ++y) {
         int32_t *row = ring + (y % kRing) * pitch + kPad;
@@ -175,9 +228,10 @@ __global__ __launch_bounds__(64) void dec_arm_kernel(const ArmStreamDesc *__rest
         const int32_t *crow = ring + ((y + cdy + kRing) % kRing) * pitch + kPad + cdx;
         int32_t r1 = 0, r2 = 0, r3 = 0, r4 = 0; // decoded values at x-1 .. x-4 (this row)
         const int brow = blk > 0 ? (y >> shift) * nbx : 0;
+        int bm = 1;
         for (int x = 0; x < w; ++x) {
             int32_t v;
-            const int bm = blk > 0 ? __builtin_amdgcn_readfirstlane((int)bmap[brow + (x >> shift)]) : 1;
+            if (blk > 0 && (x & mask) == 0) bm = __builtin_amdgcn_readfirstlane((int)bmap[brow + (x >> shift)]);
             if (!(bm & 1)) {
                 v = 0;
             } else if ((bm & 2) && (x & mask)) {
@@ -185,17 +239,21 @@ __global__ __launch_bounds__(64) void dec_arm_kernel(const ArmStreamDesc *__rest
             } else if ((bm & 2) && (y & mask)) {
                 v = __builtin_amdgcn_readfirstlane(up[x]);
             } else {
-                int32_t a;
-                if (same_row) a = cdx == -1 ? r1 : cdx == -2 ? r2 : cdx == -3 ? r3 : r4;
-                else a = crow[x];
+                STAMP(t0);
+                const int32_t al = crow[x]; // same-row lanes read a stale slot, replaced below
+                const int32_t rs = cdx == -1 ? r1 : cdx == -2 ? r2 : cdx == -3 ? r3 : r4;
+                int32_t a = same_row ? rs : al;
+                const bool f1 = w24 && !big; // contexts (latent << 8) fit in 24 bits
 #pragma unroll
                 for (int l = 0; l < NH; ++l) {
-                    int32_t acc = Bh[l] + a * 256; // residual
-#pragma unroll
-                    for (int i = 0; i < D; ++i) acc += Wh[l][i] * __builtin_amdgcn_readlane(a, i);
-                    a = acc < 0 ? 0 : (acc + 128) >> 8;
+                    if (l == 0) a = f1 ? arm_hidden<D, true>(Wh[0], Bh[0], a) : arm_hidden<D, false>(Wh[0], Bh[0], a);
+                    else a = w24 ? arm_hidden<D, true>(Wh[l], Bh[l], a) : arm_hidden<D, false>(Wh[l], Bh[l], a);
                 }
-                int32_t s0 = row_sum16(Wo0 * a), s1 = row_sum16(Wo1 * a);
+                STAMP(t1);
+                const bool fo = NH > 0 ? w24 : f1;
+                const int32_t p0 = fo ? imul<true>(Wo0, a) : imul<false>(Wo0, a);
+                const int32_t p1 = fo ? imul<true>(Wo1, a) : imul<false>(Wo1, a);
+                int32_t s0 = row_sum16(p0), s1 = row_sum16(p1);
                 int32_t m0 = __builtin_amdgcn_readlane(s0, 15), m1 = __builtin_amdgcn_readlane(s1, 15);
                 if (D > 16) {
                     m0 += __builtin_amdgcn_readlane(s0, 31);
@@ -203,6 +261,7 @@ __global__ __launch_bounds__(64) void dec_arm_kernel(const ArmStreamDesc *__rest
                 }
                 m0 += bo0;
                 m1 += bo1;
+                STAMP(t2);
                 const int32_t mu = m0 < 0 ? -((-m0 + 128) >> 8) : (m0 + 128) >> 8;
                 const int32_t ls = m1 < 0 ? -((-m1 + 128) >> 8) : (m1 + 128) >> 8;
                 // get_val_mu_indicies (cc-contexts.h:20-48)
@@ -214,7 +273,11 @@ __global__ __launch_bounds__(64) void dec_arm_kernel(const ArmStreamDesc *__rest
                 si = si > 49 ? 49 : si;
                 const uint32_t ci = (uint32_t)(mi * 50 + si) * 2u;
                 const uint32_t st = c_ctx.v[ci], stp = c_ctx.v[ci + 1];
-                // decode_single (cc-bac.h:192-231)
+#if defined(CCMI_ARM_STAMPS)
+                asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+#endif
+                STAMP(t3);
+                // decode_single (cc-bac.h:192-231): static contexts
                 int32_t val = 0;
                 if (cab.bin_static(st & 0xFF)) {
                     if (!cab.bin_static((st >> 8) & 0xFF)) val = 1;
@@ -223,7 +286,17 @@ __global__ __launch_bounds__(64) void dec_arm_kernel(const ArmStreamDesc *__rest
                     else val = cab.expgolomb(0) + 4;
                     if (cab.bin_static(stp)) val = -val;
                 }
-                v = (int32_t)((uint32_t)((mr >> 8) + val) << kArmPrec);
+                STAMP(t4);
+                ACC(0, t0, t1);
+                ACC(1, t1, t2);
+                ACC(2, t2, t3);
+                ACC(3, t3, t4);
+#if defined(CCMI_ARM_STAMPS)
+                st_acc[4] += 1;
+#endif
+                const int32_t q = (mr >> 8) + val;
+                big |= (q >= 32768 || q <= -32768);
+                v = (int32_t)((uint32_t)q << kArmPrec);
             }
             r4 = r3;
             r3 = r2;
@@ -236,6 +309,11 @@ __global__ __launch_bounds__(64) void dec_arm_kernel(const ArmStreamDesc *__rest
         for (int x = lane; x < w; x += 64) dst[x] = row[x];
         __syncthreads();
     }
+#if defined(CCMI_ARM_STAMPS)
+    st_acc[6] = __builtin_amdgcn_s_memtime() - t_loop; // whole latent loop
+    if (lane == 0 && S.dbg)
+        for (int k = 0; k < 8; ++k) S.dbg[k] = st_acc[k];
+#endif
 }
 
 // ------------------------------------------------------------------ upsampling (integer)

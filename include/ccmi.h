@@ -175,6 +175,12 @@ int ccmi_decode_batch(const uint8_t *const *streams, const size_t *lens, int n,
                       uint8_t *const *out, const size_t *out_caps, size_t *out_sizes,
                       int out_bitdepth, int out_chroma, int as_yuv, void *stream);
 
+/* Device-side stage times (ms, HIP events on the decode stream) of this thread's last
+ * successful ccmi_decode_batch / ccmi_decode_file: [0] upload of streams + weights,
+ * [1] ARM + CABAC latent decode, [2] upsampling + synthesis + output conversion,
+ * [3] download of the decoded bytes. */
+int ccmi_decode_last_timing(float *ms4);
+
 /* Byte size of the decoded output of one stream (header parse only). */
 int ccmi_decode_output_size(const uint8_t *stream, size_t len, int out_bitdepth,
                             int out_chroma, int as_yuv, size_t *size);
