@@ -17,6 +17,10 @@
 //                   (syn_cpu.hpp / synlb_cpu.hpp) with replicate padding, one launch.
 //  dec_syn_layer    generic per-layer integer conv (any ks / widths).
 //  dec_output       444 -> 420/444 8/10-bit or PPM payload (ccdecapi.cpp:59-240).
+#include <stdlib.h>
+
+#include <utility>
+
 #include "ccmi_cabac.h"
 #include "dec_internal.h"
 
@@ -104,7 +108,7 @@ __device__ __forceinline__ void ctx_dydx(int i, int &dy, int &dx)
 }
 
 constexpr int kRing = 5;   // rows y-4 .. y
-constexpr int kPad = 4;    // zero columns either side of a ring row
+constexpr int kPad = 8;    // zero columns either side of a ring row (speculative groups read x+3+4)
 
 // int32 multiply with two's-complement wrap; the 24-bit form (v_mad_i32_i24, full rate)
 // is exact whenever both operands fit in 24 signed bits.
@@ -314,6 +318,227 @@ __global__ __launch_bounds__(64) void dec_arm_kernel(const ArmStreamDesc *__rest
     if (lane == 0 && S.dbg)
         for (int k = 0; k < 8; ++k) S.dbg[k] = st_acc[k];
 #endif
+}
+
+// ------------------------------------------------------------------ speculative ARM decode (d <= 16)
+// Same stream semantics as dec_arm_kernel, restructured for latency.  The wave's four
+// DPP rows (16 lanes each) evaluate the ARM for four consecutive latents x .. x+3 at
+// once: row g assumes the latents x .. x+g-1 (not decoded yet) are 0, the most likely
+// value.  The CABAC then decodes x, x+1, ... in order and stops at the first latent
+// whose decoded value is not 0: every later row was computed from a wrong guess and is
+// discarded; all rows up to and including that latent were exact.  Neuron o of row g
+// sits in lane 16g + o; the matrix-vector products broadcast a_i inside each row with
+// DPP row_newbcast (no SGPR round trip), fused by the compiler into v_mul_i32_i24_dpp.
+// The 17 x 50 context table is staged in LDS (one ds_read_b64 per latent instead of a
+// scalar load that misses the constant cache).
+template <bool F24, int... I>
+__device__ __forceinline__ int32_t row_dot(const int32_t (&W)[16], int32_t a, std::integer_sequence<int, I...>)
+{
+    int32_t acc = 0;
+    ((acc += imul<F24>(W[I], __builtin_amdgcn_update_dpp(0, a, 0x150 + I, 0xF, 0xF, false))), ...);
+    return acc;
+}
+
+template <int D, bool F24>
+__device__ __forceinline__ int32_t arm_hidden_rows(const int32_t (&W)[16], int32_t bias, int32_t a)
+{
+    const int32_t acc = bias + a * 256 + row_dot<F24>(W, a, std::make_integer_sequence<int, D>{});
+    return acc < 0 ? 0 : (acc + 128) >> 8;
+}
+
+constexpr int kSpec = 4; // latents evaluated per ARM pass (one per DPP row)
+
+template <int D, int NH>
+__global__ __launch_bounds__(64) void dec_arm_spec_kernel(const ArmStreamDesc *__restrict__ streams, int pitch)
+{
+    static_assert(D <= 16, "one neuron per lane of a DPP row");
+    extern __shared__ int32_t smem[];
+    uint32_t *ctab = reinterpret_cast<uint32_t *>(smem);               // 17 x 50 x 2
+    int32_t *ring = smem + 17 * 50 * 2;                                // kRing x pitch
+    uint8_t *bmap = reinterpret_cast<uint8_t *>(ring + kRing * pitch); // block sig/flat map
+
+    const ArmStreamDesc S = streams[blockIdx.x];
+    const int lane = threadIdx.x;
+    const int grp = lane >> 4, o = lane & 15;
+    const bool live = o < D;
+    const int h = S.h, w = S.w;
+    const bool w24 = (S.flags & 1) != 0;
+
+    for (int i = lane; i < 17 * 50 * 2; i += 64) ctab[i] = c_ctx.v[i];
+    for (int i = lane; i < kRing * pitch; i += 64) ring[i] = 0;
+
+    int32_t Wh[NH > 0 ? NH : 1][16], Bh[NH > 0 ? NH : 1];
+#pragma unroll
+    for (int l = 0; l < NH; ++l) {
+        const int32_t *base = S.weights + l * (D * D + D);
+#pragma unroll
+        for (int i = 0; i < 16; ++i) Wh[l][i] = (live && i < D) ? base[o * D + i] : 0;
+        Bh[l] = live ? base[D * D + o] : 0;
+    }
+    const int32_t *ob = S.weights + NH * (D * D + D);
+    const int32_t Wo0 = live ? ob[o] : 0, Wo1 = live ? ob[D + o] : 0;
+    const int32_t bo0 = __builtin_amdgcn_readfirstlane(ob[2 * D]);
+    const int32_t bo1 = __builtin_amdgcn_readfirstlane(ob[2 * D + 1]);
+
+    // ---- CABAC start + block significance / flat maps (BACContext::set_layer, cc-bac.h:24-130)
+    Cabac<DevBytes> cab;
+    cab.src.init(S.bytes, S.nbytes);
+    cab.start();
+    const int updated = S.sig_blk < 0;
+    const int blk = S.sig_blk < 0 ? -S.sig_blk : S.sig_blk;
+    int shift = 0;
+    while ((1 << shift) < blk) ++shift;
+    const int mask = (1 << shift) - 1;
+    int nby = 1, nbx = 1;
+    if (blk > 0) {
+        nby = (h + blk - 1) >> shift;
+        nbx = (w + blk - 1) >> shift;
+    }
+    const int nblk = nby * nbx;
+    for (int i = lane; i < nblk; i += 64) bmap[i] = 1; // bit0 sig, bit1 flat
+    __syncthreads();
+    if (nblk > 1) {
+        if (cab.ep()) {
+            Model m;
+            m.init(65);
+            for (int i = 0; i < nblk; ++i) {
+                const uint32_t b = updated ? cab.bin_adaptive(m) : cab.ep();
+                if (lane == 0) bmap[i] = (uint8_t)b;
+            }
+        }
+        __syncthreads();
+        if (cab.ep()) {
+            Model m;
+            m.init(65);
+            for (int i = 0; i < nblk; ++i) {
+                const int sig = __builtin_amdgcn_readfirstlane((int)bmap[i]);
+                if (sig) {
+                    const uint32_t f = updated ? cab.bin_adaptive(m) : cab.ep();
+                    if (lane == 0) bmap[i] = (uint8_t)(sig | (f << 1));
+                }
+            }
+        }
+    }
+    __syncthreads();
+
+    int cdy, cdx;
+    ctx_dydx<D>(o, cdy, cdx);
+    const bool same_row = cdy == 0;
+    int big = 0;
+
+    for (int y = 0; y < h; ++y) {
+        int32_t *row = ring + (y % kRing) * pitch + kPad;
+        const int32_t *up = ring + ((y + kRing - 1) % kRing) * pitch + kPad;
+        const int32_t *crow = ring + ((y + cdy + kRing) % kRing) * pitch + kPad + cdx + grp;
+        int32_t r1 = 0, r2 = 0, r3 = 0, r4 = 0; // decoded values at x-1 .. x-4 (this row)
+        const int brow = blk > 0 ? (y >> shift) * nbx : 0;
+        auto push = [&](int32_t v, int x) {
+            r4 = r3;
+            r3 = r2;
+            r2 = r1;
+            r1 = v;
+            if (lane == 0) row[x] = v;
+        };
+        int bm = 1, bend = w; // block flags of the current block, and its end column
+        for (int x = 0; x < w;) {
+            if (blk > 0 && (x & mask) == 0) {
+                bm = __builtin_amdgcn_readfirstlane((int)bmap[brow + (x >> shift)]);
+                bend = min(x + blk, w);
+            }
+            int L;
+            if (!(bm & 1)) {
+                // zero block: the whole remaining block at once
+                for (; x < bend; ++x) push(0, x);
+                continue;
+            } else if (bm & 2) {
+                if (x & mask) {
+                    push(r1, x);
+                    ++x;
+                    continue;
+                }
+                if (y & mask) {
+                    push(__builtin_amdgcn_readfirstlane(up[x]), x);
+                    ++x;
+                    continue;
+                }
+                L = 1; // the coded corner of a flat block
+            } else {
+                L = min(kSpec, bend - x);
+            }
+
+            // context of lane (g, o): latent x+g, neighbour (cdy, cdx); same-row neighbours
+            // at or right of x are the speculative zeros
+            const int k = -(grp + cdx); // same row: distance back from x (1..4), <= 0 -> guess
+            const int32_t rs = k == 1 ? r1 : k == 2 ? r2 : k == 3 ? r3 : k == 4 ? r4 : 0;
+            int32_t a = same_row ? rs : crow[x];
+            const bool f1 = w24 && !big;
+#pragma unroll
+            for (int l = 0; l < NH; ++l) {
+                if (l == 0) a = f1 ? arm_hidden_rows<D, true>(Wh[0], Bh[0], a) : arm_hidden_rows<D, false>(Wh[0], Bh[0], a);
+                else a = w24 ? arm_hidden_rows<D, true>(Wh[l], Bh[l], a) : arm_hidden_rows<D, false>(Wh[l], Bh[l], a);
+            }
+            const bool fo = NH > 0 ? w24 : f1;
+            const int32_t s0 = row_sum16(fo ? imul<true>(Wo0, a) : imul<false>(Wo0, a));
+            const int32_t s1 = row_sum16(fo ? imul<true>(Wo1, a) : imul<false>(Wo1, a));
+
+            int32_t sums0[kSpec], sums1[kSpec];
+            sums0[0] = __builtin_amdgcn_readlane(s0, 15) + bo0;
+            sums1[0] = __builtin_amdgcn_readlane(s1, 15) + bo1;
+            sums0[1] = __builtin_amdgcn_readlane(s0, 31) + bo0;
+            sums1[1] = __builtin_amdgcn_readlane(s1, 31) + bo1;
+            sums0[2] = __builtin_amdgcn_readlane(s0, 47) + bo0;
+            sums1[2] = __builtin_amdgcn_readlane(s1, 47) + bo1;
+            sums0[3] = __builtin_amdgcn_readlane(s0, 63) + bo0;
+            sums1[3] = __builtin_amdgcn_readlane(s1, 63) + bo1;
+            int32_t mrs[kSpec];
+            uint32_t sts[kSpec], stps[kSpec];
+#pragma unroll
+            for (int j = 0; j < kSpec; ++j) {
+                const int32_t m_0 = sums0[j], m_1 = sums1[j];
+                const int32_t mu = m_0 < 0 ? -((-m_0 + 128) >> 8) : (m_0 + 128) >> 8;
+                const int32_t ls = m_1 < 0 ? -((-m_1 + 128) >> 8) : (m_1 + 128) >> 8;
+                // get_val_mu_indicies (cc-contexts.h:20-48)
+                const int32_t mr = mu >= 0 ? ((mu + 128) >> 8) << 8 : -(((-mu + 128) >> 8) << 8);
+                int32_t mi = (mu - mr) * 16;
+                mi = (mi >= 0 ? (mi + 128) >> 8 : -((-mi + 128) >> 8)) + 8;
+                const int32_t lsp = ls + 256;
+                int32_t si = lsp < 0 ? 0 : (lsp * 5 + 128) >> 8;
+                si = si > 49 ? 49 : si;
+                const uint32_t ci = (uint32_t)(mi * 50 + si) * 2u;
+                const uint2 e = *reinterpret_cast<const uint2 *>(ctab + ci);
+                mrs[j] = mr;
+                sts[j] = __builtin_amdgcn_readfirstlane(e.x);
+                stps[j] = __builtin_amdgcn_readfirstlane(e.y);
+            }
+            // decode_single (cc-bac.h:192-231), in order, until the first non-zero latent
+            int nd = 0;
+#pragma unroll 1
+            for (int j = 0; j < L; ++j) {
+                // select chains keep the per-row scalars in SGPRs (no indexed register file)
+                const uint32_t st = j == 0 ? sts[0] : j == 1 ? sts[1] : j == 2 ? sts[2] : sts[3];
+                const uint32_t stp = j == 0 ? stps[0] : j == 1 ? stps[1] : j == 2 ? stps[2] : stps[3];
+                const int32_t mr = j == 0 ? mrs[0] : j == 1 ? mrs[1] : j == 2 ? mrs[2] : mrs[3];
+                int32_t val = 0;
+                if (cab.bin_static(st & 0xFF)) {
+                    if (!cab.bin_static((st >> 8) & 0xFF)) val = 1;
+                    else if (!cab.bin_static((st >> 16) & 0xFF)) val = 2;
+                    else if (!cab.bin_static(st >> 24)) val = 3;
+                    else val = cab.expgolomb(0) + 4;
+                    if (cab.bin_static(stp)) val = -val;
+                }
+                const int32_t q = (mr >> 8) + val;
+                big |= (q >= 32768 || q <= -32768);
+                push((int32_t)((uint32_t)q << kArmPrec), x + j);
+                ++nd;
+                if (q != 0) break;
+            }
+            x += nd;
+        }
+        __syncthreads();
+        int32_t *dst = S.out + (int64_t)y * w;
+        for (int x = lane; x < w; x += 64) dst[x] = row[x];
+        __syncthreads();
+    }
 }
 
 // ------------------------------------------------------------------ upsampling (integer)
@@ -609,6 +834,20 @@ int launch_dec_arm(const ArmStreamDesc *d_streams, int n_streams, int max_w, int
 {
     const int pitch = max_w + 2 * kPad;
     const size_t lds = sizeof(int32_t) * kRing * pitch + ((size_t)max_blocks + 16);
+    const size_t lds_spec = lds + sizeof(uint32_t) * 17 * 50 * 2;
+    // CCMI_ARM_NOSPEC=1 selects the one-latent-per-pass kernel (A/B measurements)
+    static const bool spec_off = getenv("CCMI_ARM_NOSPEC") != nullptr;
+    if (!spec_off && d <= 16 && lds_spec <= 160 * 1024) {
+#define CCMI_ARM_SPEC(DD, NN)                                                                                   \
+        if (d == DD && nh == NN) {                                                                              \
+            hipLaunchKernelGGL((dec_arm_spec_kernel<DD, NN>), dim3(n_streams), dim3(64), lds_spec, s, d_streams, pitch); \
+            CCMI_HIP_CHECK(hipGetLastError());                                                                  \
+            return CCMI_OK;                                                                                     \
+        }
+        CCMI_ARM_SPEC(8, 0) CCMI_ARM_SPEC(8, 1) CCMI_ARM_SPEC(8, 2) CCMI_ARM_SPEC(8, 3) CCMI_ARM_SPEC(8, 4)
+        CCMI_ARM_SPEC(16, 0) CCMI_ARM_SPEC(16, 1) CCMI_ARM_SPEC(16, 2) CCMI_ARM_SPEC(16, 3) CCMI_ARM_SPEC(16, 4)
+#undef CCMI_ARM_SPEC
+    }
     if (lds > 160 * 1024) return ccmi_set_error(CCMI_ERR_UNSUPPORTED, "dec: latent width %d too large for LDS ring", max_w);
 #define CCMI_ARM_CASE(DD, NN)                                                                                   \
     if (d == DD && nh == NN) {                                                                                  \

@@ -27,6 +27,10 @@ constexpr int kHalo = 4;
 constexpr int kLW = kTX + 2 * kHalo;          // 72
 constexpr int kLH = kTY + kHalo;              // 12
 
+typedef float f2 __attribute__((ext_vector_type(2)));
+// weights through a constant-address-space pointer -> scalar (SMEM) loads
+typedef const __attribute__((address_space(4))) float *cfloat_ptr;
+
 struct ArmGeom {
     int n;
     int h[CCMI_MAX_GRIDS], w[CCMI_MAX_GRIDS], off[CCMI_MAX_GRIDS];
@@ -91,65 +95,59 @@ __global__ __launch_bounds__(kThreads) void arm_fwd_kernel(
     }
     __syncthreads();
 
-    const float *p = params + (int64_t)b * pstride;
+    const cfloat_ptr p = (cfloat_ptr)(size_t)(params + (int64_t)b * pstride);
     const int cx = threadIdx.x % kTX;
     const int cy0 = threadIdx.x / kTX;
 
-    float a[kNL][D];
+    // the two latents of a thread travel as one packed pair (v_pk_fma_f32): every
+    // wave-uniform weight feeds both with one instruction
+    static_assert(kNL == 2, "packed pair layout");
+    f2 a[D];
 #pragma unroll
-    for (int n = 0; n < kNL; ++n) {
-        const int cy = cy0 + n * kRowsPerPass;
-#pragma unroll
-        for (int i = 0; i < D; ++i) {
-            int dy, dx;
-            ctx_offset<D>(i, dy, dx);
-            a[n][i] = tile[cy + kHalo + dy][cx + kHalo + dx];
-        }
+    for (int i = 0; i < D; ++i) {
+        int dy, dx;
+        ctx_offset<D>(i, dy, dx);
+        a[i] = f2{tile[cy0 + kHalo + dy][cx + kHalo + dx], tile[cy0 + kRowsPerPass + kHalo + dy][cx + kHalo + dx]};
     }
 
     for (int layer = 0; layer < nh; ++layer) {
-        const float *Wl = p + layer * (D * D + D);
-        const float *bl = Wl + D * D;
-        float o[kNL][D];
+        const cfloat_ptr Wl = p + layer * (D * D + D);
+        const cfloat_ptr bl = Wl + D * D;
+        f2 o[D];
 #pragma unroll
         for (int j = 0; j < D; ++j) {
-            const float bj = bl[j];
+            f2 acc = f2(0.f);
 #pragma unroll
-            for (int n = 0; n < kNL; ++n) {
-                float acc = 0.f;
-#pragma unroll
-                for (int i = 0; i < D; ++i) acc = fmaf(Wl[j * D + i], a[n][i], acc);
-                o[n][j] = fmaxf((acc + bj) + a[n][j], 0.f); // F.linear(x) + x, then ReLU
-            }
+            for (int i = 0; i < D; ++i) acc = __builtin_elementwise_fma(f2(Wl[j * D + i]), a[i], acc);
+            // F.linear(x) + x, then ReLU
+            o[j] = __builtin_elementwise_max((acc + f2(bl[j])) + a[j], f2(0.f));
         }
 #pragma unroll
-        for (int n = 0; n < kNL; ++n)
-#pragma unroll
-            for (int j = 0; j < D; ++j) a[n][j] = o[n][j];
+        for (int j = 0; j < D; ++j) a[j] = o[j];
     }
 
-    const float *Wo = p + nh * (D * D + D);
-    const float b_mu = Wo[2 * D], b_ls = Wo[2 * D + 1];
+    const cfloat_ptr Wo = p + nh * (D * D + D);
+    f2 m = f2(0.f), ls = f2(0.f);
+#pragma unroll
+    for (int i = 0; i < D; ++i) {
+        m = __builtin_elementwise_fma(f2(Wo[i]), a[i], m);
+        ls = __builtin_elementwise_fma(f2(Wo[D + i]), a[i], ls);
+    }
+    m += f2(Wo[2 * D]);
+    ls += f2(Wo[2 * D + 1]);
 #pragma unroll
     for (int n = 0; n < kNL; ++n) {
         const int y = y0 + cy0 + n * kRowsPerPass, x = x0 + cx;
-        float m = 0.f, ls = 0.f;
-#pragma unroll
-        for (int i = 0; i < D; ++i) {
-            m = fmaf(Wo[i], a[n][i], m);
-            ls = fmaf(Wo[D + i], a[n][i], ls);
-        }
-        m += b_mu;
-        ls += b_ls;
+        const float mn = n ? m.y : m.x, lsn = n ? ls.y : ls.x;
         if (y < H && x < W) {
-            const float sc = expf(fminf(fmaxf(ls - 4.f, -4.6f), 5.0f));
+            const float sc = expf(fminf(fmaxf(lsn - 4.f, -4.6f), 5.0f));
             const float q = tile[cy0 + n * kRowsPerPass + kHalo][cx + kHalo];
             const int64_t idx = (int64_t)b * ostride + g.off[l] + y * W + x;
-            if (o_mu) o_mu[idx] = m;
+            if (o_mu) o_mu[idx] = mn;
             if (o_scale) o_scale[idx] = sc;
-            if (o_log_scale) o_log_scale[idx] = ls;
+            if (o_log_scale) o_log_scale[idx] = lsn;
             if (o_rate) {
-                const float pr = fmaxf(laplace_cdf(q + 0.5f, m, sc) - laplace_cdf(q - 0.5f, m, sc), 1.52587890625e-05f);
+                const float pr = fmaxf(laplace_cdf(q + 0.5f, mn, sc) - laplace_cdf(q - 0.5f, mn, sc), 1.52587890625e-05f);
                 o_rate[idx] = -log2f(pr);
             }
         }

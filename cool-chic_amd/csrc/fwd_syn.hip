@@ -52,21 +52,38 @@ struct FusedArgs {
 
 __device__ __forceinline__ int clampi(int v, int hi) { return v < 0 ? 0 : (v > hi ? hi : v); }
 
+typedef float f2 __attribute__((ext_vector_type(2)));
+// Weights are read through a constant-address-space pointer: the loads are wave-uniform
+// and the buffer is never written by the kernel, so they become scalar (SMEM) loads even
+// after the kernel's own global stores (which would otherwise force vector loads).
+typedef const __attribute__((address_space(4))) float *cfloat_ptr;
+
 // Fused head + 3x3 tail.  The workgroup's working region is a fixed 32 x 64 window
-// (2048 pixels, 8 per thread): the output tile is the window minus a halo of one pixel
-// per 3x3 layer.  All stages share the window's coordinate frame (pitch 64); stage t is
-// valid on rows/cols [t, 32-t) x [t, 64-t).  Thread (c = tid & 63, r0 = tid >> 6) owns
-// column c of rows r0, r0+4, ...; the head processes 4 rows per pass so each weight
-// (wave-uniform, scalar-loaded) feeds 4 FMAs, and hidden activations are consumed as
-// they are produced (never stored).
-constexpr int kRW = 64, kRH = 32, kRegion = kRW * kRH;
-constexpr int kRowsPerThread = kRH / (kThreads / kRW); // 8
-constexpr int kNP = 4;                                  // rows per head pass
+// (2048 pixels, 512 threads, 4 per thread): the output tile is the window minus a halo
+// of one pixel per 3x3 layer.  All stages share the window's coordinate frame (pitch
+// 64); stage t is valid on rows/cols [t, 32-t) x [t, 64-t).  Thread (c = tid & 63,
+// g = tid >> 6) owns column c of the 4 consecutive rows 4g .. 4g+3 in every stage.
+//  * head: packed fp32 (v_pk_fma_f32) over pixel pairs, wave-uniform weights from
+//    SGPRs, hidden activations consumed as they are produced (never stored);
+//  * 3x3 layers: the thread slides a 3-row register window down its 4 rows, so a
+//    pixel costs 3*CMID LDS reads instead of 9*CMID.  Window row i maps to image row
+//    clamp(oy + i) (replicate padding); rows whose image row lies outside the image
+//    or outside the stage's valid band are computed but never read or stored, which
+//    keeps control flow uniform.
+constexpr int kFThreads = 512;
+constexpr int kRW = 64, kRH = 32;
+constexpr int kPlane = kRW * (kRH + 2); // LDS plane: window rows -1 .. kRH (guard rows)
+constexpr int kRowsPerThread = kRH / (kFThreads / kRW); // 4
 
 template <int CIN, int CMID>
-__global__ __launch_bounds__(kThreads) void syn_fused_kernel(FusedArgs A)
+__global__ __launch_bounds__(kFThreads) void syn_fused_kernel(FusedArgs A)
 {
-    __shared__ float s_buf[2][CMID][kRegion];
+    constexpr int NR = kRowsPerThread;
+    constexpr int NW = CMID * CMID * 9 + CMID; // weights + biases of one 3x3 layer
+    __shared__ float s_buf[2][CMID][kPlane];
+    // 3x3 weights staged in LDS: read back as broadcast ds_read_b128 into VGPRs (the
+    // 81+ weights of a layer do not fit the SGPR budget next to the head's state)
+    __shared__ __attribute__((aligned(16))) float s_w[kMaxSp][(NW + 3) & ~3];
 
     const int b = blockIdx.y;
     const int halo = A.n_sp;
@@ -74,130 +91,169 @@ __global__ __launch_bounds__(kThreads) void syn_fused_kernel(FusedArgs A)
     const int y0 = (blockIdx.x / A.tiles_x) * TY;
     const int x0 = (blockIdx.x % A.tiles_x) * TX;
     const int oy = y0 - halo, ox = x0 - halo; // global coords of window (0,0)
-    const float *prm = A.params + (int64_t)b * A.pstride;
+    const cfloat_ptr prm = (cfloat_ptr)(size_t)(A.params + (int64_t)b * A.pstride);
     const float *in = A.in + (int64_t)b * A.in_stride;
     float *out = A.out + (int64_t)b * A.out_stride;
     const int64_t plane = (int64_t)A.H * A.W;
     const int c = threadIdx.x & (kRW - 1);
-    const int r0 = threadIdx.x >> 6;
+    const int rb = (threadIdx.x >> 6) * NR; // first window row of this thread
     const int gx = ox + c;
     const int cxg = clampi(gx, A.W - 1);
 
+    for (int i = threadIdx.x; i < A.n_sp * NW; i += kFThreads) {
+        const int l = i / NW, j = i - l * NW;
+        s_w[l][j] = prm[A.sp[l].w_off + j]; // biases follow the weights in the block
+    }
+
     // ------------------------ pass 0: per-pixel 1x1 head ------------------------
-    const float *w0 = prm + A.w0_off, *b0 = prm + A.b0_off;
-    const float *w1 = prm + A.w1_off, *b1 = prm + A.b1_off;
-    const int hid = A.n_head == 2 ? A.hid : 0;
+    {
+        const cfloat_ptr w0 = prm + A.w0_off, b0 = prm + A.b0_off;
+        const cfloat_ptr w1 = prm + A.w1_off, b1 = prm + A.b1_off;
+        float x[NR][CIN];
+        float o[NR][CMID];
 #pragma unroll
-    for (int g = 0; g < kRowsPerThread / kNP; ++g) {
-        float x[kNP][CIN];
-        float o[kNP][CMID];
-#pragma unroll
-        for (int p = 0; p < kNP; ++p) {
-            const int r = r0 + 4 * (g * kNP + p);
-            const int64_t pix = (int64_t)clampi(oy + r, A.H - 1) * A.W + cxg;
+        for (int p = 0; p < NR; ++p) {
+            const int64_t pix = (int64_t)clampi(oy + rb + p, A.H - 1) * A.W + cxg;
 #pragma unroll
             for (int k = 0; k < CIN; ++k) x[p][k] = in[k * plane + pix];
-#pragma unroll
-            for (int m = 0; m < CMID; ++m) o[p][m] = 0.f;
         }
-        if (hid > 0) {
+        if (A.n_head == 2) {
+            const int hid = A.hid;
+            // fmaxf(acc, lo0) is the optional ReLU without a per-element select
+            const f2 lo0 = f2(A.relu0 ? 0.f : -INFINITY);
+            f2 xp[NR / 2][CIN], op[NR / 2][CMID];
+#pragma unroll
+            for (int q = 0; q < NR / 2; ++q) {
+#pragma unroll
+                for (int k = 0; k < CIN; ++k) xp[q][k] = f2{x[2 * q][k], x[2 * q + 1][k]};
+#pragma unroll
+                for (int m = 0; m < CMID; ++m) op[q][m] = f2(0.f);
+            }
+#pragma unroll 2
             for (int j = 0; j < hid; ++j) {
-                const float *wj = w0 + j * CIN;
-                const float bj = b0[j];
-                float wm[CMID];
+                const cfloat_ptr wj = w0 + j * CIN;
+                const f2 bj = f2(b0[j]);
+                f2 wm[CMID];
 #pragma unroll
-                for (int m = 0; m < CMID; ++m) wm[m] = w1[m * hid + j];
+                for (int m = 0; m < CMID; ++m) wm[m] = f2(w1[m * hid + j]);
 #pragma unroll
-                for (int p = 0; p < kNP; ++p) {
-                    float acc = 0.f;
+                for (int q = 0; q < NR / 2; ++q) {
+                    f2 acc = bj;
 #pragma unroll
-                    for (int k = 0; k < CIN; ++k) acc = fmaf(wj[k], x[p][k], acc);
-                    acc += bj;
-                    if (A.relu0) acc = fmaxf(acc, 0.f);
+                    for (int k = 0; k < CIN; ++k) acc = __builtin_elementwise_fma(f2(wj[k]), xp[q][k], acc);
+                    acc = __builtin_elementwise_max(acc, lo0);
 #pragma unroll
-                    for (int m = 0; m < CMID; ++m) o[p][m] = fmaf(wm[m], acc, o[p][m]);
+                    for (int m = 0; m < CMID; ++m) op[q][m] = __builtin_elementwise_fma(wm[m], acc, op[q][m]);
                 }
             }
+            const float lo1 = A.relu1 ? 0.f : -INFINITY;
 #pragma unroll
-            for (int p = 0; p < kNP; ++p)
+            for (int q = 0; q < NR / 2; ++q)
 #pragma unroll
                 for (int m = 0; m < CMID; ++m) {
-                    float v = o[p][m] + b1[m];
-                    o[p][m] = A.relu1 ? fmaxf(v, 0.f) : v;
+                    o[2 * q][m] = fmaxf(op[q][m].x + b1[m], lo1);
+                    o[2 * q + 1][m] = fmaxf(op[q][m].y + b1[m], lo1);
                 }
         } else {
+            const float lo0 = A.relu0 ? 0.f : -INFINITY;
 #pragma unroll
             for (int m = 0; m < CMID; ++m) {
                 const float bm = b0[m];
 #pragma unroll
-                for (int p = 0; p < kNP; ++p) {
-                    float acc = 0.f;
+                for (int p = 0; p < NR; ++p) {
+                    float acc = bm;
 #pragma unroll
                     for (int k = 0; k < CIN; ++k) acc = fmaf(w0[m * CIN + k], x[p][k], acc);
-                    acc += bm;
-                    o[p][m] = A.relu0 ? fmaxf(acc, 0.f) : acc;
+                    o[p][m] = fmaxf(acc, lo0);
                 }
             }
         }
+        if (halo == 0) {
 #pragma unroll
-        for (int p = 0; p < kNP; ++p) {
-            const int r = r0 + 4 * (g * kNP + p);
-            if (halo == 0) {
-                const int gy = oy + r;
+            for (int p = 0; p < NR; ++p) {
+                const int gy = oy + rb + p;
                 if (gy < A.H && gx < A.W)
 #pragma unroll
                     for (int m = 0; m < CMID; ++m) out[m * plane + (int64_t)gy * A.W + gx] = o[p][m];
-            } else {
-#pragma unroll
-                for (int m = 0; m < CMID; ++m) s_buf[0][m][r * kRW + c] = o[p][m];
             }
+            return;
         }
+#pragma unroll
+        for (int p = 0; p < NR; ++p)
+#pragma unroll
+            for (int m = 0; m < CMID; ++m) s_buf[0][m][(rb + p + 1) * kRW + c] = o[p][m];
     }
-    if (halo == 0) return;
 
     // ------------------------ 3x3 layers, replicate padding ------------------------
+    // Every LDS image is kept "pre-clamped" along rows: a window row outside the image
+    // holds the value of the nearest image row wherever it can be read.  The head computes
+    // all window rows at clamped coordinates; a 3x3 layer stores its in-image rows and the
+    // edge rows again one row further out (the only out-of-image rows an in-image output
+    // reads).  So the vertical neighbours of window row r are simply rows r-1, r+1, and a
+    // thread reads row pairs {r, r+1} straight into packed registers.  Columns are lanes:
+    // the horizontal neighbours use clamped columns lx[].
+    int lx[3];
+#pragma unroll
+    for (int d = 0; d < 3; ++d) lx[d] = clampi(cxg + d - 1, A.W - 1) - ox;
+    const bool col_in = gx < A.W;
     int cur = 0;
     for (int s = 0; s < A.n_sp; ++s) {
         __syncthreads();
-        const int t = s + 1; // valid margin of this layer's output within the window
+        const int t = s + 1;
         const bool last = s == A.n_sp - 1;
-        const float *wt = prm + A.sp[s].w_off;
-        const float *bs = prm + A.sp[s].b_off;
-        const bool col_ok = c >= t && c < kRW - t;
-        int lx[3];
+        const float *wt = s_w[s];
+        const float *bs = s_w[s] + CMID * CMID * 9;
+        const float lo = A.sp[s].relu ? 0.f : -INFINITY;
+        const float rsd = A.sp[s].residual ? 1.f : 0.f;
+        // plane row of window row (rb - 1) in this thread's column
+        const float *src = &s_buf[cur][0][0] + rb * kRW + c;
 #pragma unroll
-        for (int d = 0; d < 3; ++d) lx[d] = clampi(cxg + d - 1, A.W - 1) - ox;
-        for (int r = r0 + t; r < kRH - t; r += 4) {
-            const int gy = oy + r;
-            if (!col_ok || (last && (gy >= A.H || gx >= A.W))) continue;
-            const int cyg = clampi(gy, A.H - 1);
-            int ly[3];
+        for (int q = 0; q < NR / 2; ++q) {
+            // output rows rb + 2q, rb + 2q + 1 read window rows rb + 2q - 1 .. rb + 2q + 2
+            f2 P[3][CMID][3]; // P[dy] = {row rb+2q-1+dy, row rb+2q+dy}
 #pragma unroll
-            for (int d = 0; d < 3; ++d) ly[d] = (clampi(cyg + d - 1, A.H - 1) - oy) * kRW;
-            float nb[CMID][3][3];
+            for (int dy = 0; dy < 3; ++dy)
 #pragma unroll
-            for (int k = 0; k < CMID; ++k)
+                for (int k = 0; k < CMID; ++k)
 #pragma unroll
-                for (int dy = 0; dy < 3; ++dy)
-#pragma unroll
-                    for (int dx = 0; dx < 3; ++dx) nb[k][dy][dx] = s_buf[cur][k][ly[dy] + lx[dx]];
+                    for (int d = 0; d < 3; ++d) {
+                        const float *e = src + k * kPlane + (2 * q + dy) * kRW + (lx[d] - c);
+                        P[dy][k][d] = f2{e[0], e[kRW]};
+                    }
+            f2 acc[CMID];
 #pragma unroll
             for (int m = 0; m < CMID; ++m) {
-                float acc = 0.f;
+                // one output channel's weights in flight at a time (bounds VGPR use)
+                __builtin_amdgcn_sched_barrier(0);
+                acc[m] = f2(bs[m]);
 #pragma unroll
                 for (int k = 0; k < CMID; ++k)
 #pragma unroll
                     for (int dy = 0; dy < 3; ++dy)
 #pragma unroll
                         for (int dx = 0; dx < 3; ++dx)
-                            acc = fmaf(wt[((m * CMID + k) * 3 + dy) * 3 + dx], nb[k][dy][dx], acc);
-                float v = acc + bs[m];
-                if (A.sp[s].residual) v += nb[m][1][1]; // the input at the clamped centre
-                if (A.sp[s].relu) v = fmaxf(v, 0.f);
-                if (last)
-                    out[m * plane + (int64_t)gy * A.W + gx] = v;
-                else
-                    s_buf[cur ^ 1][m][r * kRW + c] = v;
+                            acc[m] = __builtin_elementwise_fma(f2(wt[((m * CMID + k) * 3 + dy) * 3 + dx]),
+                                                               P[dy][k][dx], acc[m]);
+                // residual: the input at the centre
+                acc[m] = __builtin_elementwise_max(__builtin_elementwise_fma(f2(rsd), P[1][m][1], acc[m]), f2(lo));
+            }
+#pragma unroll
+            for (int h = 0; h < 2; ++h) {
+                const int r = rb + 2 * q + h, gy = oy + r;
+                if (last) {
+                    if (r >= t && r < kRH - t && c >= t && c < kRW - t && gy < A.H && col_in)
+#pragma unroll
+                        for (int m = 0; m < CMID; ++m) out[m * plane + (int64_t)gy * A.W + gx] = h ? acc[m].y : acc[m].x;
+                } else if (gy >= 0 && gy < A.H) {
+                    float *dst = &s_buf[cur ^ 1][0][0] + (r + 1) * kRW + c;
+#pragma unroll
+                    for (int m = 0; m < CMID; ++m) {
+                        const float v = h ? acc[m].y : acc[m].x;
+                        dst[m * kPlane] = v;
+                        if (gy == 0) dst[m * kPlane - kRW] = v;     // replicate above the image
+                        if (gy == A.H - 1) dst[m * kPlane + kRW] = v; // and below it
+                    }
+                }
             }
         }
         cur ^= 1;
@@ -335,14 +391,14 @@ template <int CMID>
 void launch_fused(dim3 grid, hipStream_t s, const FusedArgs &fa)
 {
     switch (fa.cin) {
-    case 1: hipLaunchKernelGGL((syn_fused_kernel<1, CMID>), grid, dim3(kThreads), 0, s, fa); break;
-    case 2: hipLaunchKernelGGL((syn_fused_kernel<2, CMID>), grid, dim3(kThreads), 0, s, fa); break;
-    case 3: hipLaunchKernelGGL((syn_fused_kernel<3, CMID>), grid, dim3(kThreads), 0, s, fa); break;
-    case 4: hipLaunchKernelGGL((syn_fused_kernel<4, CMID>), grid, dim3(kThreads), 0, s, fa); break;
-    case 5: hipLaunchKernelGGL((syn_fused_kernel<5, CMID>), grid, dim3(kThreads), 0, s, fa); break;
-    case 6: hipLaunchKernelGGL((syn_fused_kernel<6, CMID>), grid, dim3(kThreads), 0, s, fa); break;
-    case 7: hipLaunchKernelGGL((syn_fused_kernel<7, CMID>), grid, dim3(kThreads), 0, s, fa); break;
-    case 8: hipLaunchKernelGGL((syn_fused_kernel<8, CMID>), grid, dim3(kThreads), 0, s, fa); break;
+    case 1: hipLaunchKernelGGL((syn_fused_kernel<1, CMID>), grid, dim3(kFThreads), 0, s, fa); break;
+    case 2: hipLaunchKernelGGL((syn_fused_kernel<2, CMID>), grid, dim3(kFThreads), 0, s, fa); break;
+    case 3: hipLaunchKernelGGL((syn_fused_kernel<3, CMID>), grid, dim3(kFThreads), 0, s, fa); break;
+    case 4: hipLaunchKernelGGL((syn_fused_kernel<4, CMID>), grid, dim3(kFThreads), 0, s, fa); break;
+    case 5: hipLaunchKernelGGL((syn_fused_kernel<5, CMID>), grid, dim3(kFThreads), 0, s, fa); break;
+    case 6: hipLaunchKernelGGL((syn_fused_kernel<6, CMID>), grid, dim3(kFThreads), 0, s, fa); break;
+    case 7: hipLaunchKernelGGL((syn_fused_kernel<7, CMID>), grid, dim3(kFThreads), 0, s, fa); break;
+    case 8: hipLaunchKernelGGL((syn_fused_kernel<8, CMID>), grid, dim3(kFThreads), 0, s, fa); break;
     }
 }
 

@@ -155,6 +155,147 @@ __global__ __launch_bounds__(kThreads) void ups_level_kernel(LevelArgs A)
     }
 }
 
+// ---------------------------------------------------------------------------------------------
+// Specialised level kernel for compile-time kernel sizes (the reference's defaults are
+// K = 8 transposed taps, KP = 7 refine taps).  Differences from the generic kernel:
+//   * one staging pass loads the refine input and the source tiles of ALL channels, so a
+//     tile costs 2 barriers instead of 3 * (C + 1);
+//   * the polyphase loops are unrolled: a thread produces an (even, odd) output pair from
+//     K/2 + 1 shared source samples, horizontally and then vertically;
+//   * no per-element division: all pitches are compile-time.
+// ---------------------------------------------------------------------------------------------
+constexpr int kMaxC = CCMI_MAX_GRIDS - 1; // channels of the source stack
+
+template <int K, int KP>
+struct UpsTile {
+    static constexpr int K2 = K / 2;
+    static constexpr int D0 = -((K2 + 1) / 2);      // min source offset over both parities
+    static constexpr int NS = K2 + 1;               // source samples shared by an (even, odd) pair
+    static constexpr int SH = kTY / 2 + NS - 1;     // source tile rows
+    static constexpr int SW = kTX / 2 + NS - 1;     // source tile cols
+    static constexpr int PAD = KP / 2;
+    static constexpr int RH = kTY + KP - 1, RW = kTX + KP - 1;
+    // tap used by parity a at source offset d (or -1)
+    static constexpr int tap(int a, int d) { return (a + K2 - 1 - 2 * d >= 0 && a + K2 - 1 - 2 * d < K) ? a + K2 - 1 - 2 * d : -1; }
+};
+
+template <int K, int KP>
+__global__ __launch_bounds__(kThreads) void ups_level_fixed(LevelArgs A)
+{
+    using T = UpsTile<K, KP>;
+    static_assert(T::NS == K / 2 + 1, "");
+    __shared__ float s_ref[T::RH * T::RW];
+    __shared__ float s_refh[T::RH * kTX];
+    __shared__ float s_src[kMaxC * T::SH * T::SW];
+    __shared__ float s_h[kMaxC * T::SH * kTX];
+
+    const int b = blockIdx.y;
+    const int y0 = (blockIdx.x / A.tiles_x) * kTY;
+    const int x0 = (blockIdx.x % A.tiles_x) * kTX;
+    const float *prm = A.params + (int64_t)b * A.pstride;
+    float wu[K], wr[KP];
+#pragma unroll
+    for (int k = 0; k < K; ++k) wu[k] = prm[A.up_off + k];
+#pragma unroll
+    for (int k = 0; k < KP; ++k) wr[k] = prm[A.pre_off + k];
+    float *dst = A.dst + (int64_t)b * A.dst_stride;
+    const int64_t dplane = (int64_t)A.hd * A.wd;
+    const int tid = threadIdx.x;
+    const int C = A.C;
+
+    // ---- stage: refine input (zero padded) and every source channel (replicate clamped) ----
+    {
+        const float *rs = A.ref_src + (int64_t)b * A.ref_stride;
+        for (int i = tid; i < T::RH * T::RW; i += kThreads) {
+            const int r = i / T::RW, c = i - r * T::RW;
+            const int y = y0 - T::PAD + r, x = x0 - T::PAD + c;
+            float v = 0.f;
+            if (y >= 0 && y < A.hd && x >= 0 && x < A.wd) {
+                v = rs[y * A.wd + x];
+                if (A.ref_quant) v = rintf(A.gain * v);
+            }
+            s_ref[i] = v;
+        }
+        const float *src = A.src + (int64_t)b * A.src_stride;
+        const int64_t splane = (int64_t)A.hs * A.ws;
+        const int sy0 = y0 / 2 + T::D0, sx0 = x0 / 2 + T::D0;
+        const int n = C * T::SH * T::SW;
+        for (int i = tid; i < n; i += kThreads) {
+            const int c = i / (T::SH * T::SW), rem = i - c * (T::SH * T::SW);
+            const int r = rem / T::SW, cc = rem - r * T::SW;
+            const int y = clampi(sy0 + r, A.hs - 1), x = clampi(sx0 + cc, A.ws - 1);
+            float v = src[c * splane + y * A.ws + x];
+            if (A.src_quant) v = rintf(A.gain * v);
+            s_src[i] = v;
+        }
+    }
+    __syncthreads();
+
+    // ---- horizontal passes ----
+    for (int i = tid; i < T::RH * kTX; i += kThreads) {
+        const int r = i / kTX, c = i - r * kTX;
+        const float *p = s_ref + r * T::RW + c;
+        float acc = 0.f;
+#pragma unroll
+        for (int k = 0; k < KP; ++k) acc = fmaf(wr[k], p[k], acc);
+        s_refh[i] = acc;
+    }
+    {
+        // one (even, odd) destination column pair per item: source column j = x0/2 + q
+        const int n = C * T::SH * (kTX / 2);
+        for (int i = tid; i < n; i += kThreads) {
+            const int row = i / (kTX / 2), q = i - row * (kTX / 2); // row = c * SH + r
+            const float *p = s_src + row * T::SW + q;              // offset D0 at index 0
+            float e = 0.f, o = 0.f;
+#pragma unroll
+            for (int m = 0; m < T::NS; ++m) {
+                const float v = p[m];
+                const int d = T::D0 + m;
+                const int te = T::tap(0, d), to = T::tap(1, d);
+                if (te >= 0) e = fmaf(wu[te], v, e);
+                if (to >= 0) o = fmaf(wu[to], v, o);
+            }
+            *reinterpret_cast<float2 *>(s_h + row * kTX + 2 * q) = make_float2(e, o);
+        }
+    }
+    __syncthreads();
+
+    // ---- vertical passes + coalesced stores ----
+    for (int i = tid; i < kTY * kTX; i += kThreads) {
+        const int r = i / kTX, c = i - r * kTX;
+        const int y = y0 + r, x = x0 + c;
+        if (y < A.hd && x < A.wd) {
+            float acc = 0.f;
+#pragma unroll
+            for (int k = 0; k < KP; ++k) acc = fmaf(wr[k], s_refh[(r + k) * kTX + c], acc);
+            dst[(int64_t)y * A.wd + x] = acc + s_ref[(r + T::PAD) * T::RW + c + T::PAD];
+        }
+    }
+    {
+        const int n = C * (kTY / 2) * kTX;
+        for (int i = tid; i < n; i += kThreads) {
+            const int c = i / ((kTY / 2) * kTX), rem = i - c * ((kTY / 2) * kTX);
+            const int q = rem / kTX, x = rem - q * kTX; // destination rows y0 + 2q, y0 + 2q + 1
+            const float *p = s_h + (c * T::SH + q) * kTX + x;
+            float e = 0.f, o = 0.f;
+#pragma unroll
+            for (int m = 0; m < T::NS; ++m) {
+                const float v = p[m * kTX];
+                const int d = T::D0 + m;
+                const int te = T::tap(0, d), to = T::tap(1, d);
+                if (te >= 0) e = fmaf(wu[te], v, e);
+                if (to >= 0) o = fmaf(wu[to], v, o);
+            }
+            const int yd = y0 + 2 * q, xd = x0 + x;
+            if (xd < A.wd) {
+                float *out = dst + (int64_t)(c + 1) * dplane + (int64_t)yd * A.wd + xd;
+                if (yd < A.hd) out[0] = e;
+                if (yd + 1 < A.hd) out[A.wd] = o;
+            }
+        }
+    }
+}
+
 } // namespace
 
 extern "C" size_t ccmi_ups_workspace_bytes(int n_grids, const int *h, const int *w, int batch)
@@ -232,7 +373,10 @@ int ccmi_launch_ups_f32(const ccmi_ups_args *a, hipStream_t s)
         A.pre_off = a->n_ups * a->ups_k + (step % a->n_pre) * a->pre_k;
         A.tiles_x = ccmi_div_up(A.wd, kTX);
         dim3 grid(A.tiles_x * ccmi_div_up(A.hd, kTY), a->batch);
-        hipLaunchKernelGGL(ups_level_kernel, grid, dim3(kThreads), 0, s, A);
+        if (A.K == 8 && A.Kp == 7 && A.C <= kMaxC)
+            hipLaunchKernelGGL((ups_level_fixed<8, 7>), grid, dim3(kThreads), 0, s, A);
+        else
+            hipLaunchKernelGGL(ups_level_kernel, grid, dim3(kThreads), 0, s, A);
         CCMI_HIP_CHECK(hipGetLastError());
     }
     return CCMI_OK;
