@@ -64,13 +64,25 @@ def flops_per_frame():
     return {"arm": 2 * arm_mac, "ups": 2 * ups_mac, "syn": 2 * syn_mac, "n_lat": n_lat}
 
 
+def flops_fused_per_frame():
+    """The fused kernel: last upsampling step (level 1 -> 0) + synthesis (+ post, no flops)."""
+    fl = flops_per_frame()
+    h0, w0 = sizes()[0]
+    last_ups = 2 * h0 * w0 * (14 + 8 * (N_GRIDS - 1))
+    return last_ups + fl["syn"]
+
+
 def bytes_per_frame():
-    n_lat = sum(h * w for h, w in sizes())
+    s = sizes()
+    n_lat = sum(h * w for h, w in s)
     npx = H * W
+    h1, w1 = s[1]
     return {"arm": 4 * n_lat * 2,                       # read latents, write rate
             "ups": 4 * (n_lat + N_GRIDS * npx),          # read latents, write dense synthesis input
             "syn": 4 * (N_GRIDS * npx + 3 * npx),        # read dense input, write 3 planes
-            "post": 4 * (3 * npx + npx * 3 // 2)}
+            "post": 4 * (3 * npx + npx * 3 // 2),
+            # fused: read the level-1 stack + full-res latent, write the 420 frame
+            "decode_fused": 4 * ((N_GRIDS - 1) * h1 * w1 + npx + npx * 3 // 2)}
 
 
 def make_inputs(B, dev, seed):
@@ -116,21 +128,28 @@ class Pipeline:
         self.synargs = F._syn_args(self.dense, HOP, inp["syn"], self.syn, B, N_GRIDS, H, W)
         self.post = ccmi.PostArgs(in_=p(self.syn), in_stride=3 * H * W, h=H, w=W, bitdepth=8, yuv420=1,
                                   out=p(self.yuv), out_stride=self.yuv.shape[1], batch=B)
+        # fused decode tail: pyramid (levels 6 -> 1) then ONE kernel for the last
+        # upsampling step + synthesis + 420 post (no dense stack, no raw synthesis output)
+        self.dec = [ccmi.DecodeArgs(ups=self.ups, syn=self.synargs, bitdepth=8, yuv420=1, out=p(self.yuv),
+                                    out_stride=self.yuv.shape[1], stages=st) for st in (1, 2)]
         self.byref = ctypes.byref
         self.stream = torch.cuda.current_stream(dev)
 
-    def step(self, events=None):
+    STAGES = {"fused": ["arm", "ups_pyramid", "decode_fused"], "staged": ["arm", "ups", "syn", "post"]}
+
+    def step(self, events=None, mode="fused"):
         import ccmi
         L, s, br = self.L, self.stream.cuda_stream, self.byref
-        if events: events[0].record(self.stream)
-        ccmi.check(L.ccmi_arm_forward_f32(br(self.arm), s))
-        if events: events[1].record(self.stream)
-        ccmi.check(L.ccmi_ups_forward_f32(br(self.ups), s))
-        if events: events[2].record(self.stream)
-        ccmi.check(L.ccmi_syn_forward_f32(br(self.synargs), s))
-        if events: events[3].record(self.stream)
-        ccmi.check(L.ccmi_post_f32(br(self.post), s))
-        if events: events[4].record(self.stream)
+        if mode == "fused":
+            calls = [(L.ccmi_arm_forward_f32, self.arm), (L.ccmi_decode_forward_f32, self.dec[0]),
+                     (L.ccmi_decode_forward_f32, self.dec[1])]
+        else:
+            calls = [(L.ccmi_arm_forward_f32, self.arm), (L.ccmi_ups_forward_f32, self.ups),
+                     (L.ccmi_syn_forward_f32, self.synargs), (L.ccmi_post_f32, self.post)]
+        for i, (fn, a) in enumerate(calls):
+            if events: events[i].record(self.stream)
+            ccmi.check(fn(br(a), s))
+        if events: events[len(calls)].record(self.stream)
 
 
 def cpu_baseline(inp, budget_s=12.0, max_frames=64):
@@ -231,6 +250,8 @@ def main():
     ap.add_argument("--batch", type=int, default=8, help="720p frames per step per GPU")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--decode-reps", type=int, default=8, help="class-E stream copies for the bit-exact decode leg")
+    ap.add_argument("--staged", action="store_true",
+                    help="run upsampling / synthesis / post as separate kernels (module-boundary path)")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -248,17 +269,19 @@ def main():
     inp = make_inputs(B, dev, seed=1000 * rank + 1)
     pipe = Pipeline(inp, B, dev)
 
+    mode = "staged" if args.staged else "fused"
+    names = Pipeline.STAGES[mode]
     for _ in range(args.warmup):
-        pipe.step()
+        pipe.step(mode=mode)
     torch.cuda.synchronize()
 
     # per-stage HIP events over the timed region (recorded on the launch stream)
-    ev = [[torch.cuda.Event(enable_timing=True) for _ in range(5)] for _ in range(args.steps)]
+    ev = [[torch.cuda.Event(enable_timing=True) for _ in range(len(names) + 1)] for _ in range(args.steps)]
     if dist: dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for k in range(args.steps):
-        pipe.step(ev[k])
+        pipe.step(ev[k], mode)
     torch.cuda.synchronize()
     t1 = time.perf_counter()
     if dist: dist.barrier()
@@ -269,10 +292,11 @@ def main():
         dt = float(t.item())
 
     stage_ms = {n: sum(ev[k][i].elapsed_time(ev[k][i + 1]) for k in range(args.steps)) / args.steps
-                for i, n in enumerate(["arm", "ups", "syn", "post"])}
+                for i, n in enumerate(names)}
     fl = flops_per_frame()
+    fl["decode_fused"] = flops_fused_per_frame()
     by = bytes_per_frame()
-    dom = max(("arm", "syn"), key=lambda n: stage_ms[n])
+    dom = max(("arm", "decode_fused" if mode == "fused" else "syn"), key=lambda n: stage_ms[n])
     achieved = fl[dom] * B / (stage_ms[dom] * 1e-3) / 1e12
     traffic, src = pmc_traffic(dom)
 
@@ -293,7 +317,9 @@ def main():
         "data": "synthetic (seeded N(0,0.5) latents, random-init hop weights per frame)",
         "config": {"workload": "1280x720 YUV420 8-bit frames, hop/c3x decoder (arm 16x2, syn 48-1/3-1/3-3r/3-3r, "
                                "7 latent grids), float forward ARM+rate -> upsampling -> synthesis -> 420 post",
-                   "frames_per_step_per_gpu": B, "parallelism": f"image-parallel x{world}"},
+                   "frames_per_step_per_gpu": B, "parallelism": f"image-parallel x{world}",
+                   "kernels": "ARM | upsampling pyramid | fused last-upsampling+synthesis+post" if mode == "fused"
+                   else "ARM | upsampling | synthesis | post"},
         "stage_ms_per_step": {k: round(v, 4) for k, v in stage_ms.items()},
         "roofline": {"bound": "mfma", "kernel": dom, "achieved": round(achieved, 3), "peak": PEAK_FP32_TFLOPS,
                      "unit": "TFLOP/s", "frac": round(achieved / PEAK_FP32_TFLOPS, 4),

@@ -24,7 +24,7 @@ OK, ERR_ARG, ERR_HIP, ERR_UNSUPPORTED, ERR_BITSTREAM, ERR_IO = range(6)
 EXPORTED = [
     "ccmi_last_error", "ccmi_version", "ccmi_device_count",
     "ccmi_arm_forward_f32", "ccmi_arm_context_f32", "ccmi_arm_mlp_f32", "ccmi_ups_workspace_bytes", "ccmi_ups_forward_f32",
-    "ccmi_syn_workspace_bytes", "ccmi_syn_forward_f32", "ccmi_post_f32",
+    "ccmi_syn_workspace_bytes", "ccmi_syn_forward_f32", "ccmi_post_f32", "ccmi_decode_forward_f32",
     "ccmi_decode_file", "ccmi_decode_batch", "ccmi_decode_output_size", "ccmi_decode_last_timing",
 ]
 
@@ -82,6 +82,13 @@ class PostArgs(C.Structure):
     ]
 
 
+class DecodeArgs(C.Structure):
+    _fields_ = [
+        ("ups", UpsArgs), ("syn", SynArgs), ("bitdepth", C.c_int), ("yuv420", C.c_int),
+        ("out", C.c_void_p), ("out_stride", C.c_int64), ("stages", C.c_int),
+    ]
+
+
 _lib = None
 
 
@@ -104,7 +111,8 @@ def lib() -> C.CDLL:
     L.ccmi_version.restype = C.c_int
     L.ccmi_device_count.restype = C.c_int
     for name, st in (("ccmi_arm_forward_f32", ArmArgs), ("ccmi_ups_forward_f32", UpsArgs),
-                     ("ccmi_syn_forward_f32", SynArgs), ("ccmi_post_f32", PostArgs)):
+                     ("ccmi_syn_forward_f32", SynArgs), ("ccmi_post_f32", PostArgs),
+                     ("ccmi_decode_forward_f32", DecodeArgs)):
         f = getattr(L, name)
         f.argtypes = [C.POINTER(st), C.c_void_p]
         f.restype = C.c_int

@@ -12,7 +12,7 @@ from typing import Sequence
 
 import torch
 
-from . import (ArmArgs, MAX_GRIDS, MAX_SYN_LAYERS, PostArgs, SynArgs, SynLayer, UpsArgs, check, lib, ptr,
+from . import (ArmArgs, DecodeArgs, MAX_GRIDS, MAX_SYN_LAYERS, PostArgs, SynArgs, SynLayer, UpsArgs, check, lib, ptr,
                require_cuda, stream_handle)
 
 
@@ -168,6 +168,53 @@ def post_forward(x: torch.Tensor, bitdepth: int = 8, yuv420: bool = False) -> to
     check(lib().ccmi_post_f32(a, stream_handle(x.device)))
     if not yuv420:
         out = out.view(B, 3, H, W)
+    return out[0] if squeeze else out
+
+
+def decode_forward(latent: torch.Tensor, sizes, ups_params: torch.Tensor, ups_k: int, n_ups: int, pre_k: int,
+                   n_pre: int, layers, syn_params: torch.Tensor, gain: float = 16.0, quantize: bool = True,
+                   bitdepth: int = 8, yuv420: bool = False) -> torch.Tensor:
+    """Fused upsampling -> synthesis -> post (ccmi_decode_forward_f32): latent [B, N] ->
+    post-processed frames (layout of post_forward), or with bitdepth=0 the raw synthesis
+    output [B, C_out, H, W].  Raises CcmiError(ERR_UNSUPPORTED) for architectures
+    without a fused kernel (use ups_forward / syn_forward / post_forward)."""
+    squeeze = latent.dim() == 1
+    latent = latent.unsqueeze(0) if squeeze else latent
+    B, N = latent.shape
+    ups_params, ups_stride = _as_batch(ups_params, B)
+    syn_params, syn_stride = _as_batch(syn_params, B)
+    require_cuda(latent, ups_params, syn_params)
+    if N != n_latents(sizes):
+        raise ValueError(f"latent has {N} values, grids hold {n_latents(sizes)}")
+    L = len(sizes)
+    H, W = sizes[0]
+    if ups_params.shape[1] < n_ups * ups_k + n_pre * pre_k:
+        raise ValueError("ups params: wrong shape")
+    if syn_params.shape[1] < syn_param_count(L, layers):
+        raise ValueError("syn params: wrong shape")
+    latent = latent.float().contiguous()
+    ups_params = ups_params.float().contiguous()
+    syn_params = syn_params.float().contiguous()
+    n_out = int(layers[-1][0])
+    if bitdepth > 0:
+        n = H * W + 2 * (H // 2) * (W // 2) if yuv420 else n_out * H * W
+    else:
+        n = n_out * H * W
+    out = torch.empty(B, n, device=latent.device, dtype=torch.float32)
+    h, w = _grid_arrays(sizes)
+    nws = lib().ccmi_ups_workspace_bytes(L, h, w, B)
+    ws = torch.empty(max(nws, 4), device=latent.device, dtype=torch.uint8)
+    u = UpsArgs(latent=ptr(latent), latent_stride=N, n_grids=L, h=h, w=w, gain=float(gain),
+                quantize=int(bool(quantize)), ups_k=ups_k, n_ups=n_ups, pre_k=pre_k, n_pre=n_pre,
+                params=ptr(ups_params), param_stride=ups_stride, out=None, out_stride=0,
+                workspace=ptr(ws), workspace_bytes=nws, batch=B)
+    y = _syn_args(latent, layers, syn_params, out.view(B, -1, H, W) if (bitdepth == 0 or not yuv420) else out,
+                  B, L, H, W, syn_stride)
+    y.in_ = None
+    a = DecodeArgs(ups=u, syn=y, bitdepth=int(bitdepth), yuv420=int(bool(yuv420)), out=ptr(out), out_stride=n)
+    check(lib().ccmi_decode_forward_f32(a, stream_handle(latent.device)))
+    if bitdepth == 0 or not yuv420:
+        out = out.view(B, n_out, H, W)
     return out[0] if squeeze else out
 
 

@@ -352,6 +352,12 @@ template <int D, int NH>
 __global__ __launch_bounds__(64) void dec_arm_spec_kernel(const ArmStreamDesc *__restrict__ streams, int pitch)
 {
     static_assert(D <= 16, "one neuron per lane of a DPP row");
+#if defined(CCMI_ARM_STAMPS)
+    // [0] ARM pass (ctx + MLP + output sums)  [1] index + table  [2] CABAC  [3] ARM passes
+    // [4] coded latents  [5] setup  [6] latent loop
+    uint64_t st_acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    const uint64_t t_begin = __builtin_amdgcn_s_memtime();
+#endif
     extern __shared__ int32_t smem[];
     uint32_t *ctab = reinterpret_cast<uint32_t *>(smem);               // 17 x 50 x 2
     int32_t *ring = smem + 17 * 50 * 2;                                // kRing x pitch
@@ -425,6 +431,10 @@ __global__ __launch_bounds__(64) void dec_arm_spec_kernel(const ArmStreamDesc *_
     ctx_dydx<D>(o, cdy, cdx);
     const bool same_row = cdy == 0;
     int big = 0;
+#if defined(CCMI_ARM_STAMPS)
+    st_acc[5] = __builtin_amdgcn_s_memtime() - t_begin;
+    const uint64_t t_loop = __builtin_amdgcn_s_memtime();
+#endif
 
     for (int y = 0; y < h; ++y) {
         int32_t *row = ring + (y % kRing) * pitch + kPad;
@@ -439,32 +449,59 @@ __global__ __launch_bounds__(64) void dec_arm_spec_kernel(const ArmStreamDesc *_
             r1 = v;
             if (lane == 0) row[x] = v;
         };
-        int bm = 1, bend = w; // block flags of the current block, and its end column
-        for (int x = 0; x < w;) {
-            if (blk > 0 && (x & mask) == 0) {
-                bm = __builtin_amdgcn_readfirstlane((int)bmap[brow + (x >> shift)]);
-                bend = min(x + blk, w);
-            }
-            int L;
-            if (!(bm & 1)) {
-                // zero block: the whole remaining block at once
-                for (; x < bend; ++x) push(0, x);
-                continue;
-            } else if (bm & 2) {
-                if (x & mask) {
-                    push(r1, x);
-                    ++x;
-                    continue;
-                }
-                if (y & mask) {
-                    push(__builtin_amdgcn_readfirstlane(up[x]), x);
-                    ++x;
-                    continue;
-                }
-                L = 1; // the coded corner of a flat block
+        // n (>= 1) uncoded columns [x, x+n) written by the lanes in parallel; the last four
+        // values are re-read into r1..r4 (they are uniform)
+        auto fill = [&](int x, int n, int kind /*0 zero, 1 = r1, 2 = up*/) {
+            const int32_t c1 = r1;
+            for (int i = lane; i < n; i += 64) row[x + i] = kind == 0 ? 0 : kind == 1 ? c1 : up[x + i];
+            if (kind == 2) {
+                __builtin_amdgcn_s_waitcnt(0);
+                __builtin_amdgcn_wave_barrier();
+                auto at = [&](int j) { return __builtin_amdgcn_readfirstlane(row[j]); };
+                r4 = n >= 4 ? at(x + n - 4) : n == 3 ? r1 : n == 2 ? r2 : r3;
+                r3 = n >= 3 ? at(x + n - 3) : n == 2 ? r1 : r2;
+                r2 = n >= 2 ? at(x + n - 2) : r1;
+                r1 = at(x + n - 1);
             } else {
-                L = min(kSpec, bend - x);
+                const int32_t v = kind == 0 ? 0 : c1;
+                r4 = n >= 4 ? v : n == 3 ? r1 : n == 2 ? r2 : r3;
+                r3 = n >= 3 ? v : n == 2 ? r1 : r2;
+                r2 = n >= 2 ? v : r1;
+                r1 = v;
             }
+        };
+        int bm = 1, bend = 0; // flags of the current block and its end column
+        for (int x = 0; x < w;) {
+            int L;
+            if (blk > 0) {
+                if (x >= bend) {
+                    bm = __builtin_amdgcn_readfirstlane((int)bmap[brow + (x >> shift)]);
+                    bend = min((x | mask) + 1, w);
+                }
+                if (!(bm & 1)) {
+                    fill(x, bend - x, 0);
+                    x = bend;
+                    continue;
+                }
+                if (bm & 2) {
+                    if (y & mask) {
+                        fill(x, bend - x, 2);
+                        x = bend;
+                        continue;
+                    }
+                    if (x & mask) {
+                        fill(x, bend - x, 1);
+                        x = bend;
+                        continue;
+                    }
+                    L = 1; // the coded corner of a flat block
+                } else {
+                    L = min(kSpec, bend - x);
+                }
+            } else {
+                L = min(kSpec, w - x);
+            }
+            STAMP(t0);
 
             // context of lane (g, o): latent x+g, neighbour (cdy, cdx); same-row neighbours
             // at or right of x are the speculative zeros
@@ -478,46 +515,33 @@ __global__ __launch_bounds__(64) void dec_arm_spec_kernel(const ArmStreamDesc *_
                 else a = w24 ? arm_hidden_rows<D, true>(Wh[l], Bh[l], a) : arm_hidden_rows<D, false>(Wh[l], Bh[l], a);
             }
             const bool fo = NH > 0 ? w24 : f1;
-            const int32_t s0 = row_sum16(fo ? imul<true>(Wo0, a) : imul<false>(Wo0, a));
-            const int32_t s1 = row_sum16(fo ? imul<true>(Wo1, a) : imul<false>(Wo1, a));
-
-            int32_t sums0[kSpec], sums1[kSpec];
-            sums0[0] = __builtin_amdgcn_readlane(s0, 15) + bo0;
-            sums1[0] = __builtin_amdgcn_readlane(s1, 15) + bo1;
-            sums0[1] = __builtin_amdgcn_readlane(s0, 31) + bo0;
-            sums1[1] = __builtin_amdgcn_readlane(s1, 31) + bo1;
-            sums0[2] = __builtin_amdgcn_readlane(s0, 47) + bo0;
-            sums1[2] = __builtin_amdgcn_readlane(s1, 47) + bo1;
-            sums0[3] = __builtin_amdgcn_readlane(s0, 63) + bo0;
-            sums1[3] = __builtin_amdgcn_readlane(s1, 63) + bo1;
-            int32_t mrs[kSpec];
-            uint32_t sts[kSpec], stps[kSpec];
-#pragma unroll
-            for (int j = 0; j < kSpec; ++j) {
-                const int32_t m_0 = sums0[j], m_1 = sums1[j];
-                const int32_t mu = m_0 < 0 ? -((-m_0 + 128) >> 8) : (m_0 + 128) >> 8;
-                const int32_t ls = m_1 < 0 ? -((-m_1 + 128) >> 8) : (m_1 + 128) >> 8;
-                // get_val_mu_indicies (cc-contexts.h:20-48)
-                const int32_t mr = mu >= 0 ? ((mu + 128) >> 8) << 8 : -(((-mu + 128) >> 8) << 8);
-                int32_t mi = (mu - mr) * 16;
-                mi = (mi >= 0 ? (mi + 128) >> 8 : -((-mi + 128) >> 8)) + 8;
-                const int32_t lsp = ls + 256;
-                int32_t si = lsp < 0 ? 0 : (lsp * 5 + 128) >> 8;
-                si = si > 49 ? 49 : si;
-                const uint32_t ci = (uint32_t)(mi * 50 + si) * 2u;
-                const uint2 e = *reinterpret_cast<const uint2 *>(ctab + ci);
-                mrs[j] = mr;
-                sts[j] = __builtin_amdgcn_readfirstlane(e.x);
-                stps[j] = __builtin_amdgcn_readfirstlane(e.y);
-            }
+            const int32_t m_0 = row_sum16(fo ? imul<true>(Wo0, a) : imul<false>(Wo0, a)) + bo0;
+            const int32_t m_1 = row_sum16(fo ? imul<true>(Wo1, a) : imul<false>(Wo1, a)) + bo1;
+#if defined(CCMI_ARM_STAMPS)
+            __builtin_amdgcn_s_waitcnt(0);
+#endif
+            STAMP(t1);
+            // mu / scale -> context-table entry, in every lane at once (lane 16g+15 holds
+            // row g's sums; the other lanes compute harmless in-range garbage)
+            const int32_t mu = m_0 < 0 ? -((-m_0 + 128) >> 8) : (m_0 + 128) >> 8;
+            const int32_t ls = m_1 < 0 ? -((-m_1 + 128) >> 8) : (m_1 + 128) >> 8;
+            // get_val_mu_indicies (cc-contexts.h:20-48)
+            const int32_t mr = mu >= 0 ? ((mu + 128) >> 8) << 8 : -(((-mu + 128) >> 8) << 8);
+            int32_t mi = (mu - mr) * 16;
+            mi = (mi >= 0 ? (mi + 128) >> 8 : -((-mi + 128) >> 8)) + 8;
+            const int32_t lsp = ls + 256;
+            int32_t si = lsp < 0 ? 0 : (lsp * 5 + 128) >> 8;
+            si = si > 49 ? 49 : si;
+            const uint2 e = *reinterpret_cast<const uint2 *>(ctab + (uint32_t)(mi * 50 + si) * 2u);
+            const int32_t mq = mr >> 8;
+            STAMP(t2);
             // decode_single (cc-bac.h:192-231), in order, until the first non-zero latent
             int nd = 0;
 #pragma unroll 1
             for (int j = 0; j < L; ++j) {
-                // select chains keep the per-row scalars in SGPRs (no indexed register file)
-                const uint32_t st = j == 0 ? sts[0] : j == 1 ? sts[1] : j == 2 ? sts[2] : sts[3];
-                const uint32_t stp = j == 0 ? stps[0] : j == 1 ? stps[1] : j == 2 ? stps[2] : stps[3];
-                const int32_t mr = j == 0 ? mrs[0] : j == 1 ? mrs[1] : j == 2 ? mrs[2] : mrs[3];
+                const int src_lane = 16 * j + 15;
+                const uint32_t st = __builtin_amdgcn_readlane(e.x, src_lane);
+                const uint32_t stp = __builtin_amdgcn_readlane(e.y, src_lane);
                 int32_t val = 0;
                 if (cab.bin_static(st & 0xFF)) {
                     if (!cab.bin_static((st >> 8) & 0xFF)) val = 1;
@@ -526,12 +550,20 @@ __global__ __launch_bounds__(64) void dec_arm_spec_kernel(const ArmStreamDesc *_
                     else val = cab.expgolomb(0) + 4;
                     if (cab.bin_static(stp)) val = -val;
                 }
-                const int32_t q = (mr >> 8) + val;
+                const int32_t q = __builtin_amdgcn_readlane(mq, src_lane) + val;
                 big |= (q >= 32768 || q <= -32768);
                 push((int32_t)((uint32_t)q << kArmPrec), x + j);
                 ++nd;
                 if (q != 0) break;
             }
+            STAMP(t3);
+            ACC(0, t0, t1);
+            ACC(1, t1, t2);
+            ACC(2, t2, t3);
+#if defined(CCMI_ARM_STAMPS)
+            st_acc[3] += 1;
+            st_acc[4] += nd;
+#endif
             x += nd;
         }
         __syncthreads();
@@ -539,6 +571,11 @@ __global__ __launch_bounds__(64) void dec_arm_spec_kernel(const ArmStreamDesc *_
         for (int x = lane; x < w; x += 64) dst[x] = row[x];
         __syncthreads();
     }
+#if defined(CCMI_ARM_STAMPS)
+    st_acc[6] = __builtin_amdgcn_s_memtime() - t_loop;
+    if (lane == 0 && S.dbg)
+        for (int k = 0; k < 8; ++k) S.dbg[k] = st_acc[k];
+#endif
 }
 
 // ------------------------------------------------------------------ upsampling (integer)

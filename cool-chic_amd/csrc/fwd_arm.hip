@@ -14,7 +14,10 @@
 // same column, so every weight (wave-uniform, held in SGPRs via scalar loads) feeds two
 // FMAs.  LDS reads are lane-consecutive (conflict-free).  Grids of all resolutions
 // share one launch through a tile prefix table (no per-grid launches).
-#include "ccmi_internal.h"
+#include "fwd_common.h"
+
+using ccmi_fwd::cfloat_ptr;
+using ccmi_fwd::f2;
 
 namespace {
 
@@ -27,9 +30,6 @@ constexpr int kHalo = 4;
 constexpr int kLW = kTX + 2 * kHalo;          // 72
 constexpr int kLH = kTY + kHalo;              // 12
 
-typedef float f2 __attribute__((ext_vector_type(2)));
-// weights through a constant-address-space pointer -> scalar (SMEM) loads
-typedef const __attribute__((address_space(4))) float *cfloat_ptr;
 
 struct ArmGeom {
     int n;

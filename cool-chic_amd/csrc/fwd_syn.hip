@@ -19,44 +19,14 @@
 //
 // Any other architecture runs the generic per-layer kernel (one launch per layer,
 // ping-pong through the caller's workspace).
-#include "ccmi_internal.h"
+#include "fwd_common.h"
+
+using namespace ccmi_fwd;
 
 namespace {
 
 constexpr int kThreads = 256;
-constexpr int kMaxIn = 8;   // fused path: max synthesis input channels
-constexpr int kMaxMid = 4;  // fused path: max channels through the 3x3 layers
-constexpr int kMaxSp = 3;   // fused path: max number of 3x3 layers
 
-struct SpLayer {
-    int w_off, b_off; // offsets in the frame's parameter block
-    int residual, relu;
-};
-
-struct FusedArgs {
-    const float *in;
-    int64_t in_stride;
-    int cin, H, W;
-    int n_head;          // 1 or 2 1x1 layers
-    int hid;             // hidden width of a 2-layer head
-    int w0_off, b0_off, relu0;
-    int w1_off, b1_off, relu1;
-    int n_sp;            // 3x3 layers after the head
-    SpLayer sp[kMaxSp];
-    const float *params;
-    int64_t pstride;
-    float *out;
-    int64_t out_stride;
-    int tiles_x;
-};
-
-__device__ __forceinline__ int clampi(int v, int hi) { return v < 0 ? 0 : (v > hi ? hi : v); }
-
-typedef float f2 __attribute__((ext_vector_type(2)));
-// Weights are read through a constant-address-space pointer: the loads are wave-uniform
-// and the buffer is never written by the kernel, so they become scalar (SMEM) loads even
-// after the kernel's own global stores (which would otherwise force vector loads).
-typedef const __attribute__((address_space(4))) float *cfloat_ptr;
 
 // Fused head + 3x3 tail.  The workgroup's working region is a fixed 32 x 64 window
 // (2048 pixels, 512 threads, 4 per thread): the output tile is the window minus a halo
@@ -75,15 +45,53 @@ constexpr int kRW = 64, kRH = 32;
 constexpr int kPlane = kRW * (kRH + 2); // LDS plane: window rows -1 .. kRH (guard rows)
 constexpr int kRowsPerThread = kRH / (kFThreads / kRW); // 4
 
-template <int CIN, int CMID>
-__global__ __launch_bounds__(kFThreads) void syn_fused_kernel(FusedArgs A)
+// Fused-upsampling input (UPS = true): the window's CIN input channels are not read from
+// a [CIN][H][W] tensor but evaluated in the kernel from the level-1 stack and the
+// full-resolution latent (the last Upsampling step, same operation order as
+// ups_level_fixed<8, 7>): the horizontal passes of the 2x transposed conv (C = CIN-1
+// channels, kHsRows half-resolution rows) and of the refine (kHrRows rows) are staged in
+// LDS for the window's clamped image rectangle, and each head pixel finishes the vertical
+// passes from there.  The staging area aliases the second 3x3 ping-pong buffer, which is
+// first written after the head has finished reading it.
+// Output of channel m at (gy, gx): the synthesis value, or with A.qmax > 0 the
+// post-processed frame of FrameEncoder.forward (eval): round to the 2^bd - 1 grid, clamp
+// to [0, 1], and for yuv420 the chroma planes sampled at even rows / columns.
+__device__ __forceinline__ void store_out(const FusedArgs &A, float *out, int64_t plane, int m, int gy, int gx, float v)
+{
+    if (A.qmax <= 0.f) {
+        out[m * plane + (int64_t)gy * A.W + gx] = v;
+        return;
+    }
+    const float q = fminf(fmaxf(rintf(v * A.qmax) / A.qmax, 0.f), 1.f);
+    if (!A.yuv420 || m == 0) {
+        out[m * plane + (int64_t)gy * A.W + gx] = q;
+    } else if (!(gy & 1) && !(gx & 1) && (gy >> 1) < (A.H >> 1) && (gx >> 1) < (A.W >> 1)) {
+        const int64_t cp = (int64_t)(A.H >> 1) * (A.W >> 1);
+        out[plane + (m - 1) * cp + (int64_t)(gy >> 1) * (A.W >> 1) + (gx >> 1)] = q;
+    }
+}
+
+using FT = UpsTile<8, 7, kRH, kRW>;
+constexpr int kHsRows = kRH / 2 + 1 + FT::NS - 1; // half-res rows under <= kRH clamped rows
+constexpr int kHrRows = kRH + 7 - 1;              // refine rows incl. the 7-tap halo
+
+template <int CIN, int CMID, bool UPS>
+__global__ __launch_bounds__(kFThreads) void syn_fused_kernel(FusedArgs A, LevelArgs U)
 {
     constexpr int NR = kRowsPerThread;
-    constexpr int NW = CMID * CMID * 9 + CMID; // weights + biases of one 3x3 layer
-    __shared__ float s_buf[2][CMID][kPlane];
-    // 3x3 weights staged in LDS: read back as broadcast ds_read_b128 into VGPRs (the
-    // 81+ weights of a layer do not fit the SGPR budget next to the head's state)
-    __shared__ __attribute__((aligned(16))) float s_w[kMaxSp][(NW + 3) & ~3];
+    constexpr int kStage = UPS ? (CIN - 1) * kHsRows * kRW + kHrRows * kRW : 0;
+    constexpr int kBuf1 = CMID * kPlane > kStage ? CMID * kPlane : kStage;
+    __shared__ __attribute__((aligned(16))) float s_pool[CMID * kPlane + kBuf1];
+    float(*s_buf0)[kPlane] = reinterpret_cast<float(*)[kPlane]>(s_pool);
+    float(*s_buf1)[kPlane] = reinterpret_cast<float(*)[kPlane]>(s_pool + CMID * kPlane);
+    float *s_hs = s_pool + CMID * kPlane;          // [CIN-1][kHsRows][kRW]   (UPS only)
+    float *s_hr = s_hs + (CIN - 1) * kHsRows * kRW; // [kHrRows][kRW]          (UPS only)
+    auto buf = [&](int which) { return which ? s_buf1 : s_buf0; };
+    // head hidden unit j as 16 floats: w0[j][0..CIN), b0[j], w1[0..CMID)[j]; read back as
+    // four broadcast ds_read_b128 (all lanes, one address) -- the loads are issued well
+    // ahead of use, unlike the SGPR path whose scalar loads the compiler waits on at once
+    __shared__ __attribute__((aligned(16))) float s_head[kMaxHid][16];
+    static_assert(CIN + 1 + CMID <= 16, "hidden-unit record");
 
     const int b = blockIdx.y;
     const int halo = A.n_sp;
@@ -100,22 +108,118 @@ __global__ __launch_bounds__(kFThreads) void syn_fused_kernel(FusedArgs A)
     const int gx = ox + c;
     const int cxg = clampi(gx, A.W - 1);
 
-    for (int i = threadIdx.x; i < A.n_sp * NW; i += kFThreads) {
-        const int l = i / NW, j = i - l * NW;
-        s_w[l][j] = prm[A.sp[l].w_off + j]; // biases follow the weights in the block
+    if (A.n_head == 2)
+        for (int i = threadIdx.x; i < A.hid * 16; i += kFThreads) {
+            const int j = i >> 4, f = i & 15;
+            float v = 0.f;
+            if (f < CIN) v = prm[A.w0_off + j * CIN + f];
+            else if (f == CIN) v = prm[A.b0_off + j];
+            else if (f <= CIN + CMID) v = prm[A.w1_off + (f - CIN - 1) * A.hid + j];
+            s_head[j][f] = v;
+        }
+
+    // window's clamped image rectangle [Ya, Yb] x [Xa, Xb] (fused upsampling only)
+    const int Ya = clampi(oy, A.H - 1), Yb = clampi(oy + kRH - 1, A.H - 1);
+    const int Xa = clampi(ox, A.W - 1), Xb = clampi(ox + kRW - 1, A.W - 1);
+    float wu[8], wr[7];
+    if constexpr (UPS) {
+        constexpr int C = CIN - 1;
+        const float *uprm = U.params + (int64_t)b * U.pstride;
+#pragma unroll
+        for (int k = 0; k < 8; ++k) wu[k] = uprm[U.up_off + k];
+#pragma unroll
+        for (int k = 0; k < 7; ++k) wr[k] = uprm[U.pre_off + k];
+        const int nX = Xb - Xa + 1;
+        // horizontal pass of the transposed conv: Hs[c][jj][xi], half-res row Ya/2 + D0 + jj
+        {
+            const float *src = U.src + (int64_t)b * U.src_stride;
+            const int64_t splane = (int64_t)U.hs * U.ws;
+            const int jbase = Ya / 2 + FT::D0;
+            const int nj = Yb / 2 - Ya / 2 + FT::NS;
+            for (int i = threadIdx.x; i < C * kHsRows * kRW; i += kFThreads) {
+                const int ch = i / (kHsRows * kRW), rem = i - ch * (kHsRows * kRW);
+                const int jj = rem / kRW, xi = rem - jj * kRW;
+                if (jj >= nj || xi >= nX) continue;
+                const int X = Xa + xi, a = X & 1, i0 = (X >> 1) + FT::D0;
+                const float *sr = src + ch * splane + (int64_t)clampi(jbase + jj, U.hs - 1) * U.ws;
+                float acc = 0.f;
+#pragma unroll
+                for (int m = 0; m < FT::NS; ++m) {
+                    const int te = FT::tap(0, FT::D0 + m), to = FT::tap(1, FT::D0 + m);
+                    const int tp = a ? to : te;
+                    if ((a ? to : te) >= 0) {
+                        float v = sr[clampi(i0 + m, U.ws - 1)];
+                        if (U.src_quant) v = rintf(U.gain * v);
+                        acc = fmaf(wu[tp], v, acc);
+                    }
+                }
+                s_hs[i] = acc;
+            }
+        }
+        // horizontal pass of the refine (zero padding): Hr[yr][xi], image row Ya - 3 + yr
+        {
+            const float *rs = U.ref_src + (int64_t)b * U.ref_stride;
+            const int nr = Yb - Ya + 7;
+            for (int i = threadIdx.x; i < kHrRows * kRW; i += kFThreads) {
+                const int yr = i / kRW, xi = i - yr * kRW;
+                if (yr >= nr || xi >= nX) continue;
+                const int Y = Ya - 3 + yr, X = Xa + xi;
+                float acc = 0.f;
+                if (Y >= 0 && Y < U.hd) {
+#pragma unroll
+                    for (int k = 0; k < 7; ++k) {
+                        const int xx = X - 3 + k;
+                        float v = 0.f;
+                        if (xx >= 0 && xx < U.wd) {
+                            v = rs[(int64_t)Y * U.wd + xx];
+                            if (U.ref_quant) v = rintf(U.gain * v);
+                        }
+                        acc = fmaf(wr[k], v, acc);
+                    }
+                }
+                s_hr[i] = acc;
+            }
+        }
+        __syncthreads();
     }
 
     // ------------------------ pass 0: per-pixel 1x1 head ------------------------
     {
         const cfloat_ptr w0 = prm + A.w0_off, b0 = prm + A.b0_off;
-        const cfloat_ptr w1 = prm + A.w1_off, b1 = prm + A.b1_off;
+        const cfloat_ptr b1 = prm + A.b1_off;
         float x[NR][CIN];
         float o[NR][CMID];
 #pragma unroll
         for (int p = 0; p < NR; ++p) {
-            const int64_t pix = (int64_t)clampi(oy + rb + p, A.H - 1) * A.W + cxg;
+            const int Y = clampi(oy + rb + p, A.H - 1);
+            if constexpr (UPS) {
+                // vertical passes, in ups_level_fixed's operation order
+                const int xi = cxg - Xa, yi = Y - Ya;
+                {
+                    float acc = 0.f;
 #pragma unroll
-            for (int k = 0; k < CIN; ++k) x[p][k] = in[k * plane + pix];
+                    for (int k = 0; k < 7; ++k) acc = fmaf(wr[k], s_hr[(yi + k) * kRW + xi], acc);
+                    float q0 = U.ref_src[(int64_t)b * U.ref_stride + (int64_t)Y * U.wd + cxg];
+                    if (U.ref_quant) q0 = rintf(U.gain * q0);
+                    x[p][0] = acc + q0;
+                }
+                const int jj0 = Y / 2 - Ya / 2, a = Y & 1;
+#pragma unroll
+                for (int k = 1; k < CIN; ++k) {
+                    const float *h = s_hs + ((k - 1) * kHsRows + jj0) * kRW + xi;
+                    float acc = 0.f;
+#pragma unroll
+                    for (int m = 0; m < FT::NS; ++m) {
+                        const int te = FT::tap(0, FT::D0 + m), to = FT::tap(1, FT::D0 + m);
+                        if ((a ? to : te) >= 0) acc = fmaf(wu[a ? to : te], h[m * kRW], acc);
+                    }
+                    x[p][k] = acc;
+                }
+            } else {
+                const int64_t pix = (int64_t)Y * A.W + cxg;
+#pragma unroll
+                for (int k = 0; k < CIN; ++k) x[p][k] = in[k * plane + pix];
+            }
         }
         if (A.n_head == 2) {
             const int hid = A.hid;
@@ -129,22 +233,32 @@ __global__ __launch_bounds__(kFThreads) void syn_fused_kernel(FusedArgs A)
 #pragma unroll
                 for (int m = 0; m < CMID; ++m) op[q][m] = f2(0.f);
             }
-#pragma unroll 2
-            for (int j = 0; j < hid; ++j) {
-                const cfloat_ptr wj = w0 + j * CIN;
-                const f2 bj = f2(b0[j]);
-                f2 wm[CMID];
-#pragma unroll
-                for (int m = 0; m < CMID; ++m) wm[m] = f2(w1[m * hid + j]);
+            __syncthreads(); // s_head staged
+            // software pipelined: the record of unit j+2 is loaded while unit j+1 computes
+            struct Rec { float4 v[4]; };
+            auto load = [&](int j) {
+                const float4 *p = reinterpret_cast<const float4 *>(s_head[j < hid ? j : hid - 1]);
+                return Rec{{p[0], p[1], p[2], p[3]}};
+            };
+            auto unit = [&](const Rec &r) {
+                const float *u = reinterpret_cast<const float *>(r.v);
+                const f2 bj = f2(u[CIN]);
 #pragma unroll
                 for (int q = 0; q < NR / 2; ++q) {
                     f2 acc = bj;
 #pragma unroll
-                    for (int k = 0; k < CIN; ++k) acc = __builtin_elementwise_fma(f2(wj[k]), xp[q][k], acc);
+                    for (int k = 0; k < CIN; ++k) acc = __builtin_elementwise_fma(f2(u[k]), xp[q][k], acc);
                     acc = __builtin_elementwise_max(acc, lo0);
 #pragma unroll
-                    for (int m = 0; m < CMID; ++m) op[q][m] = __builtin_elementwise_fma(wm[m], acc, op[q][m]);
+                    for (int m = 0; m < CMID; ++m) op[q][m] = __builtin_elementwise_fma(f2(u[CIN + 1 + m]), acc, op[q][m]);
                 }
+            };
+            Rec ra = load(0), rb2 = load(1);
+            for (int j = 0; j < hid; j += 2) {
+                unit(ra);
+                ra = load(j + 2);
+                if (j + 1 < hid) unit(rb2);
+                rb2 = load(j + 3);
             }
             const float lo1 = A.relu1 ? 0.f : -INFINITY;
 #pragma unroll
@@ -174,14 +288,14 @@ __global__ __launch_bounds__(kFThreads) void syn_fused_kernel(FusedArgs A)
                 const int gy = oy + rb + p;
                 if (gy < A.H && gx < A.W)
 #pragma unroll
-                    for (int m = 0; m < CMID; ++m) out[m * plane + (int64_t)gy * A.W + gx] = o[p][m];
+                    for (int m = 0; m < CMID; ++m) store_out(A, out, plane, m, gy, gx, o[p][m]);
             }
             return;
         }
 #pragma unroll
         for (int p = 0; p < NR; ++p)
 #pragma unroll
-            for (int m = 0; m < CMID; ++m) s_buf[0][m][(rb + p + 1) * kRW + c] = o[p][m];
+            for (int m = 0; m < CMID; ++m) s_buf0[m][(rb + p + 1) * kRW + c] = o[p][m];
     }
 
     // ------------------------ 3x3 layers, replicate padding ------------------------
@@ -201,12 +315,12 @@ __global__ __launch_bounds__(kFThreads) void syn_fused_kernel(FusedArgs A)
         __syncthreads();
         const int t = s + 1;
         const bool last = s == A.n_sp - 1;
-        const float *wt = s_w[s];
-        const float *bs = s_w[s] + CMID * CMID * 9;
+        const cfloat_ptr wt = prm + A.sp[s].w_off;
+        const cfloat_ptr bs = prm + A.sp[s].b_off;
         const float lo = A.sp[s].relu ? 0.f : -INFINITY;
         const float rsd = A.sp[s].residual ? 1.f : 0.f;
         // plane row of window row (rb - 1) in this thread's column
-        const float *src = &s_buf[cur][0][0] + rb * kRW + c;
+        const float *src = &buf(cur)[0][0] + rb * kRW + c;
 #pragma unroll
         for (int q = 0; q < NR / 2; ++q) {
             // output rows rb + 2q, rb + 2q + 1 read window rows rb + 2q - 1 .. rb + 2q + 2
@@ -220,38 +334,36 @@ __global__ __launch_bounds__(kFThreads) void syn_fused_kernel(FusedArgs A)
                         const float *e = src + k * kPlane + (2 * q + dy) * kRW + (lx[d] - c);
                         P[dy][k][d] = f2{e[0], e[kRW]};
                     }
-            f2 acc[CMID];
-#pragma unroll
+            // one output channel per iteration (not unrolled): its CMID*9 weights + bias are
+            // wave-uniform scalar loads, so the 3x3 stage spends no LDS bandwidth on weights
+#pragma unroll 1
             for (int m = 0; m < CMID; ++m) {
-                // one output channel's weights in flight at a time (bounds VGPR use)
-                __builtin_amdgcn_sched_barrier(0);
-                acc[m] = f2(bs[m]);
+                const cfloat_ptr wm = wt + m * CMID * 9;
+                f2 acc = f2(bs[m]);
 #pragma unroll
                 for (int k = 0; k < CMID; ++k)
 #pragma unroll
                     for (int dy = 0; dy < 3; ++dy)
 #pragma unroll
                         for (int dx = 0; dx < 3; ++dx)
-                            acc[m] = __builtin_elementwise_fma(f2(wt[((m * CMID + k) * 3 + dy) * 3 + dx]),
-                                                               P[dy][k][dx], acc[m]);
-                // residual: the input at the centre
-                acc[m] = __builtin_elementwise_max(__builtin_elementwise_fma(f2(rsd), P[1][m][1], acc[m]), f2(lo));
-            }
+                            acc = __builtin_elementwise_fma(f2(wm[(k * 3 + dy) * 3 + dx]), P[dy][k][dx], acc);
+                // residual: the input at the centre (select chain: no indexed registers)
+                f2 ctr = P[1][0][1];
 #pragma unroll
-            for (int h = 0; h < 2; ++h) {
-                const int r = rb + 2 * q + h, gy = oy + r;
-                if (last) {
-                    if (r >= t && r < kRH - t && c >= t && c < kRW - t && gy < A.H && col_in)
+                for (int k = 1; k < CMID; ++k) ctr = m == k ? P[1][k][1] : ctr;
+                acc = __builtin_elementwise_max(__builtin_elementwise_fma(f2(rsd), ctr, acc), f2(lo));
 #pragma unroll
-                        for (int m = 0; m < CMID; ++m) out[m * plane + (int64_t)gy * A.W + gx] = h ? acc[m].y : acc[m].x;
-                } else if (gy >= 0 && gy < A.H) {
-                    float *dst = &s_buf[cur ^ 1][0][0] + (r + 1) * kRW + c;
-#pragma unroll
-                    for (int m = 0; m < CMID; ++m) {
-                        const float v = h ? acc[m].y : acc[m].x;
-                        dst[m * kPlane] = v;
-                        if (gy == 0) dst[m * kPlane - kRW] = v;     // replicate above the image
-                        if (gy == A.H - 1) dst[m * kPlane + kRW] = v; // and below it
+                for (int h = 0; h < 2; ++h) {
+                    const int r = rb + 2 * q + h, gy = oy + r;
+                    const float v = h ? acc.y : acc.x;
+                    if (last) {
+                        if (r >= t && r < kRH - t && c >= t && c < kRW - t && gy < A.H && col_in)
+                            store_out(A, out, plane, m, gy, gx, v);
+                    } else if (gy >= 0 && gy < A.H) {
+                        float *dst = &buf(cur ^ 1)[m][0] + (r + 1) * kRW + c;
+                        dst[0] = v;
+                        if (gy == 0) dst[-kRW] = v;     // replicate above the image
+                        if (gy == A.H - 1) dst[kRW] = v; // and below it
                     }
                 }
             }
@@ -318,13 +430,23 @@ __global__ __launch_bounds__(kThreads) void post_kernel(const float *__restrict_
     }
 }
 
-struct Plan {
-    bool fused;
-    int hid, cmid;
-    FusedArgs fa;
-};
+template <int CMID, bool UPS>
+void launch_fused(dim3 grid, hipStream_t s, const FusedArgs &fa, const LevelArgs &u)
+{
+    switch (fa.cin) {
+    case 1: hipLaunchKernelGGL((syn_fused_kernel<1, CMID, false>), grid, dim3(kFThreads), 0, s, fa, u); break;
+#define CCMI_FUSED_CASE(N) \
+    case N: hipLaunchKernelGGL((syn_fused_kernel<N, CMID, UPS>), grid, dim3(kFThreads), 0, s, fa, u); break;
+    CCMI_FUSED_CASE(2) CCMI_FUSED_CASE(3) CCMI_FUSED_CASE(4) CCMI_FUSED_CASE(5) CCMI_FUSED_CASE(6)
+    CCMI_FUSED_CASE(7) CCMI_FUSED_CASE(8)
+#undef CCMI_FUSED_CASE
+    }
+}
 
-// Offsets of each layer's weights / biases in a frame's parameter block.
+} // namespace
+
+namespace ccmi_fwd {
+
 void layer_offsets(const ccmi_syn_args *a, int *w_off, int *b_off, int *cin_of, int64_t *total)
 {
     int64_t o = 0;
@@ -354,6 +476,7 @@ bool make_plan(const ccmi_syn_args *a, Plan *P)
     const int cmid = L[n_head - 1].n_out;
     if (cmid < 1 || cmid > kMaxMid) return false;
     int hid = n_head == 2 ? L[0].n_out : 0;
+    if (hid > kMaxHid) return false;
     const int n_sp = a->n_layers - n_head;
     if (n_sp > kMaxSp) return false;
     for (int l = n_head; l < a->n_layers; ++l)
@@ -387,22 +510,7 @@ bool make_plan(const ccmi_syn_args *a, Plan *P)
     return true;
 }
 
-template <int CMID>
-void launch_fused(dim3 grid, hipStream_t s, const FusedArgs &fa)
-{
-    switch (fa.cin) {
-    case 1: hipLaunchKernelGGL((syn_fused_kernel<1, CMID>), grid, dim3(kFThreads), 0, s, fa); break;
-    case 2: hipLaunchKernelGGL((syn_fused_kernel<2, CMID>), grid, dim3(kFThreads), 0, s, fa); break;
-    case 3: hipLaunchKernelGGL((syn_fused_kernel<3, CMID>), grid, dim3(kFThreads), 0, s, fa); break;
-    case 4: hipLaunchKernelGGL((syn_fused_kernel<4, CMID>), grid, dim3(kFThreads), 0, s, fa); break;
-    case 5: hipLaunchKernelGGL((syn_fused_kernel<5, CMID>), grid, dim3(kFThreads), 0, s, fa); break;
-    case 6: hipLaunchKernelGGL((syn_fused_kernel<6, CMID>), grid, dim3(kFThreads), 0, s, fa); break;
-    case 7: hipLaunchKernelGGL((syn_fused_kernel<7, CMID>), grid, dim3(kFThreads), 0, s, fa); break;
-    case 8: hipLaunchKernelGGL((syn_fused_kernel<8, CMID>), grid, dim3(kFThreads), 0, s, fa); break;
-    }
-}
-
-} // namespace
+} // namespace ccmi_fwd
 
 extern "C" size_t ccmi_syn_workspace_bytes(const ccmi_syn_args *a)
 {
@@ -437,8 +545,8 @@ int ccmi_launch_syn_f32(const ccmi_syn_args *a, hipStream_t s)
         const int halo = P.fa.n_sp;
         P.fa.tiles_x = ccmi_div_up(a->w, kRW - 2 * halo);
         dim3 grid(P.fa.tiles_x * ccmi_div_up(a->h, kRH - 2 * halo), a->batch);
-        if (P.cmid == 3) launch_fused<3>(grid, s, P.fa);
-        else launch_fused<4>(grid, s, P.fa);
+        if (P.cmid == 3) launch_fused<3, false>(grid, s, P.fa, LevelArgs{});
+        else launch_fused<4, false>(grid, s, P.fa, LevelArgs{});
         CCMI_HIP_CHECK(hipGetLastError());
         return CCMI_OK;
     }
@@ -479,6 +587,44 @@ int ccmi_launch_post_f32(const ccmi_post_args *a, hipStream_t s)
     dim3 grid((unsigned)((plane + kThreads - 1) / kThreads), a->batch);
     hipLaunchKernelGGL(post_kernel, grid, dim3(kThreads), 0, s, a->in, a->in_stride, a->h, a->w,
                        (float)((1 << a->bitdepth) - 1), a->yuv420, a->out, a->out_stride);
+    CCMI_HIP_CHECK(hipGetLastError());
+    return CCMI_OK;
+}
+
+extern "C" int ccmi_decode_forward_f32(const ccmi_decode_args *a, void *stream)
+{
+    if (!a || !a->out || !a->ups.latent || !a->ups.params || !a->syn.params)
+        return ccmi_set_error(CCMI_ERR_ARG, "decode: null argument");
+    const ccmi_ups_args &u = a->ups;
+    const ccmi_syn_args &y = a->syn;
+    if (u.batch < 1 || y.batch != u.batch) return ccmi_set_error(CCMI_ERR_ARG, "decode: batch mismatch");
+    if (u.n_grids < 2 || u.n_grids > CCMI_MAX_GRIDS) return ccmi_set_error(CCMI_ERR_ARG, "decode: n_grids");
+    if (y.c_in != u.n_grids || y.h != u.h[0] || y.w != u.w[0])
+        return ccmi_set_error(CCMI_ERR_ARG, "decode: synthesis input must be the %d x %d x %d upsampled stack", u.n_grids,
+                              u.h[0], u.w[0]);
+    if (a->bitdepth < 0 || a->bitdepth > 16) return ccmi_set_error(CCMI_ERR_ARG, "decode: bitdepth %d", a->bitdepth);
+    if (y.n_layers < 1 || y.n_layers > CCMI_MAX_SYN_LAYERS) return ccmi_set_error(CCMI_ERR_ARG, "decode: n_layers");
+    Plan P;
+    if (u.ups_k != 8 || u.pre_k != 7 || !make_plan(&y, &P))
+        return ccmi_set_error(CCMI_ERR_UNSUPPORTED, "decode: no fused kernel for this architecture");
+    if (a->bitdepth > 0 && P.cmid != 3) return ccmi_set_error(CCMI_ERR_ARG, "decode: post-processing needs 3 output planes");
+    hipStream_t s = static_cast<hipStream_t>(stream);
+    const int stages = a->stages ? a->stages : 3;
+    LevelArgs last{};
+    if (int rc = ups_pyramid(&u, s, &last, (stages & 1) != 0)) return rc;
+    if (!(stages & 2)) return CCMI_OK;
+    P.fa.in = nullptr;
+    P.fa.params = y.params;
+    P.fa.pstride = y.param_stride;
+    P.fa.out = a->out;
+    P.fa.out_stride = a->out_stride;
+    P.fa.qmax = a->bitdepth > 0 ? (float)((1 << a->bitdepth) - 1) : 0.f;
+    P.fa.yuv420 = a->yuv420;
+    const int halo = P.fa.n_sp;
+    P.fa.tiles_x = ccmi_div_up(y.w, kRW - 2 * halo);
+    dim3 grid(P.fa.tiles_x * ccmi_div_up(y.h, kRH - 2 * halo), y.batch);
+    if (P.cmid == 3) launch_fused<3, true>(grid, s, P.fa, last);
+    else launch_fused<4, true>(grid, s, P.fa, last);
     CCMI_HIP_CHECK(hipGetLastError());
     return CCMI_OK;
 }

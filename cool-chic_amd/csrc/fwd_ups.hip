@@ -16,7 +16,9 @@
 // Each workgroup computes a 16 x 64 destination tile for every channel: the source
 // tile (with clamped halo) and the horizontal pass are staged in LDS, then the
 // vertical pass writes coalesced rows.
-#include "ccmi_internal.h"
+#include "fwd_common.h"
+
+using namespace ccmi_fwd;
 
 namespace {
 
@@ -27,30 +29,6 @@ constexpr int kSrcW = kTX / 2 + kMaxK / 2 + 2;  // source tile row pitch (incl. 
 constexpr int kRefH = kTY + kMaxK;              // refine rows incl. halo
 constexpr int kRefW = kTX + kMaxK;
 
-struct LevelArgs {
-    // source stack (level k): C channels of hs x ws; channel c at src + c * hs * ws
-    const float *src;
-    int64_t src_stride;
-    int src_quant; // source is the raw coarsest latent grid -> round(gain * x)
-    int C, hs, ws;
-    // refine input: raw latent grid of level k-1 (flat latent vector + offset)
-    const float *ref_src;
-    int64_t ref_stride;
-    int ref_quant;
-    // destination stack (level k-1): C + 1 channels of hd x wd
-    float *dst;
-    int64_t dst_stride;
-    int hd, wd;
-    float gain;
-    // kernels, per frame: up taps at params + up_off, refine taps at params + pre_off
-    const float *params;
-    int64_t pstride;
-    int up_off, K;
-    int pre_off, Kp;
-    int tiles_x;
-};
-
-__device__ __forceinline__ int clampi(int v, int hi) { return v < 0 ? 0 : (v > hi ? hi : v); }
 
 __global__ __launch_bounds__(kThreads) void ups_level_kernel(LevelArgs A)
 {
@@ -158,53 +136,37 @@ __global__ __launch_bounds__(kThreads) void ups_level_kernel(LevelArgs A)
 // ---------------------------------------------------------------------------------------------
 // Specialised level kernel for compile-time kernel sizes (the reference's defaults are
 // K = 8 transposed taps, KP = 7 refine taps).  Differences from the generic kernel:
-//   * one staging pass loads the refine input and the source tiles of ALL channels, so a
-//     tile costs 2 barriers instead of 3 * (C + 1);
+//   * one channel per workgroup (grid z), small LDS footprint -> high occupancy;
 //   * the polyphase loops are unrolled: a thread produces an (even, odd) output pair from
 //     K/2 + 1 shared source samples, horizontally and then vertically;
 //   * no per-element division: all pitches are compile-time.
 // ---------------------------------------------------------------------------------------------
-constexpr int kMaxC = CCMI_MAX_GRIDS - 1; // channels of the source stack
-
-template <int K, int KP>
-struct UpsTile {
-    static constexpr int K2 = K / 2;
-    static constexpr int D0 = -((K2 + 1) / 2);      // min source offset over both parities
-    static constexpr int NS = K2 + 1;               // source samples shared by an (even, odd) pair
-    static constexpr int SH = kTY / 2 + NS - 1;     // source tile rows
-    static constexpr int SW = kTX / 2 + NS - 1;     // source tile cols
-    static constexpr int PAD = KP / 2;
-    static constexpr int RH = kTY + KP - 1, RW = kTX + KP - 1;
-    // tap used by parity a at source offset d (or -1)
-    static constexpr int tap(int a, int d) { return (a + K2 - 1 - 2 * d >= 0 && a + K2 - 1 - 2 * d < K) ? a + K2 - 1 - 2 * d : -1; }
-};
 
 template <int K, int KP>
 __global__ __launch_bounds__(kThreads) void ups_level_fixed(LevelArgs A)
 {
-    using T = UpsTile<K, KP>;
-    static_assert(T::NS == K / 2 + 1, "");
-    __shared__ float s_ref[T::RH * T::RW];
-    __shared__ float s_refh[T::RH * kTX];
-    __shared__ float s_src[kMaxC * T::SH * T::SW];
-    __shared__ float s_h[kMaxC * T::SH * kTX];
+    using T = UpsTile<K, KP, kTY, kTX>;
+    // blockIdx.z = job: 0 -> refine channel, c >= 1 -> transposed-conv channel c.  One
+    // channel per workgroup keeps LDS small (the union of the two jobs' buffers), so many
+    // workgroups are resident per CU to hide the L2/HBM latency of the tile loads.
+    constexpr int kRef = T::RH * T::RW + T::RH * kTX;
+    constexpr int kUp = T::SH * T::SW + T::SH * kTX;
+    __shared__ float s_mem[kRef > kUp ? kRef : kUp];
 
     const int b = blockIdx.y;
+    const int job = blockIdx.z;
     const int y0 = (blockIdx.x / A.tiles_x) * kTY;
     const int x0 = (blockIdx.x % A.tiles_x) * kTX;
     const float *prm = A.params + (int64_t)b * A.pstride;
-    float wu[K], wr[KP];
-#pragma unroll
-    for (int k = 0; k < K; ++k) wu[k] = prm[A.up_off + k];
-#pragma unroll
-    for (int k = 0; k < KP; ++k) wr[k] = prm[A.pre_off + k];
     float *dst = A.dst + (int64_t)b * A.dst_stride;
     const int64_t dplane = (int64_t)A.hd * A.wd;
     const int tid = threadIdx.x;
-    const int C = A.C;
 
-    // ---- stage: refine input (zero padded) and every source channel (replicate clamped) ----
-    {
+    if (job == 0) {
+        float wr[KP];
+#pragma unroll
+        for (int k = 0; k < KP; ++k) wr[k] = prm[A.pre_off + k];
+        float *s_ref = s_mem, *s_refh = s_mem + T::RH * T::RW;
         const float *rs = A.ref_src + (int64_t)b * A.ref_stride;
         for (int i = tid; i < T::RH * T::RW; i += kThreads) {
             const int r = i / T::RW, c = i - r * T::RW;
@@ -216,82 +178,80 @@ __global__ __launch_bounds__(kThreads) void ups_level_fixed(LevelArgs A)
             }
             s_ref[i] = v;
         }
-        const float *src = A.src + (int64_t)b * A.src_stride;
-        const int64_t splane = (int64_t)A.hs * A.ws;
+        __syncthreads();
+        for (int i = tid; i < T::RH * kTX; i += kThreads) {
+            const int r = i / kTX, c = i - r * kTX;
+            const float *p = s_ref + r * T::RW + c;
+            float acc = 0.f;
+#pragma unroll
+            for (int k = 0; k < KP; ++k) acc = fmaf(wr[k], p[k], acc);
+            s_refh[i] = acc;
+        }
+        __syncthreads();
+        for (int i = tid; i < kTY * kTX; i += kThreads) {
+            const int r = i / kTX, c = i - r * kTX;
+            const int y = y0 + r, x = x0 + c;
+            if (y < A.hd && x < A.wd) {
+                float acc = 0.f;
+#pragma unroll
+                for (int k = 0; k < KP; ++k) acc = fmaf(wr[k], s_refh[(r + k) * kTX + c], acc);
+                dst[(int64_t)y * A.wd + x] = acc + s_ref[(r + T::PAD) * T::RW + c + T::PAD];
+            }
+        }
+        return;
+    }
+
+    const int c = job - 1;
+    float wu[K];
+#pragma unroll
+    for (int k = 0; k < K; ++k) wu[k] = prm[A.up_off + k];
+    float *s_src = s_mem, *s_h = s_mem + T::SH * T::SW;
+    {
+        const float *src = A.src + (int64_t)b * A.src_stride + (int64_t)c * A.hs * A.ws;
         const int sy0 = y0 / 2 + T::D0, sx0 = x0 / 2 + T::D0;
-        const int n = C * T::SH * T::SW;
-        for (int i = tid; i < n; i += kThreads) {
-            const int c = i / (T::SH * T::SW), rem = i - c * (T::SH * T::SW);
-            const int r = rem / T::SW, cc = rem - r * T::SW;
+        for (int i = tid; i < T::SH * T::SW; i += kThreads) {
+            const int r = i / T::SW, cc = i - r * T::SW;
             const int y = clampi(sy0 + r, A.hs - 1), x = clampi(sx0 + cc, A.ws - 1);
-            float v = src[c * splane + y * A.ws + x];
+            float v = src[y * A.ws + x];
             if (A.src_quant) v = rintf(A.gain * v);
             s_src[i] = v;
         }
     }
     __syncthreads();
-
-    // ---- horizontal passes ----
-    for (int i = tid; i < T::RH * kTX; i += kThreads) {
-        const int r = i / kTX, c = i - r * kTX;
-        const float *p = s_ref + r * T::RW + c;
-        float acc = 0.f;
+    // horizontal: one (even, odd) destination column pair per item, source column x0/2 + q
+    for (int i = tid; i < T::SH * (kTX / 2); i += kThreads) {
+        const int r = i / (kTX / 2), q = i - r * (kTX / 2);
+        const float *p = s_src + r * T::SW + q; // offset D0 at index 0
+        float e = 0.f, o = 0.f;
 #pragma unroll
-        for (int k = 0; k < KP; ++k) acc = fmaf(wr[k], p[k], acc);
-        s_refh[i] = acc;
-    }
-    {
-        // one (even, odd) destination column pair per item: source column j = x0/2 + q
-        const int n = C * T::SH * (kTX / 2);
-        for (int i = tid; i < n; i += kThreads) {
-            const int row = i / (kTX / 2), q = i - row * (kTX / 2); // row = c * SH + r
-            const float *p = s_src + row * T::SW + q;              // offset D0 at index 0
-            float e = 0.f, o = 0.f;
-#pragma unroll
-            for (int m = 0; m < T::NS; ++m) {
-                const float v = p[m];
-                const int d = T::D0 + m;
-                const int te = T::tap(0, d), to = T::tap(1, d);
-                if (te >= 0) e = fmaf(wu[te], v, e);
-                if (to >= 0) o = fmaf(wu[to], v, o);
-            }
-            *reinterpret_cast<float2 *>(s_h + row * kTX + 2 * q) = make_float2(e, o);
+        for (int m = 0; m < T::NS; ++m) {
+            const float v = p[m];
+            const int d = T::D0 + m;
+            const int te = T::tap(0, d), to = T::tap(1, d);
+            if (te >= 0) e = fmaf(wu[te], v, e);
+            if (to >= 0) o = fmaf(wu[to], v, o);
         }
+        *reinterpret_cast<float2 *>(s_h + r * kTX + 2 * q) = make_float2(e, o);
     }
     __syncthreads();
-
-    // ---- vertical passes + coalesced stores ----
-    for (int i = tid; i < kTY * kTX; i += kThreads) {
-        const int r = i / kTX, c = i - r * kTX;
-        const int y = y0 + r, x = x0 + c;
-        if (y < A.hd && x < A.wd) {
-            float acc = 0.f;
+    // vertical: destination rows y0 + 2q, y0 + 2q + 1 of column x
+    for (int i = tid; i < (kTY / 2) * kTX; i += kThreads) {
+        const int q = i / kTX, x = i - q * kTX;
+        const float *p = s_h + q * kTX + x;
+        float e = 0.f, o = 0.f;
 #pragma unroll
-            for (int k = 0; k < KP; ++k) acc = fmaf(wr[k], s_refh[(r + k) * kTX + c], acc);
-            dst[(int64_t)y * A.wd + x] = acc + s_ref[(r + T::PAD) * T::RW + c + T::PAD];
+        for (int m = 0; m < T::NS; ++m) {
+            const float v = p[m * kTX];
+            const int d = T::D0 + m;
+            const int te = T::tap(0, d), to = T::tap(1, d);
+            if (te >= 0) e = fmaf(wu[te], v, e);
+            if (to >= 0) o = fmaf(wu[to], v, o);
         }
-    }
-    {
-        const int n = C * (kTY / 2) * kTX;
-        for (int i = tid; i < n; i += kThreads) {
-            const int c = i / ((kTY / 2) * kTX), rem = i - c * ((kTY / 2) * kTX);
-            const int q = rem / kTX, x = rem - q * kTX; // destination rows y0 + 2q, y0 + 2q + 1
-            const float *p = s_h + (c * T::SH + q) * kTX + x;
-            float e = 0.f, o = 0.f;
-#pragma unroll
-            for (int m = 0; m < T::NS; ++m) {
-                const float v = p[m * kTX];
-                const int d = T::D0 + m;
-                const int te = T::tap(0, d), to = T::tap(1, d);
-                if (te >= 0) e = fmaf(wu[te], v, e);
-                if (to >= 0) o = fmaf(wu[to], v, o);
-            }
-            const int yd = y0 + 2 * q, xd = x0 + x;
-            if (xd < A.wd) {
-                float *out = dst + (int64_t)(c + 1) * dplane + (int64_t)yd * A.wd + xd;
-                if (yd < A.hd) out[0] = e;
-                if (yd + 1 < A.hd) out[A.wd] = o;
-            }
+        const int yd = y0 + 2 * q, xd = x0 + x;
+        if (xd < A.wd) {
+            float *out = dst + (int64_t)(c + 1) * dplane + (int64_t)yd * A.wd + xd;
+            if (yd < A.hd) out[0] = e;
+            if (yd + 1 < A.hd) out[A.wd] = o;
         }
     }
 }
@@ -305,7 +265,20 @@ extern "C" size_t ccmi_ups_workspace_bytes(int n_grids, const int *h, const int 
     return per * sizeof(float) * (size_t)(batch > 0 ? batch : 0);
 }
 
-int ccmi_launch_ups_f32(const ccmi_ups_args *a, hipStream_t s)
+namespace {
+int launch_level(const LevelArgs &A, int batch, hipStream_t s)
+{
+    dim3 grid(A.tiles_x * ccmi_div_up(A.hd, kTY), batch);
+    if (A.K == 8 && A.Kp == 7)
+        hipLaunchKernelGGL((ups_level_fixed<8, 7>), dim3(grid.x, grid.y, A.C + 1), dim3(kThreads), 0, s, A);
+    else
+        hipLaunchKernelGGL(ups_level_kernel, grid, dim3(kThreads), 0, s, A);
+    CCMI_HIP_CHECK(hipGetLastError());
+    return CCMI_OK;
+}
+} // namespace
+
+int ccmi_fwd::ups_pyramid(const ccmi_ups_args *a, hipStream_t s, LevelArgs *last, bool launch)
 {
     const int L = a->n_grids;
     if (L < 2) return ccmi_set_error(CCMI_ERR_UNSUPPORTED, "ups: needs at least 2 latent grids (got %d)", L);
@@ -325,7 +298,6 @@ int ccmi_launch_ups_f32(const ccmi_ups_args *a, hipStream_t s)
     int total = 0;
     for (int l = 0; l < L; ++l) { off[l] = total; total += a->h[l] * a->w[l]; }
     if (a->latent_stride < total) return ccmi_set_error(CCMI_ERR_ARG, "ups: latent_stride < %d", total);
-    if (a->out_stride < (int64_t)L * a->h[0] * a->w[0]) return ccmi_set_error(CCMI_ERR_ARG, "ups: out_stride too small");
 
     // workspace layout: stack of level k (1..L-2) for all frames: [batch][L-k][h_k][w_k]
     float *ws_base = static_cast<float *>(a->workspace);
@@ -356,7 +328,7 @@ int ccmi_launch_ups_f32(const ccmi_ups_args *a, hipStream_t s)
         A.ref_stride = a->latent_stride;
         A.ref_quant = a->quantize;
         if (k - 1 == 0) {
-            A.dst = a->out;
+            A.dst = a->out; // may be null when the caller fuses the last step
             A.dst_stride = a->out_stride;
         } else {
             A.dst = stack_ptr[k - 1];
@@ -372,12 +344,21 @@ int ccmi_launch_ups_f32(const ccmi_ups_args *a, hipStream_t s)
         A.Kp = a->pre_k;
         A.pre_off = a->n_ups * a->ups_k + (step % a->n_pre) * a->pre_k;
         A.tiles_x = ccmi_div_up(A.wd, kTX);
-        dim3 grid(A.tiles_x * ccmi_div_up(A.hd, kTY), a->batch);
-        if (A.K == 8 && A.Kp == 7 && A.C <= kMaxC)
-            hipLaunchKernelGGL((ups_level_fixed<8, 7>), grid, dim3(kThreads), 0, s, A);
-        else
-            hipLaunchKernelGGL(ups_level_kernel, grid, dim3(kThreads), 0, s, A);
-        CCMI_HIP_CHECK(hipGetLastError());
+        if (step == L - 2) {
+            *last = A;
+            break;
+        }
+        if (launch)
+            if (int rc = launch_level(A, a->batch, s)) return rc;
     }
     return CCMI_OK;
+}
+
+int ccmi_launch_ups_f32(const ccmi_ups_args *a, hipStream_t s)
+{
+    if (a->out_stride < (int64_t)a->n_grids * a->h[0] * a->w[0])
+        return ccmi_set_error(CCMI_ERR_ARG, "ups: out_stride too small");
+    LevelArgs last{};
+    if (int rc = ups_pyramid(a, s, &last)) return rc;
+    return launch_level(last, a->batch, s);
 }

@@ -156,6 +156,29 @@ typedef struct ccmi_post_args {
 } ccmi_post_args;
 int ccmi_post_f32(const ccmi_post_args *args, void *stream);
 
+/* Fused decode tail: Upsampling.forward -> Synthesis.forward -> post-processing of
+ * FrameEncoder.forward (eval) as ONE pass that never materialises the [n_grids][H][W]
+ * upsampled stack nor the raw synthesis output (the composition of
+ * ccmi_ups_forward_f32, ccmi_syn_forward_f32 and ccmi_post_f32, the decoder's path:
+ * coolchic.py:395-437 then frame.py:175-183).  ups.out and syn.in are ignored;
+ * syn.c_in must equal ups.n_grids and syn.h/w equal ups.h[0]/w[0]; ups.workspace as for
+ * ccmi_ups_forward_f32.  bitdepth > 0: out receives the post-processed frame (layout
+ * of ccmi_post_f32); bitdepth == 0: out receives the raw synthesis output.
+ * CCMI_ERR_UNSUPPORTED when the architecture has no fused kernel (ups_k != 8,
+ * pre_k != 7, or a synthesis outside the fused plan): run the three stages instead. */
+typedef struct ccmi_decode_args {
+    ccmi_ups_args ups;
+    ccmi_syn_args syn;
+    int bitdepth;
+    int yuv420;
+    float *out;
+    int64_t out_stride;
+    int stages;             /* 0 = all; bit 0: upsampling pyramid down to level 1 (into
+                               ups.workspace), bit 1: the fused full-resolution kernel --
+                               lets a caller time the two apart */
+} ccmi_decode_args;
+int ccmi_decode_forward_f32(const ccmi_decode_args *args, void *stream);
+
 /* ------------------------------------------------------------------------- */
 /* Path B: fixed-point .cool decoder, bit-exact with coolchic/cpp.             */
 /* ------------------------------------------------------------------------- */

@@ -18,7 +18,7 @@ from collections import defaultdict
 from pathlib import Path
 
 ROOT = Path(__file__).resolve().parents[1]
-STAGES = {"arm_fwd_kernel": "arm", "ups_level_kernel": "ups", "syn_fused_kernel": "syn", "syn_layer_kernel": "syn",
+STAGES = {"arm_fwd_kernel": "arm", "ups_level_kernel": "ups", "ups_level_fixed": "ups", "syn_fused_kernel": "syn", "syn_layer_kernel": "syn",
           "post_kernel": "post", "dec_arm": "dec_arm", "dec_ups": "dec_ups", "dec_syn": "dec_syn"}
 
 
