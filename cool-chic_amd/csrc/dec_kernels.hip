@@ -370,7 +370,18 @@ __global__ __launch_bounds__(64) void dec_arm_spec_kernel(const ArmStreamDesc *_
     const int h = S.h, w = S.w;
     const bool w24 = (S.flags & 1) != 0;
 
-    for (int i = lane; i < 17 * 50 * 2; i += 64) ctab[i] = c_ctx.v[i];
+    // context table with every static-context index already turned into its model state
+    // (Model::init + state(), done once here instead of per bin)
+    for (int i = lane; i < 17 * 50 * 2; i += 64) {
+        const uint32_t v = c_ctx.v[i];
+        uint32_t o = 0;
+        for (int k = 0; k < 4; ++k) {
+            Model m;
+            m.init((int)((v >> (8 * k)) & 0xFF));
+            o |= m.state() << (8 * k);
+        }
+        ctab[i] = (i & 1) ? (o & 0xFF) : o;
+    }
     for (int i = lane; i < kRing * pitch; i += 64) ring[i] = 0;
 
     int32_t Wh[NH > 0 ? NH : 1][16], Bh[NH > 0 ? NH : 1];
@@ -471,6 +482,10 @@ __global__ __launch_bounds__(64) void dec_arm_spec_kernel(const ArmStreamDesc *_
             }
         };
         int bm = 1, bend = 0; // flags of the current block and its end column
+        // above-row context of the next pass, prefetched from LDS before the CABAC of the
+        // current one: the next pass starts at x + nd (nd = 1..4 latents decoded)
+        int pf_x = -1;
+        int32_t pf_a = 0;
         for (int x = 0; x < w;) {
             int L;
             if (blk > 0) {
@@ -507,7 +522,7 @@ __global__ __launch_bounds__(64) void dec_arm_spec_kernel(const ArmStreamDesc *_
             // at or right of x are the speculative zeros
             const int k = -(grp + cdx); // same row: distance back from x (1..4), <= 0 -> guess
             const int32_t rs = k == 1 ? r1 : k == 2 ? r2 : k == 3 ? r3 : k == 4 ? r4 : 0;
-            int32_t a = same_row ? rs : crow[x];
+            int32_t a = same_row ? rs : (x == pf_x ? pf_a : crow[x]);
             const bool f1 = w24 && !big;
 #pragma unroll
             for (int l = 0; l < NH; ++l) {
@@ -534,6 +549,7 @@ __global__ __launch_bounds__(64) void dec_arm_spec_kernel(const ArmStreamDesc *_
             si = si > 49 ? 49 : si;
             const uint2 e = *reinterpret_cast<const uint2 *>(ctab + (uint32_t)(mi * 50 + si) * 2u);
             const int32_t mq = mr >> 8;
+            const int32_t pf1 = crow[x + 1], pf2 = crow[x + 2], pf3 = crow[x + 3], pf4 = crow[x + 4];
             STAMP(t2);
             // decode_single (cc-bac.h:192-231), in order, until the first non-zero latent
             int nd = 0;
@@ -543,12 +559,12 @@ __global__ __launch_bounds__(64) void dec_arm_spec_kernel(const ArmStreamDesc *_
                 const uint32_t st = __builtin_amdgcn_readlane(e.x, src_lane);
                 const uint32_t stp = __builtin_amdgcn_readlane(e.y, src_lane);
                 int32_t val = 0;
-                if (cab.bin_static(st & 0xFF)) {
-                    if (!cab.bin_static((st >> 8) & 0xFF)) val = 1;
-                    else if (!cab.bin_static((st >> 16) & 0xFF)) val = 2;
-                    else if (!cab.bin_static(st >> 24)) val = 3;
+                if (cab.bin_state(st & 0xFF)) {
+                    if (!cab.bin_state((st >> 8) & 0xFF)) val = 1;
+                    else if (!cab.bin_state((st >> 16) & 0xFF)) val = 2;
+                    else if (!cab.bin_state(st >> 24)) val = 3;
                     else val = cab.expgolomb(0) + 4;
-                    if (cab.bin_static(stp)) val = -val;
+                    if (cab.bin_state(stp)) val = -val;
                 }
                 const int32_t q = __builtin_amdgcn_readlane(mq, src_lane) + val;
                 big |= (q >= 32768 || q <= -32768);
@@ -565,6 +581,8 @@ __global__ __launch_bounds__(64) void dec_arm_spec_kernel(const ArmStreamDesc *_
             st_acc[4] += nd;
 #endif
             x += nd;
+            pf_x = x;
+            pf_a = nd == 1 ? pf1 : nd == 2 ? pf2 : nd == 3 ? pf3 : pf4;
         }
         __syncthreads();
         int32_t *dst = S.out + (int64_t)y * w;

@@ -19,6 +19,8 @@
 //
 // Any other architecture runs the generic per-layer kernel (one launch per layer,
 // ping-pong through the caller's workspace).
+#include <type_traits>
+
 #include "fwd_common.h"
 
 using namespace ccmi_fwd;
@@ -71,22 +73,49 @@ __device__ __forceinline__ void store_out(const FusedArgs &A, float *out, int64_
     }
 }
 
+#if defined(CCMI_ARM_STAMPS)
+// diagnostic build (make stamps): per-phase cycle totals of the fused kernel, wave 0 of
+// every workgroup; read with ccmi_debug_fused_stamps()
+__device__ unsigned long long g_fstamp[8];
+#define FSTAMP(k)                                                                  \
+    do {                                                                           \
+        __syncthreads();                                                           \
+        const unsigned long long _t = __builtin_amdgcn_s_memtime();                \
+        if (threadIdx.x == 0) atomicAdd(&g_fstamp[k], _t - t_prev);                \
+        t_prev = _t;                                                               \
+    } while (0)
+#else
+#define FSTAMP(k)
+#endif
+
 using FT = UpsTile<8, 7, kRH, kRW>;
 constexpr int kHsRows = kRH / 2 + 1 + FT::NS - 1; // half-res rows under <= kRH clamped rows
 constexpr int kHrRows = kRH + 7 - 1;              // refine rows incl. the 7-tap halo
+constexpr int kSW = kRW / 2 + 1 + FT::NS - 1 + 3; // raw source tile pitch (37 used)
+constexpr int kTW = kRW + 7 - 1 + 2;              // raw latent tile pitch (70 used, 72 read)
+constexpr int kPairs = kRW / 2 + 1;               // even/odd column pairs under <= kRW columns
 
 template <int CIN, int CMID, bool UPS>
 __global__ __launch_bounds__(kFThreads) void syn_fused_kernel(FusedArgs A, LevelArgs U)
 {
     constexpr int NR = kRowsPerThread;
+    // region 0: raw input tiles (UPS, phase A-B), then the head output / 3x3 buffer 0
+    // region 1: horizontal-pass results (UPS, phase B-C), then the 3x3 buffer 1
+    constexpr int kRaw = UPS ? (CIN - 1) * kHsRows * kSW + kHrRows * kTW : 0;
     constexpr int kStage = UPS ? (CIN - 1) * kHsRows * kRW + kHrRows * kRW : 0;
+    constexpr int kBuf0 = CMID * kPlane > kRaw ? CMID * kPlane : kRaw;
     constexpr int kBuf1 = CMID * kPlane > kStage ? CMID * kPlane : kStage;
-    __shared__ __attribute__((aligned(16))) float s_pool[CMID * kPlane + kBuf1];
+    __shared__ __attribute__((aligned(16))) float s_pool[kBuf0 + kBuf1];
     float(*s_buf0)[kPlane] = reinterpret_cast<float(*)[kPlane]>(s_pool);
-    float(*s_buf1)[kPlane] = reinterpret_cast<float(*)[kPlane]>(s_pool + CMID * kPlane);
-    float *s_hs = s_pool + CMID * kPlane;          // [CIN-1][kHsRows][kRW]   (UPS only)
+    float(*s_buf1)[kPlane] = reinterpret_cast<float(*)[kPlane]>(s_pool + kBuf0);
+    float *s_st = s_pool;                           // [CIN-1][kHsRows][kSW] raw source tile (UPS only)
+    float *s_yt = s_st + (CIN - 1) * kHsRows * kSW; // [kHrRows][kTW] raw latent tile (UPS only)
+    float *s_hs = s_pool + kBuf0;                   // [CIN-1][kHsRows][kRW]   (UPS only)
     float *s_hr = s_hs + (CIN - 1) * kHsRows * kRW; // [kHrRows][kRW]          (UPS only)
     auto buf = [&](int which) { return which ? s_buf1 : s_buf0; };
+#if defined(CCMI_ARM_STAMPS)
+    unsigned long long t_prev = __builtin_amdgcn_s_memtime();
+#endif
     // head hidden unit j as 16 floats: w0[j][0..CIN), b0[j], w1[0..CMID)[j]; read back as
     // four broadcast ds_read_b128 (all lanes, one address) -- the loads are issued well
     // ahead of use, unlike the SGPR path whose scalar loads the compiler waits on at once
@@ -130,67 +159,154 @@ __global__ __launch_bounds__(kFThreads) void syn_fused_kernel(FusedArgs A, Level
 #pragma unroll
         for (int k = 0; k < 7; ++k) wr[k] = uprm[U.pre_off + k];
         const int nX = Xb - Xa + 1;
-        // horizontal pass of the transposed conv: Hs[c][jj][xi], half-res row Ya/2 + D0 + jj
+        const int jbase = Ya / 2 + FT::D0, ibase = Xa / 2 + FT::D0;
+        const int nj = Yb / 2 - Ya / 2 + FT::NS, ni = Xb / 2 - Xa / 2 + FT::NS;
+        const int nr = Yb - Ya + 7, nt = nX + 6;
+        // phase A: raw tiles, coalesced (lane-consecutive columns); fixed trip counts, so
+        // every load of a thread is issued before the first LDS store waits on one
         {
             const float *src = U.src + (int64_t)b * U.src_stride;
             const int64_t splane = (int64_t)U.hs * U.ws;
-            const int jbase = Ya / 2 + FT::D0;
-            const int nj = Yb / 2 - Ya / 2 + FT::NS;
-            for (int i = threadIdx.x; i < C * kHsRows * kRW; i += kFThreads) {
-                const int ch = i / (kHsRows * kRW), rem = i - ch * (kHsRows * kRW);
-                const int jj = rem / kRW, xi = rem - jj * kRW;
-                if (jj >= nj || xi >= nX) continue;
-                const int X = Xa + xi, a = X & 1, i0 = (X >> 1) + FT::D0;
-                const float *sr = src + ch * splane + (int64_t)clampi(jbase + jj, U.hs - 1) * U.ws;
-                float acc = 0.f;
+            constexpr int NSI = C * kHsRows * kSW, NSU = (NSI + kFThreads - 1) / kFThreads;
+            float sv[NSU];
 #pragma unroll
-                for (int m = 0; m < FT::NS; ++m) {
-                    const int te = FT::tap(0, FT::D0 + m), to = FT::tap(1, FT::D0 + m);
-                    const int tp = a ? to : te;
-                    if ((a ? to : te) >= 0) {
-                        float v = sr[clampi(i0 + m, U.ws - 1)];
-                        if (U.src_quant) v = rintf(U.gain * v);
-                        acc = fmaf(wu[tp], v, acc);
-                    }
-                }
-                s_hs[i] = acc;
+            for (int u = 0; u < NSU; ++u) {
+                const int i = threadIdx.x + u * kFThreads;
+                const int ch = i / (kHsRows * kSW), rem = i - ch * (kHsRows * kSW);
+                const int jj = rem / kSW, ii = rem - jj * kSW;
+                sv[u] = 0.f;
+                if (i < NSI && jj < nj && ii < ni)
+                    sv[u] = src[ch * splane + (int64_t)clampi(jbase + jj, U.hs - 1) * U.ws + clampi(ibase + ii, U.ws - 1)];
+            }
+            const float *rs = U.ref_src + (int64_t)b * U.ref_stride;
+            constexpr int NTI = kHrRows * kTW, NTU = (NTI + kFThreads - 1) / kFThreads;
+            float tv[NTU];
+#pragma unroll
+            for (int u = 0; u < NTU; ++u) {
+                const int i = threadIdx.x + u * kFThreads;
+                const int yr = i / kTW, xt = i - yr * kTW;
+                const int Y = Ya - 3 + yr, X = Xa - 3 + xt;
+                tv[u] = 0.f;
+                if (i < NTI && yr < nr && xt < nt && Y >= 0 && Y < U.hd && X >= 0 && X < U.wd)
+                    tv[u] = rs[(int64_t)Y * U.wd + X];
+            }
+#pragma unroll
+            for (int u = 0; u < NSU; ++u) {
+                const int i = threadIdx.x + u * kFThreads;
+                if (i < NSI) s_st[i] = U.src_quant ? rintf(U.gain * sv[u]) : sv[u];
+            }
+#pragma unroll
+            for (int u = 0; u < NTU; ++u) {
+                const int i = threadIdx.x + u * kFThreads;
+                if (i < NTI) s_yt[i] = U.ref_quant ? rintf(U.gain * tv[u]) : tv[u];
             }
         }
-        // horizontal pass of the refine (zero padding): Hr[yr][xi], image row Ya - 3 + yr
+        __syncthreads();
+        FSTAMP(0);
+        // phase B: horizontal passes from LDS, in ups_level_fixed's operation order.
+        // Transposed conv: one item = the (even, odd) column pair 2k, 2k+1 of a source row,
+        // which share NS source samples (compile-time taps per parity).
         {
-            const float *rs = U.ref_src + (int64_t)b * U.ref_stride;
-            const int nr = Yb - Ya + 7;
-            for (int i = threadIdx.x; i < kHrRows * kRW; i += kFThreads) {
-                const int yr = i / kRW, xi = i - yr * kRW;
-                if (yr >= nr || xi >= nX) continue;
-                const int Y = Ya - 3 + yr, X = Xa + xi;
-                float acc = 0.f;
-                if (Y >= 0 && Y < U.hd) {
+            const int xe0 = Xa & ~1; // first even column of the pairs
+#pragma unroll 2
+            for (int i = threadIdx.x; i < C * kHsRows * kPairs; i += kFThreads) {
+                const int ch = i / (kHsRows * kPairs), rem = i - ch * (kHsRows * kPairs);
+                const int jj = rem / kPairs, k = rem - jj * kPairs;
+                if (jj >= nj) continue;
+                const int xe = xe0 + 2 * k - Xa; // window-relative column of the even output
+                if (xe > nX - 1) continue;
+                const float *sr = s_st + (ch * kHsRows + jj) * kSW + k;
+                float e = 0.f, o = 0.f;
 #pragma unroll
-                    for (int k = 0; k < 7; ++k) {
-                        const int xx = X - 3 + k;
-                        float v = 0.f;
-                        if (xx >= 0 && xx < U.wd) {
-                            v = rs[(int64_t)Y * U.wd + xx];
-                            if (U.ref_quant) v = rintf(U.gain * v);
-                        }
-                        acc = fmaf(wr[k], v, acc);
-                    }
+                for (int m = 0; m < FT::NS; ++m) {
+                    const float v = sr[m];
+                    const int te = FT::tap(0, FT::D0 + m), to = FT::tap(1, FT::D0 + m);
+                    if (te >= 0) e = fmaf(wu[te], v, e);
+                    if (to >= 0) o = fmaf(wu[to], v, o);
                 }
-                s_hr[i] = acc;
+                float *hr = s_hs + (ch * kHsRows + jj) * kRW;
+                if (xe >= 0) hr[xe] = e;
+                if (xe + 1 < nX) hr[xe + 1] = o;
+            }
+        }
+        // refine: one item = 4 consecutive columns of a row (sliding 7-tap window)
+        for (int i = threadIdx.x; i < kHrRows * (kRW / 4); i += kFThreads) {
+            const int yr = i / (kRW / 4), x4 = (i - yr * (kRW / 4)) * 4;
+            if (yr >= nr || x4 >= nX) continue;
+            const float *tr = s_yt + yr * kTW + x4;
+            float t[10];
+#pragma unroll
+            for (int k = 0; k < 10; ++k) t[k] = tr[k];
+            // rows outside the image are the vertical pass's zero padding
+            const int Y = Ya - 3 + yr;
+            const bool in_img = Y >= 0 && Y < U.hd;
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                float acc = 0.f;
+#pragma unroll
+                for (int k = 0; k < 7; ++k) acc = fmaf(wr[k], t[q + k], acc);
+                s_hr[yr * kRW + x4 + q] = in_img ? acc : 0.f;
             }
         }
         __syncthreads();
     }
 
+    FSTAMP(1);
     // ------------------------ pass 0: per-pixel 1x1 head ------------------------
     {
         const cfloat_ptr w0 = prm + A.w0_off, b0 = prm + A.b0_off;
         const cfloat_ptr b1 = prm + A.b1_off;
         float x[NR][CIN];
         float o[NR][CMID];
+        // interior windows (no row clamping): the thread's 4 rows are consecutive, so the
+        // vertical passes share their LDS rows -- 10 refine rows and 6 or 7 half-res rows
+        // per channel for 4 pixels, offsets fixed by the parity of the window's first row
+        bool done = false;
+        if constexpr (UPS) {
+            if (oy >= 0 && oy + kRH <= A.H) {
+                const int xi = cxg - Xa;
+                auto gather = [&](auto par) {
+                    constexpr int P = decltype(par)::value; // parity of oy (and of row rb)
+                    {
+                        float h[NR + 6];
+#pragma unroll
+                        for (int k = 0; k < NR + 6; ++k) h[k] = s_hr[(rb + k) * kRW + xi];
+#pragma unroll
+                        for (int p = 0; p < NR; ++p) {
+                            float acc = 0.f;
+#pragma unroll
+                            for (int k = 0; k < 7; ++k) acc = fmaf(wr[k], h[p + k], acc);
+                            x[p][0] = acc + s_yt[(rb + p + 3) * kTW + xi + 3];
+                        }
+                    }
+                    constexpr int NH = FT::NS + (NR / 2) - 1 + P; // half-res rows for 4 pixels
+                    const int j0 = rb / 2;
+#pragma unroll
+                    for (int k = 1; k < CIN; ++k) {
+                        float h[NH];
+#pragma unroll
+                        for (int m = 0; m < NH; ++m) h[m] = s_hs[((k - 1) * kHsRows + j0 + m) * kRW + xi];
+#pragma unroll
+                        for (int p = 0; p < NR; ++p) {
+                            const int a = (P + p) & 1, off = (P + p) >> 1;
+                            float acc = 0.f;
+#pragma unroll
+                            for (int m = 0; m < FT::NS; ++m) {
+                                const int te = FT::tap(0, FT::D0 + m), to = FT::tap(1, FT::D0 + m);
+                                if ((a ? to : te) >= 0) acc = fmaf(wu[a ? to : te], h[off + m], acc);
+                            }
+                            x[p][k] = acc;
+                        }
+                    }
+                };
+                if (oy & 1) gather(std::integral_constant<int, 1>{});
+                else gather(std::integral_constant<int, 0>{});
+                done = true;
+            }
+        }
 #pragma unroll
         for (int p = 0; p < NR; ++p) {
+            if (done) break;
             const int Y = clampi(oy + rb + p, A.H - 1);
             if constexpr (UPS) {
                 // vertical passes, in ups_level_fixed's operation order
@@ -199,9 +315,8 @@ __global__ __launch_bounds__(kFThreads) void syn_fused_kernel(FusedArgs A, Level
                     float acc = 0.f;
 #pragma unroll
                     for (int k = 0; k < 7; ++k) acc = fmaf(wr[k], s_hr[(yi + k) * kRW + xi], acc);
-                    float q0 = U.ref_src[(int64_t)b * U.ref_stride + (int64_t)Y * U.wd + cxg];
-                    if (U.ref_quant) q0 = rintf(U.gain * q0);
-                    x[p][0] = acc + q0;
+                    // residual: the (quantised) latent, from the raw tile still in LDS
+                    x[p][0] = acc + s_yt[(yi + 3) * kTW + xi + 3];
                 }
                 const int jj0 = Y / 2 - Ya / 2, a = Y & 1;
 #pragma unroll
@@ -221,6 +336,9 @@ __global__ __launch_bounds__(kFThreads) void syn_fused_kernel(FusedArgs A, Level
                 for (int k = 0; k < CIN; ++k) x[p][k] = in[k * plane + pix];
             }
         }
+        // the raw tiles (region 0) are overwritten by the head output below
+        if constexpr (UPS) __syncthreads();
+        FSTAMP(2);
         if (A.n_head == 2) {
             const int hid = A.hid;
             // fmaxf(acc, lo0) is the optional ReLU without a per-element select
@@ -282,6 +400,7 @@ __global__ __launch_bounds__(kFThreads) void syn_fused_kernel(FusedArgs A, Level
                 }
             }
         }
+        FSTAMP(3);
         if (halo == 0) {
 #pragma unroll
             for (int p = 0; p < NR; ++p) {
@@ -370,6 +489,7 @@ __global__ __launch_bounds__(kFThreads) void syn_fused_kernel(FusedArgs A, Level
         }
         cur ^= 1;
     }
+    FSTAMP(4);
 }
 
 // Generic layer: any ks (odd), any channel counts; replicate padding.
@@ -628,3 +748,15 @@ extern "C" int ccmi_decode_forward_f32(const ccmi_decode_args *a, void *stream)
     CCMI_HIP_CHECK(hipGetLastError());
     return CCMI_OK;
 }
+
+#if defined(CCMI_ARM_STAMPS)
+extern "C" int ccmi_debug_fused_stamps(unsigned long long *out, int reset)
+{
+    if (out) CCMI_HIP_CHECK(hipMemcpyFromSymbol(out, HIP_SYMBOL(g_fstamp), sizeof(unsigned long long) * 8));
+    if (reset) {
+        unsigned long long z[8] = {};
+        CCMI_HIP_CHECK(hipMemcpyToSymbol(HIP_SYMBOL(g_fstamp), z, sizeof z));
+    }
+    return CCMI_OK;
+}
+#endif

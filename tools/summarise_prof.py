@@ -18,13 +18,20 @@ from collections import defaultdict
 from pathlib import Path
 
 ROOT = Path(__file__).resolve().parents[1]
-STAGES = {"arm_fwd_kernel": "arm", "ups_level_kernel": "ups", "ups_level_fixed": "ups", "syn_fused_kernel": "syn", "syn_layer_kernel": "syn",
-          "post_kernel": "post", "dec_arm": "dec_arm", "dec_ups": "dec_ups", "dec_syn": "dec_syn"}
+STAGES = {"arm_fwd_kernel": "arm", "ups_level_kernel": "ups", "ups_level_fixed": "ups", "syn_fused_kernel": "syn",
+          "syn_layer_kernel": "syn", "post_kernel": "post", "dec_arm": "dec_arm", "dec_ups": "dec_ups",
+          "dec_syn": "dec_syn"}
+FUSED = False  # set from the trace: a fused-decode run (syn_fused_kernel<..., true>) present
 
 
 def stage_of(name: str):
+    # the fused decode tail: syn_fused_kernel<CIN, CMID, true> ("Lb1E" in the mangled name)
+    if "syn_fused_kernel" in name and "Lb1E" in name:
+        return "decode_fused"
     for k, v in STAGES.items():
         if k in name:
+            if v == "ups" and FUSED:
+                return "ups_pyramid"
             return v
     return None
 
@@ -50,7 +57,10 @@ def main(src: str, tag: str):
     src = Path(src)
     prof = ROOT / "profiles"
     prof.mkdir(exist_ok=True)
+    global FUSED
     shutil.copy(src / "trace" / "run_kernel_stats.csv", prof / f"{tag}_kernel_stats.csv")
+    FUSED = any("syn_fused_kernel" in r["Name"] and "Lb1E" in r["Name"]
+                for r in csv.DictReader((src / "trace" / "run_kernel_stats.csv").open()))
     fetch = per_step_counter(src / "pmc_fetch" / "run_counter_collection.csv", "FETCH_SIZE")
     write = per_step_counter(src / "pmc_write" / "run_counter_collection.csv", "WRITE_SIZE")
     stats = {r["Name"]: r for r in csv.DictReader((src / "trace" / "run_kernel_stats.csv").open())}
@@ -64,7 +74,7 @@ def main(src: str, tag: str):
     n_steps = calls.get("arm", 1)
     res = {
         "source": str(src),
-        "note": "per launch = one bench step (batch of frames); ups sums its per-level dispatches. "
+        "note": "per launch = one bench step (batch of frames); ups / ups_pyramid sum their per-level dispatches. "
                 "hbm = 2 * FETCH_SIZE + WRITE_SIZE (KiB -> bytes), gfx950 FETCH_SIZE halving corrected "
                 "as MI355X_MICROARCH.md prescribes for wide reads (dword-wide accesses are uncalibrated).",
         "fetch_kib_raw": fetch,
