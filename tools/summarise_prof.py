@@ -26,7 +26,7 @@ FUSED = False  # set from the trace: a fused-decode run (syn_fused_kernel<..., t
 
 def stage_of(name: str):
     # the fused decode tail: syn_fused_kernel<CIN, CMID, true> ("Lb1E" in the mangled name)
-    if "syn_fused_kernel" in name and "Lb1E" in name:
+    if "syn_fused_kernel" in name and ("Lb1E" in name or "true>" in name):
         return "decode_fused"
     for k, v in STAGES.items():
         if k in name:
@@ -59,7 +59,7 @@ def main(src: str, tag: str):
     prof.mkdir(exist_ok=True)
     global FUSED
     shutil.copy(src / "trace" / "run_kernel_stats.csv", prof / f"{tag}_kernel_stats.csv")
-    FUSED = any("syn_fused_kernel" in r["Name"] and "Lb1E" in r["Name"]
+    FUSED = any("syn_fused_kernel" in r["Name"] and ("Lb1E" in r["Name"] or "true>" in r["Name"])
                 for r in csv.DictReader((src / "trace" / "run_kernel_stats.csv").open()))
     fetch = per_step_counter(src / "pmc_fetch" / "run_counter_collection.csv", "FETCH_SIZE")
     write = per_step_counter(src / "pmc_write" / "run_counter_collection.csv", "WRITE_SIZE")
