@@ -208,6 +208,83 @@ int ccmi_decode_last_timing(float *ms4);
 int ccmi_decode_output_size(const uint8_t *stream, size_t len, int out_bitdepth,
                             int out_chroma, int as_yuv, size_t *size);
 
+/* ------------------------------------------------------------------------- */
+/* Path B writer: .cool encoder (the inverse of the decoder above).           */
+/* ------------------------------------------------------------------------- */
+
+/* Network parameter slots, in bitstream order (header.py:352-375, encode.py:364-390). */
+enum { CCMI_NN_ARM_W = 0, CCMI_NN_ARM_B, CCMI_NN_UPS_W, CCMI_NN_UPS_B, CCMI_NN_SYN_W, CCMI_NN_SYN_B, CCMI_NN_SLOTS };
+
+/* Everything a .cool intra frame carries besides its latent substreams: the GOP header
+ * (header.py:72-117), the frame header (header.py:236-392) and the quantised network
+ * integers (the values cc_code_wb_bac codes, encode.py:255-352).  Filled by
+ * ccmi_cool_parse, consumed by ccmi_encode_frame. */
+typedef struct ccmi_cool_desc {
+    int h, w;                  /* image size */
+    int bitdepth;              /* 8..16 */
+    int frame_data_type;       /* 0 rgb, 1 yuv420, 2 yuv444 */
+    int intra_period, p_period;
+    int display_index;
+    int dim_arm, n_hidden_arm;
+    int n_ups, ups_k, n_pre, pre_k;
+    int n_branches;
+    int n_syn_layers;
+    int syn_out[16], syn_ks[16];
+    int syn_type[16];          /* raw byte: mode index * 16 + non-linearity index */
+    int flow_gain;
+    int ac_max_val_nn, ac_max_val_latent;
+    int hls_sig_blksize;       /* signed: < 0 = adaptive block flags */
+    int q_step_index[6];       /* CCMI_NN_* slots; -1 = slot absent (255 in the stream) */
+    int expgol_count[6];       /* Exp-Golomb counts; ccmi_encode_frame: -1 = search 0..12 */
+    int n_bytes_nn[6];         /* output of parse / encode */
+    int n_grids;               /* latent resolutions (one 2D grid each) */
+    int n_bytes_latent[8];     /* output of parse / encode */
+    const int32_t *nn[6];      /* quantised integers per slot (host) */
+    int nn_len[6];
+} ccmi_cool_desc;
+
+/* Parse the GOP + frame header of an intra .cool stream and decode its network
+ * integers into nn_buf (nn_cap int32 slots; desc->nn[] point into it).  Host only. */
+int ccmi_cool_parse(const uint8_t *stream, size_t len, ccmi_cool_desc *desc, int32_t *nn_buf, size_t nn_cap);
+
+/* cc_code_wb_bac (ccencapi.cpp:97-177): Exp-Golomb(count) magnitudes + EP signs, one
+ * CABAC substream.  use_count < 0 searches counts 0..12 for the fewest bytes (first
+ * wins ties).  *len = bytes written (or needed, with CCMI_ERR_ARG, when cap is short). */
+int ccmi_code_wb(const int32_t *x, int n, int use_count, uint8_t *out, size_t cap, size_t *len, int *count_used);
+
+/* cc_decode_wb::decode_wb_continue (ccencapi.cpp:412-454) without hidden state: decode
+ * n_runs consecutive runs of run_len[r] integers, run r with Exp-Golomb count
+ * run_count[r], from one network substream; out receives sum(run_len) integers. */
+int ccmi_decode_wb(const uint8_t *stream, size_t len, int n_runs, const int *run_len, const int *run_count, int32_t *out);
+
+/* cc_code_latent_layer_bac (ccencapi.cpp:179-410): one latent grid, raster order, with
+ * per-latent mu / log_scale in ARM fixed point (x256, the decoder's integers).  Host. */
+int ccmi_code_latent_layer(const int32_t *x, const int32_t *mu, const int32_t *log_scale, int h, int w,
+                           int hls_sig_blksize, uint8_t *out, size_t cap, size_t *len);
+
+/* Integer ARM over every latent of every grid, fully parallel (the encoder side knows
+ * all latents): the decoder's fixed-point arithmetic (arm_cpu.cpp:18-106 = ArmInt
+ * pure_int, armint.py:80-261).  latent: int32 values [n] (grids flattened in order);
+ * params: the decoder's integers, per hidden layer W[d][d] (out, in) then b[d], then
+ * W_out[2][d], b_out[2].  mu / log_scale: int32 [n] (x256).  Device pointers. */
+typedef struct ccmi_arm_i32_args {
+    const int32_t *latent;
+    int n_grids;
+    int h[8], w[8];
+    int dim_arm, n_hidden;
+    const int32_t *params;
+    int32_t *mu, *log_scale;
+} ccmi_arm_i32_args;
+int ccmi_arm_forward_i32(const ccmi_arm_i32_args *args, void *stream);
+
+/* Write a whole .cool stream (GOP header, frame header, network substreams, latent
+ * substreams; encode.py:113-623) for integer latents latent_dev (device, int32, grids
+ * flattened).  ARM contexts run on the GPU (ccmi_arm_forward_i32); the CABAC substreams
+ * are coded on host threads.  Fills desc->expgol_count / n_bytes_nn / n_bytes_latent.
+ * *len = bytes written (or needed, with CCMI_ERR_ARG, when cap is short). */
+int ccmi_encode_frame(ccmi_cool_desc *desc, const int32_t *latent_dev, uint8_t *out, size_t cap, size_t *len,
+                      void *stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -437,6 +437,33 @@ static int ctx_offsets(int d, int *dy, int *dx)
     return 0;
 }
 
+/* The ARM MLP at latent (y, x) of a plane holding value << 8 (arm_cpu.cpp:18-106):
+ * contexts outside the plane are 0; p[0] = mu, p[1] = log_scale, both x256. */
+static void arm_eval(const nets_t *nn, const int32_t *plane, int w, int y, int x, const int *dy, const int *dx,
+                     int32_t p[2])
+{
+    int d = nn->d;
+    int32_t a[32], b[32];
+    for (int i = 0; i < d; i++) {
+        int yy = y + dy[i], xx = x + dx[i];
+        a[i] = (yy >= 0 && xx >= 0 && xx < w) ? plane[yy * w + xx] : 0;
+    }
+    int32_t *in = a, *out = b;
+    for (int l = 0; l < nn->nh; l++) {
+        for (int o = 0; o < d; o++) {
+            int32_t s = nn->b_hidden[l][o] + in[o] * 256; /* residual */
+            for (int i = 0; i < d; i++) s += in[i] * nn->w_hidden[l][o * d + i];
+            out[o] = s < 0 ? 0 : (s + 128) >> 8;
+        }
+        int32_t *t = in; in = out; out = t;
+    }
+    for (int o = 0; o < 2; o++) {
+        int32_t s = nn->b_out[o];
+        for (int i = 0; i < d; i++) s += in[i] * nn->w_out[o * d + i];
+        p[o] = s < 0 ? -((-s + 128) >> 8) : (s + 128) >> 8;
+    }
+}
+
 static int arm_decode_layer(const nets_t *nn, const uint8_t *bytes, size_t nbytes, int sig_blk,
                             int h, int w, int32_t *plane)
 {
@@ -466,7 +493,6 @@ static int arm_decode_layer(const nets_t *nn, const uint8_t *bytes, size_t nbyte
     }
     int d = nn->d, dy[32], dx[32];
     ctx_offsets(d, dy, dx);
-    int32_t a[32], b[32];
     memset(plane, 0, sizeof(int32_t) * (size_t)h * w);
     for (int y = 0; y < h; y++)
         for (int x = 0; x < w; x++) {
@@ -479,25 +505,8 @@ static int arm_decode_layer(const nets_t *nn, const uint8_t *bytes, size_t nbyte
                     if (y & mask) { *dst = dst[-w]; continue; }
                 }
             }
-            for (int i = 0; i < d; i++) {
-                int yy = y + dy[i], xx = x + dx[i];
-                a[i] = (yy >= 0 && xx >= 0 && xx < w) ? plane[yy * w + xx] : 0;
-            }
-            int32_t *in = a, *out = b;
-            for (int l = 0; l < nn->nh; l++) {
-                for (int o = 0; o < d; o++) {
-                    int32_t s = nn->b_hidden[l][o] + in[o] * 256; /* residual */
-                    for (int i = 0; i < d; i++) s += in[i] * nn->w_hidden[l][o * d + i];
-                    out[o] = s < 0 ? 0 : (s + 128) >> 8;
-                }
-                int32_t *t = in; in = out; out = t;
-            }
             int32_t p[2];
-            for (int o = 0; o < 2; o++) {
-                int32_t s = nn->b_out[o];
-                for (int i = 0; i < d; i++) s += in[i] * nn->w_out[o * d + i];
-                p[o] = s < 0 ? -((-s + 128) >> 8) : (s + 128) >> 8;
-            }
+            arm_eval(nn, plane, w, y, x, dy, dx, p);
             int mr, mi, si;
             mu_sig_index(p[0], p[1], &mr, &mi, &si);
             *dst = (int32_t)((uint32_t)(mr + decode_value(&c, mi, si)) << ARM_PREC);
@@ -755,6 +764,27 @@ int cco_decode_frame_mem(const uint8_t *bs, size_t n, cco_frame *f)
     free_nets(nn);
     free(nn);
     return rc;
+}
+
+int cco_arm_params(const uint8_t *bs, size_t n, const cco_frame *f, int32_t **mu, int32_t **log_scale)
+{
+    hdr_t h;
+    if (parse(bs, n, &h)) return 1;
+    nets_t *nn = (nets_t *)malloc(sizeof(nets_t));
+    if (read_nets(&h, nn)) { free_nets(nn); free(nn); return 1; }
+    int dy[32], dx[32];
+    ctx_offsets(nn->d, dy, dx);
+    for (int l = 0; l < f->n_layers; l++)
+        for (int y = 0; y < f->lh[l]; y++)
+            for (int x = 0; x < f->lw[l]; x++) {
+                int32_t p[2];
+                arm_eval(nn, f->lat[l], f->lw[l], y, x, dy, dx, p);
+                mu[l][y * f->lw[l] + x] = p[0];
+                log_scale[l][y * f->lw[l] + x] = p[1];
+            }
+    free_nets(nn);
+    free(nn);
+    return 0;
 }
 
 void cco_frame_free(cco_frame *f)

@@ -38,6 +38,11 @@ typedef struct cco_frame {
 int cco_decode_frame_mem(const uint8_t *bs, size_t n, cco_frame *out);
 void cco_frame_free(cco_frame *f);
 
+/* Encoder-side ARM parameters: mu / log_scale (x256) of EVERY latent of a decoded frame
+ * (flat-block latents included), as encode.py:510-560 computes them with ArmInt before
+ * cc_code_latent_layer_bac.  mu[l], log_scale[l]: caller arrays of lh[l] * lw[l]. */
+int cco_arm_params(const uint8_t *bs, size_t n, const cco_frame *f, int32_t **mu, int32_t **log_scale);
+
 /* Output conversions, as the reference CLI writes them
  * (ccdecapi.cpp:59-128 ppm_out, :132-180 convert_444_420_8b, 444 raw). */
 size_t cco_output_size(const cco_frame *f, int out_bitdepth, int out_chroma, int is_yuv);

@@ -45,6 +45,9 @@ def oracle_c():
     import ctypes
     lib = ctypes.CDLL(str(so))
     lib.cco_decode_file.argtypes = [ctypes.c_char_p, ctypes.c_char_p, ctypes.c_int, ctypes.c_int, ctypes.c_int]
+    lib.cco_decode_frame_mem.argtypes = [ctypes.c_void_p, ctypes.c_size_t, ctypes.c_void_p]
+    lib.cco_frame_free.argtypes = [ctypes.c_void_p]
+    lib.cco_arm_params.argtypes = [ctypes.c_void_p, ctypes.c_size_t, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]
     return lib
 
 
