@@ -219,6 +219,34 @@ def bench_bitexact_decode(reps: int):
             "data": "15 shipped JVET class-E .cool bitstreams (results/image/jvet), repeated"}
 
 
+def bench_bitexact_encode(reps: int = 2):
+    """Path B writer: ccmi_encode_frame (GPU integer ARM over all latents + host CABAC, one
+    thread per latent grid) re-encoding the shipped class-E streams from their decoded
+    latents; the output must equal the shipped bytes."""
+    from ccmi import decode, encode
+    import numpy as np
+    files = sorted((ROOT / "tests/golden/cool").glob("E-*.cool"))
+    jobs = []
+    for f in files:
+        data = f.read_bytes()
+        fr = encode.parse(data)
+        lat = decode.decode_latents(data)
+        jobs.append((data, fr, torch.from_numpy(np.concatenate(lat)).to(torch.int32).cuda()))
+    encode.encode_frame(jobs[0][1], jobs[0][2])
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    exact = True
+    for _ in range(reps):
+        for data, fr, x in jobs:
+            exact &= encode.encode_frame(fr, x) == data
+    dt = time.perf_counter() - t0
+    n = reps * len(jobs)
+    return {"metric": "bit-exact .cool encode Mpixel/s (GPU ARM contexts + host CABAC, one frame at a time)",
+            "frames": n, "value": round(n * H * W / dt / 1e6, 2), "unit": "Mpixel/s",
+            "ms_per_frame": round(dt / n * 1e3, 3), "identical_to_shipped_streams": exact,
+            "data": "15 shipped JVET class-E .cool bitstreams re-encoded from their decoded latents"}
+
+
 def cpu_decode_baseline(budget_s=10.0):
     """The reference C decoder (oracle/_ref, built from /root/reference sources) -- or the C oracle
     when that binary is absent -- decoding the class-E streams, one process per core."""
@@ -365,6 +393,7 @@ def main():
         if world == 1 and not args.no_cpu_baseline:
             dec["cpu_baseline"] = cpu_decode_baseline()
         res["bitexact_decode"] = dec
+        res["bitexact_encode"] = bench_bitexact_encode()
     if rank == 0:
         print(json.dumps(res), flush=True)
     if dist:

@@ -44,6 +44,29 @@ def decode_batch(streams: Sequence[bytes], output_bitdepth: int = 0, output_chro
     return [o.raw[: got[i]] for i, o in enumerate(outs)]
 
 
+def decode_latents(stream: bytes, stream_handle: int | None = None) -> list:
+    """Integer latents of an intra .cool stream, decoded on the GPU (one np.int32 array
+    per grid, row-major)."""
+    import numpy as np
+    from . import encode
+    fr = encode.parse(stream)
+    n = sum(h * w for h, w in fr.grid_sizes)
+    out = np.zeros(n, dtype=np.int32)
+    buf = C.create_string_buffer(stream, len(stream))
+    L = lib()
+    L.ccmi_decode_latents.argtypes = [C.c_void_p, C.c_size_t, C.c_void_p, C.c_size_t, C.c_void_p]
+    L.ccmi_decode_latents.restype = C.c_int
+    if stream_handle is None:
+        import torch
+        stream_handle = torch.cuda.current_stream().cuda_stream
+    check(L.ccmi_decode_latents(C.cast(buf, C.c_void_p), len(stream), out.ctypes.data, n, stream_handle))
+    res, p = [], 0
+    for h, w in fr.grid_sizes:
+        res.append(out[p: p + h * w].copy())
+        p += h * w
+    return res
+
+
 def last_timing() -> dict:
     """Device stage times (ms) of this thread's last decode: upload, arm_cabac, ups_syn_out, download."""
     ms = (C.c_float * 4)()
@@ -51,4 +74,4 @@ def last_timing() -> dict:
     return dict(zip(("upload", "arm_cabac", "ups_syn_out", "download"), list(ms)))
 
 
-__all__ = ["last_timing", "decode_file", "decode_batch", "output_size", "CcmiError"]
+__all__ = ["last_timing", "decode_latents", "decode_file", "decode_batch", "output_size", "CcmiError"]

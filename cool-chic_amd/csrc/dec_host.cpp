@@ -283,7 +283,8 @@ struct EventSet {
 };
 
 int decode_many(const uint8_t *const *streams, const size_t *lens, int n, uint8_t *const *outs, const size_t *caps,
-                size_t *sizes, int out_bitdepth, int out_chroma, int as_yuv, hipStream_t s)
+                size_t *sizes, int out_bitdepth, int out_chroma, int as_yuv, hipStream_t s,
+                int32_t *const *lat_out = nullptr)
 {
     if (n < 1) return ccmi_set_error(CCMI_ERR_ARG, "decode: no streams");
     std::vector<FrameHost> fr(n);
@@ -501,7 +502,11 @@ int decode_many(const uint8_t *const *streams, const size_t *lens, int n, uint8_
                                       hipMemcpyDeviceToHost, s));
     }
     ev.rec(4, s);
+    for (int i = 0; i < n && lat_out; ++i)
+        CCMI_HIP_CHECK(hipMemcpyAsync(lat_out[i], dev + pl[i].lat_off, pl[i].lat_elems * 4, hipMemcpyDeviceToHost, s));
     CCMI_HIP_CHECK(hipStreamSynchronize(s));
+    for (int i = 0; i < n && lat_out; ++i)
+        for (size_t k = 0; k < pl[i].lat_elems; ++k) lat_out[i][k] >>= kArmPrec;
 #if defined(CCMI_ARM_STAMPS)
     {
         std::vector<uint64_t> dbg(8 * all.size());
@@ -549,6 +554,21 @@ extern "C" int ccmi_decode_batch(const uint8_t *const *streams, const size_t *le
     if (!streams || !lens || !out || !out_caps) return ccmi_set_error(CCMI_ERR_ARG, "decode_batch: null argument");
     return decode_many(streams, lens, n, out, out_caps, out_sizes, out_bitdepth, out_chroma, as_yuv,
                        static_cast<hipStream_t>(stream));
+}
+
+extern "C" int ccmi_decode_latents(const uint8_t *stream, size_t len, int32_t *out, size_t cap, void *hstream)
+{
+    if (!stream || !out) return ccmi_set_error(CCMI_ERR_ARG, "decode_latents: null argument");
+    FrameHost f;
+    if (int rc = parse_and_decode_frame(stream, len, f)) return rc;
+    size_t n = 0;
+    for (int l = 0; l < f.n_layers; ++l) n += (size_t)f.lh[l] * f.lw[l];
+    if (cap < n) return ccmi_set_error(CCMI_ERR_ARG, "decode_latents: buffer of %zu ints, need %zu", cap, n);
+    size_t osz = 0;
+    if (int rc = ccmi_decode_output_size(stream, len, 0, 0, 1, &osz)) return rc;
+    std::vector<uint8_t> tmp(osz);
+    uint8_t *op = tmp.data();
+    return decode_many(&stream, &len, 1, &op, &osz, nullptr, 0, 0, 1, static_cast<hipStream_t>(hstream), &out);
 }
 
 static bool ends_with(const std::string &a, const char *b)

@@ -204,6 +204,10 @@ int ccmi_decode_batch(const uint8_t *const *streams, const size_t *lens, int n,
  * [3] download of the decoded bytes. */
 int ccmi_decode_last_timing(float *ms4);
 
+/* The integer latents of one intra stream (ARM + CABAC decode on the GPU; values, not
+ * shifted), grids flattened in order: out needs sum_l h_l * w_l int32 (host buffer). */
+int ccmi_decode_latents(const uint8_t *stream, size_t len, int32_t *out, size_t cap, void *stream_handle);
+
 /* Byte size of the decoded output of one stream (header parse only). */
 int ccmi_decode_output_size(const uint8_t *stream, size_t len, int out_bitdepth,
                             int out_chroma, int as_yuv, size_t *size);

@@ -197,3 +197,14 @@ def test_gpu_encode_decode_round_trip_synthetic(enc, oracle_c, gpu, tmp_path):
     p.write_bytes(s1)
     assert oracle_c.cco_decode_file(str(p).encode(), str(tmp_path / "o.yuv").encode(), 0, 0, 0) == 0
     assert y_gpu == (tmp_path / "o.yuv").read_bytes()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("f", SMALL[::4] + E720[:1], ids=lambda f: f.stem[:36])
+def test_gpu_decode_latents_match_oracle(f, enc, oracle_c, gpu):
+    from ccmi import decode
+    data = f.read_bytes()
+    _, ref, _, _ = oracle_latents(oracle_c, data, with_params=False)
+    got = decode.decode_latents(data)
+    for a, b in zip(got, ref):
+        np.testing.assert_array_equal(a, b)
