@@ -1,0 +1,36 @@
+"""The CPU restatement of the encoder overfit step (oracle/train_oracle.py) reproduces the
+reference's loss, gradients and two clipped-Adam steps (tests/golden/train_*.npz, made
+by tools/gen_golden_train.py from the reference modules)."""
+from pathlib import Path
+
+import numpy as np
+import pytest
+import torch
+
+GOLDEN = Path(__file__).resolve().parent / "golden"
+FILES = sorted(GOLDEN.glob("train_*.npz"))
+
+
+@pytest.mark.parametrize("f", FILES, ids=lambda f: f.stem)
+def test_oracle_train_step_matches_reference(f):
+    import train_oracle as to
+    z = np.load(f)
+    st, target, meta = to.from_golden(z)
+    args = (target, meta["quantizer_type"], meta["temperature"], meta["lmbda"], meta["yuv420"])
+    L, mse, r = to.grads(st, *args)
+    assert abs(L - float(z["loss"])) <= 1e-5 * abs(float(z["loss"]))
+    assert abs(r - float(z["rate_bit"])) <= 1e-5 * float(z["rate_bit"])
+    names = to.golden_param_names(meta)
+    for name, p in zip(names, st.params()):
+        g = z[f"g/{name}"].reshape(p.shape)
+        np.testing.assert_allclose(p.grad.numpy(), g, rtol=2e-4, atol=1e-7 + 2e-4 * np.abs(g).max(), err_msg=name)
+    # two clipped Adam steps.  Adam moves every parameter by about lr * g / |g|, so for
+    # near-zero gradients the step is ill-conditioned: tolerance 2e-3 * lr absolute.
+    st, target, meta = to.from_golden(z)
+    opt = to.Adam(st.params(), meta["lr"])
+    for s in (1, 2):
+        to.grads(st, *args)
+        opt.step()
+        for name, p in zip(names, st.params()):
+            ref = z[f"s{s}/{name}"].reshape(p.shape)
+            np.testing.assert_allclose(p.detach().numpy(), ref, rtol=1e-5, atol=2e-3 * meta["lr"], err_msg=f"step {s} {name}")
