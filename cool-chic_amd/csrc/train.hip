@@ -1,0 +1,1295 @@
+// train.hip -- the encoder overfit step on the GPU: training forward, backward, gradient
+// clipping and Adam for a batch of independent frames (one network + latents each).
+//
+// Reference, enc/training/train.py:238-262 (one iteration):
+//   frame_encoder.forward (train mode)  coolchic.py:291-479, frame.py:175-183
+//     quantize            quantizer.py:16-232   (softround / noise / STE variants)
+//     ARM + Laplace rate  arm.py:227-370, coolchic.py:395-424
+//     Upsampling          upsampling.py:195-202, 322-335, 476-506 (train = kron-2D form,
+//                         mathematically the separable eval form computed here)
+//     Synthesis           synthesis.py:69-84, 264-277
+//     420 nearest + clamp yuv.py:275-299
+//   loss_function          loss.py (MSE + lmbda * rate_bpp)
+//   loss.backward(); clip_grad_norm_(params, 0.1); torch.optim.Adam.step()
+//
+// Kernels, in launch order (all frames of the batch in every launch, grid.y = frame):
+//   t_expand      trainable half kernels -> full symmetric kernels (upsampling.py:46-68)
+//   t_quant       y_hat = Q(gain * y) and dQ/dy; noise from a counter-based RNG (or given)
+//   t_arm<D,NH>   ARM forward + rate + full backward in one pass: 4 x 64 latent tile + causal
+//                 halo in LDS; context gradients accumulate in an LDS tile (ds_add) and are
+//                 flushed with one global atomic per tile position; weight gradients are
+//                 reduced per workgroup through LDS into a partial row (summed by t_colsum)
+//   (upsampling forward: the path-A level kernels, keeping every pyramid stack)
+//   t_head_fwd / t_sp_fwd   synthesis forward, intermediate 3-channel maps kept
+//   t_loss        train-mode output (420 nearest, clamp), MSE and its gradient
+//   t_sp_gpre / t_sp_bwd    3x3 layers backward (replicate-padding adjoint as a gather)
+//   t_head_bwd    1x1 head backward; weight gradients reduced through LDS
+//   t_ref_* / t_up_*        upsampling backward, one pyramid level at a time
+//   t_latgrad, t_sumsq, t_adam   dL/dy, global grad norm, clipped Adam update
+#include "fwd_common.h"
+
+using ccmi_fwd::cfloat_ptr;
+
+namespace {
+
+constexpr int kT = 256;
+constexpr int kMaxSp = 3;
+constexpr int kHeadT = 128;
+constexpr float kLn2 = 0.6931471805599453f;
+
+// Per-frame geometry and parameter offsets (same for every frame of a batch).
+struct Geo {
+    int L, N, H, W;
+    int h[CCMI_MAX_GRIDS], w[CCMI_MAX_GRIDS], off[CCMI_MAX_GRIDS];
+    int d, nh, P_arm;
+    int K, n_ups, hu, up_off;
+    int Kp, n_pre, hp, pre_off;
+    int syn_off, hid, r0, r1, w0, b0, w1, b1, P_head;
+    int n_sp, sp_w[kMaxSp], sp_b[kMaxSp], sp_res[kMaxSp], sp_relu[kMaxSp];
+    int P, kfull;
+};
+
+__device__ __forceinline__ int clampi(int v, int hi) { return v < 0 ? 0 : (v > hi ? hi : v); }
+
+__device__ __forceinline__ float block_sum(float v, float *red)
+{
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
+    const int wid = threadIdx.x >> 6, nw = blockDim.x >> 6;
+    __syncthreads();
+    if ((threadIdx.x & 63) == 0) red[wid] = v;
+    __syncthreads();
+    float s = 0.f;
+    for (int i = 0; i < nw; ++i) s += red[i];
+    return s;
+}
+
+// ------------------------------------------------------------------ parameters
+__global__ void t_expand(const float *__restrict__ th, int64_t ps, Geo g, float *__restrict__ kf)
+{
+    const int b = blockIdx.y, i = blockIdx.x * kT + threadIdx.x;
+    if (i >= g.kfull) return;
+    const float *p = th + (int64_t)b * ps;
+    float v;
+    if (i < g.n_ups * g.K) {
+        const int u = i / g.K, t = i - u * g.K;
+        v = p[g.up_off + u * g.hu + min(t, g.K - 1 - t)];
+    } else {
+        const int r = i - g.n_ups * g.K, u = r / g.Kp, t = r - u * g.Kp;
+        v = p[g.pre_off + u * g.hp + min(t, g.Kp - 1 - t)];
+    }
+    kf[(int64_t)b * g.kfull + i] = v;
+}
+
+// ------------------------------------------------------------------ quantizer
+__device__ __forceinline__ uint64_t mix64(uint64_t z)
+{
+    z += 0x9E3779B97F4A7C15ull;
+    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+    z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+    return z ^ (z >> 31);
+}
+__device__ __forceinline__ float unif(uint64_t r) { return ((float)(r >> 40) + 0.5f) * 5.9604644775390625e-08f; }
+
+struct SoftRound {
+    float t, inv; // inv = 1 / tanh(1 / (2t))
+    __device__ float f(float x) const
+    {
+        const float fx = floorf(x), d = x - fx - 0.5f;
+        return fx + 0.5f * tanhf(d / t) * inv + 0.5f;
+    }
+    __device__ float df(float x) const
+    {
+        const float fx = floorf(x), th = tanhf((x - fx - 0.5f) / t);
+        return 0.5f * (1.f - th * th) / t * inv;
+    }
+};
+
+__global__ void t_quant(const float *__restrict__ lat, int64_t ls, int N, float gain, int qt, int nz, float temp,
+                        float nprm, uint64_t seed, int step, const float *__restrict__ noise_in, float *__restrict__ yq,
+                        float *__restrict__ dq, float *__restrict__ gq)
+{
+    const int b = blockIdx.y, i = blockIdx.x * kT + threadIdx.x;
+    if (i >= N) return;
+    const int64_t li = (int64_t)b * ls + i, wi = (int64_t)b * N + i;
+    const float x = gain * lat[li];
+    float n = 0.f;
+    if (noise_in) {
+        n = noise_in[li];
+    } else if (nz != CCMI_NOISE_NONE) {
+        const uint64_t r = mix64(seed ^ mix64(((uint64_t)step << 40) ^ ((uint64_t)b << 32) ^ (uint64_t)i));
+        const float u1 = unif(r);
+        if (nz == CCMI_NOISE_KUMARASWAMY) { // generate_kumaraswamy_noise (quantizer.py:60-102)
+            const float a = nprm, bb = (exp2f(a) * (a - 1.f) + 1.f) / a;
+            n = powf(1.f - powf(1.f - u1, 1.f / bb), 1.f / a) - 0.5f;
+        } else { // gaussian: Box-Muller
+            const float u2 = unif(mix64(r + 0x632BE59BD9B4E019ull));
+            n = sqrtf(-2.f * logf(u1)) * cospif(2.f * u2) * nprm;
+        }
+    }
+    SoftRound s{temp, 1.f / tanhf(1.f / (2.f * temp))};
+    float y, d;
+    switch (qt) {
+    case CCMI_Q_NONE: y = x + n; d = 1.f; break;
+    case CCMI_Q_SOFTROUND_ALONE: y = s.f(x); d = s.df(x); break;
+    case CCMI_Q_SOFTROUND: {
+        const float u = s.f(x) + n;
+        y = s.f(u);
+        d = s.df(u) * s.df(x);
+        break;
+    }
+    case CCMI_Q_STE: y = rintf(x); d = s.df(x); break;
+    case CCMI_Q_TRUE_STE: y = rintf(x); d = 1.f; break;
+    default: y = rintf(x); d = 0.f; break; // hardround: torch.round has a zero gradient
+    }
+    yq[wi] = y;
+    dq[wi] = gain * d;
+    gq[wi] = 0.f;
+}
+
+// ------------------------------------------------------------------ ARM forward + backward
+constexpr int kATX = 64, kATY = 4, kAH = 4;
+constexpr int kALW = kATX + 2 * kAH, kALH = kATY + kAH;
+
+struct ArmTiles {
+    int n, tiles_x[CCMI_MAX_GRIDS], start[CCMI_MAX_GRIDS + 1];
+};
+
+template <int D>
+__device__ __forceinline__ void ctx_off(int i, int &dy, int &dx)
+{
+    constexpr signed char k8[8] = {13, 22, 30, 31, 32, 37, 38, 39};
+    constexpr signed char k16[16] = {13, 14, 20, 21, 22, 23, 24, 28, 29, 30, 31, 32, 33, 37, 38, 39};
+    constexpr signed char k24[24] = {4, 11, 12, 13, 14, 15, 19, 20, 21, 22, 23, 24, 25, 28, 29, 30, 31, 32, 33, 34,
+                                     36, 37, 38, 39};
+    constexpr signed char k32[32] = {2, 3, 4, 5, 10, 11, 12, 13, 14, 15, 16, 19, 20, 21, 22, 23, 24, 25, 26, 27,
+                                     28, 29, 30, 31, 32, 33, 34, 35, 36, 37, 38, 39};
+    const int k = D == 8 ? k8[i] : D == 16 ? k16[i] : D == 24 ? k24[i] : k32[i];
+    dy = k / 9 - 4;
+    dx = k % 9 - 4;
+}
+
+// Sum over the workgroup of g (R values) x a (D values) outer products and of g, written
+// as one partial row: [R][D] then [R].
+template <int R, int D>
+__device__ __forceinline__ void outer_reduce(const float (&gv)[R], const float (&av)[D], float *s_g, float *s_a,
+                                             float *__restrict__ row)
+{
+    const int t = threadIdx.x;
+#pragma unroll
+    for (int j = 0; j < R; ++j) s_g[t * (R + 1) + j] = gv[j];
+#pragma unroll
+    for (int i = 0; i < D; ++i) s_a[t * (D + 1) + i] = av[i];
+    __syncthreads();
+    for (int e = t; e < R * D + R; e += kT) {
+        float acc = 0.f;
+        if (e < R * D) {
+            const int j = e / D, i = e - j * D;
+            for (int k = 0; k < kT; ++k) acc = fmaf(s_g[k * (R + 1) + j], s_a[k * (D + 1) + i], acc);
+        } else {
+            const int j = e - R * D;
+            for (int k = 0; k < kT; ++k) acc += s_g[k * (R + 1) + j];
+        }
+        row[e] = acc;
+    }
+    __syncthreads();
+}
+
+template <int D, int NH>
+__global__ __launch_bounds__(kT) void t_arm(const float *__restrict__ yq, Geo g, ArmTiles at, const float *__restrict__ th,
+                                            int64_t ps, float lam_px, float *__restrict__ gq,
+                                            float *__restrict__ part, int nblk, float *__restrict__ acc4)
+{
+    __shared__ float s_y[kALH][kALW];
+    __shared__ float s_gy[kALH][kALW];
+    __shared__ float s_g[kT * (D + 1)];
+    __shared__ float s_a[kT * (D + 1)];
+    __shared__ float s_red[8];
+
+    const int b = blockIdx.y, t = blockIdx.x;
+    int l = 0;
+#pragma unroll
+    for (int k = 1; k < CCMI_MAX_GRIDS; ++k)
+        if (k < at.n && t >= at.start[k]) l = k;
+    const int lt = t - at.start[l];
+    const int H = g.h[l], W = g.w[l];
+    const int y0 = (lt / at.tiles_x[l]) * kATY, x0 = (lt % at.tiles_x[l]) * kATX;
+    const float *src = yq + (int64_t)b * g.N + g.off[l];
+    float *gdst = gq + (int64_t)b * g.N + g.off[l];
+    for (int i = threadIdx.x; i < kALH * kALW; i += kT) {
+        const int r = i / kALW, c = i - r * kALW;
+        const int y = y0 - kAH + r, x = x0 - kAH + c;
+        s_y[r][c] = (y >= 0 && y < H && x >= 0 && x < W) ? src[y * W + x] : 0.f;
+        s_gy[r][c] = 0.f;
+    }
+    __syncthreads();
+
+    const int cx = threadIdx.x % kATX, cy = threadIdx.x / kATX;
+    const bool valid = (y0 + cy) < H && (x0 + cx) < W;
+    const cfloat_ptr P = (cfloat_ptr)(size_t)(th + (int64_t)b * ps);
+
+    float xs[NH + 1][D];
+#pragma unroll
+    for (int i = 0; i < D; ++i) {
+        int dy, dx;
+        ctx_off<D>(i, dy, dx);
+        xs[0][i] = s_y[cy + kAH + dy][cx + kAH + dx];
+    }
+#pragma unroll
+    for (int L = 0; L < NH; ++L) {
+        const cfloat_ptr Wl = P + L * (D * D + D);
+#pragma unroll
+        for (int j = 0; j < D; ++j) {
+            float z = Wl[D * D + j];
+#pragma unroll
+            for (int i = 0; i < D; ++i) z = fmaf(Wl[j * D + i], xs[L][i], z);
+            z += xs[L][j];
+            xs[L + 1][j] = fmaxf(z, 0.f);
+        }
+    }
+    const cfloat_ptr Wo = P + NH * (D * D + D);
+    float mu = Wo[2 * D], ls = Wo[2 * D + 1];
+#pragma unroll
+    for (int i = 0; i < D; ++i) {
+        mu = fmaf(Wo[i], xs[NH][i], mu);
+        ls = fmaf(Wo[D + i], xs[NH][i], ls);
+    }
+    // scale = exp(clamp(ls - 4, -4.6, 5)) (arm.py:262-266); rate (coolchic.py:419-424)
+    const float l4 = ls - 4.f, sig = expf(fminf(fmaxf(l4, -4.6f), 5.0f));
+    const float q = s_y[cy + kAH][cx + kAH];
+    const float s1 = q + 0.5f - mu, s2 = q - 0.5f - mu;
+    const float sg1 = s1 > 0.f ? 1.f : (s1 < 0.f ? -1.f : 0.f), sg2 = s2 > 0.f ? 1.f : (s2 < 0.f ? -1.f : 0.f);
+    const float F1 = 0.5f - 0.5f * sg1 * expm1f(-fabsf(s1) / sig), F2 = 0.5f - 0.5f * sg2 * expm1f(-fabsf(s2) / sig);
+    const float Pr = F1 - F2;
+    float rate = 0.f, g_q = 0.f, g_mu = 0.f, g_ls = 0.f;
+    if (valid) {
+        rate = -log2f(fmaxf(Pr, 1.52587890625e-05f));
+        if (Pr >= 1.52587890625e-05f) { // clamp_min passes the gradient where P >= 2^-16
+            const float dLdP = -lam_px / (Pr * kLn2);
+            const float e1 = expf(-fabsf(s1) / sig), e2 = expf(-fabsf(s2) / sig);
+            // torch autograd of 0.5 - 0.5 sign(s) expm1(-|s|/sig): d/ds = 0.5 sign(s)^2 e / sig
+            const float Fs1 = 0.5f * sg1 * sg1 * e1 / sig, Fs2 = 0.5f * sg2 * sg2 * e2 / sig;
+            const float Fg1 = -0.5f * sg1 * e1 * fabsf(s1) / (sig * sig), Fg2 = -0.5f * sg2 * e2 * fabsf(s2) / (sig * sig);
+            g_q = dLdP * (Fs1 - Fs2);
+            g_mu = -g_q;
+            const float g_sig = dLdP * (Fg1 - Fg2);
+            g_ls = (l4 >= -4.6f && l4 <= 5.0f) ? g_sig * sig : 0.f;
+        }
+    }
+    // ---- backward through the MLP; weight-gradient partial rows per workgroup
+    float *row = part + ((int64_t)b * nblk + t) * g.P_arm;
+    float gx[D];
+    {
+        const float go[2] = {g_mu, g_ls};
+#pragma unroll
+        for (int i = 0; i < D; ++i) gx[i] = Wo[i] * g_mu + Wo[D + i] * g_ls;
+        outer_reduce<2, D>(go, xs[NH], s_g, s_a, row + NH * (D * D + D));
+    }
+#pragma unroll
+    for (int L = NH - 1; L >= 0; --L) {
+        const cfloat_ptr Wl = P + L * (D * D + D);
+        float gz[D];
+#pragma unroll
+        for (int j = 0; j < D; ++j) gz[j] = xs[L + 1][j] > 0.f ? gx[j] : 0.f;
+        outer_reduce<D, D>(gz, xs[L], s_g, s_a, row + L * (D * D + D));
+#pragma unroll
+        for (int i = 0; i < D; ++i) {
+            float a = gz[i]; // residual
+#pragma unroll
+            for (int j = 0; j < D; ++j) a = fmaf(Wl[j * D + i], gz[j], a);
+            gx[i] = a;
+        }
+    }
+    // ---- context gradients -> LDS tile, then one global atomic per touched position
+    if (valid) {
+#pragma unroll
+        for (int i = 0; i < D; ++i) {
+            int dy, dx;
+            ctx_off<D>(i, dy, dx);
+            atomicAdd(&s_gy[cy + kAH + dy][cx + kAH + dx], gx[i]);
+        }
+        atomicAdd(&s_gy[cy + kAH][cx + kAH], g_q);
+    }
+    const float rsum = block_sum(rate, s_red);
+    __syncthreads();
+    for (int i = threadIdx.x; i < kALH * kALW; i += kT) {
+        const int r = i / kALW, c = i - r * kALW;
+        const int y = y0 - kAH + r, x = x0 - kAH + c;
+        const float v = s_gy[r][c];
+        if (y >= 0 && y < H && x >= 0 && x < W && v != 0.f) atomicAdd(&gdst[y * W + x], v);
+    }
+    if (threadIdx.x == 0) atomicAdd(&acc4[b * 4 + 1], rsum);
+}
+
+// Column sums of per-workgroup partial rows: dst[b][col] += sum_r part[b][r][col].
+__global__ void t_colsum(const float *__restrict__ part, int nrows, int ncols, float *__restrict__ dst, int64_t dstride)
+{
+    __shared__ float s[4][64];
+    const int b = blockIdx.z, col = blockIdx.x * 64 + threadIdx.x;
+    const int r0 = blockIdx.y * 256;
+    float acc = 0.f;
+    if (col < ncols) {
+        const float *p = part + (int64_t)b * nrows * ncols;
+        for (int r = r0 + threadIdx.y; r < min(nrows, r0 + 256); r += 4) acc += p[(int64_t)r * ncols + col];
+    }
+    s[threadIdx.y][threadIdx.x] = acc;
+    __syncthreads();
+    if (threadIdx.y == 0 && col < ncols)
+        atomicAdd(&dst[(int64_t)b * dstride + col], s[0][threadIdx.x] + s[1][threadIdx.x] + s[2][threadIdx.x] + s[3][threadIdx.x]);
+}
+
+// ------------------------------------------------------------------ synthesis
+template <int CIN>
+__global__ __launch_bounds__(kT) void t_head_fwd(const float *__restrict__ dense, Geo g, const float *__restrict__ th,
+                                                 int64_t ps, float *__restrict__ z0)
+{
+    const int b = blockIdx.y;
+    const int64_t npx = (int64_t)g.H * g.W, p = (int64_t)blockIdx.x * kT + threadIdx.x;
+    if (p >= npx) return;
+    const cfloat_ptr P = (cfloat_ptr)(size_t)(th + (int64_t)b * ps);
+    const float *x = dense + (int64_t)b * CIN * npx + p;
+    float xv[CIN];
+#pragma unroll
+    for (int i = 0; i < CIN; ++i) xv[i] = x[i * npx];
+    float o0 = P[g.b1], o1 = P[g.b1 + 1], o2 = P[g.b1 + 2];
+    for (int j = 0; j < g.hid; ++j) {
+        float h = P[g.b0 + j];
+#pragma unroll
+        for (int i = 0; i < CIN; ++i) h = fmaf(P[g.w0 + j * CIN + i], xv[i], h);
+        if (g.r0) h = fmaxf(h, 0.f);
+        o0 = fmaf(P[g.w1 + j], h, o0);
+        o1 = fmaf(P[g.w1 + g.hid + j], h, o1);
+        o2 = fmaf(P[g.w1 + 2 * g.hid + j], h, o2);
+    }
+    if (g.r1) {
+        o0 = fmaxf(o0, 0.f);
+        o1 = fmaxf(o1, 0.f);
+        o2 = fmaxf(o2, 0.f);
+    }
+    float *z = z0 + (int64_t)b * 3 * npx + p;
+    z[0] = o0;
+    z[npx] = o1;
+    z[2 * npx] = o2;
+}
+
+// 3x3, 3 -> 3, replicate padding (synthesis.py:69-84), optional residual / ReLU.
+__global__ __launch_bounds__(kT) void t_sp_fwd(const float *__restrict__ in, Geo g, const float *__restrict__ th, int64_t ps,
+                                               int wo, int bo, int res, int relu, float *__restrict__ out)
+{
+    const int b = blockIdx.y;
+    const int64_t npx = (int64_t)g.H * g.W, p = (int64_t)blockIdx.x * kT + threadIdx.x;
+    if (p >= npx) return;
+    const int py = (int)(p / g.W), px = (int)(p - (int64_t)py * g.W);
+    const cfloat_ptr P = (cfloat_ptr)(size_t)(th + (int64_t)b * ps);
+    const float *x = in + (int64_t)b * 3 * npx;
+    float v[3][9];
+#pragma unroll
+    for (int i = 0; i < 3; ++i)
+#pragma unroll
+        for (int k = 0; k < 9; ++k) {
+            const int yy = clampi(py + k / 3 - 1, g.H - 1), xx = clampi(px + k % 3 - 1, g.W - 1);
+            v[i][k] = x[i * npx + (int64_t)yy * g.W + xx];
+        }
+    float *o = out + (int64_t)b * 3 * npx + p;
+#pragma unroll
+    for (int c = 0; c < 3; ++c) {
+        float a = P[bo + c];
+#pragma unroll
+        for (int i = 0; i < 3; ++i)
+#pragma unroll
+            for (int k = 0; k < 9; ++k) a = fmaf(P[wo + (c * 3 + i) * 9 + k], v[i][k], a);
+        if (res) a += v[c][4];
+        if (relu) a = fmaxf(a, 0.f);
+        o[c * npx] = a;
+    }
+}
+
+// Train-mode frame output + MSE (frame.py:175-183, loss.py _compute_mse): gradient of the
+// MSE w.r.t. the raw synthesis output; sum of squared errors into acc4[b][0].
+__global__ __launch_bounds__(kT) void t_loss(const float *__restrict__ raw, Geo g, const float *__restrict__ tgt,
+                                             int64_t tstride, int yuv420, float *__restrict__ graw, float *__restrict__ acc4)
+{
+    __shared__ float s_red[8];
+    const int b = blockIdx.y;
+    const int64_t npx = (int64_t)g.H * g.W, p = (int64_t)blockIdx.x * kT + threadIdx.x;
+    const int h2 = g.H / 2, w2 = g.W / 2;
+    const float total = yuv420 ? (float)(npx + 2 * (int64_t)h2 * w2) : (float)(3 * npx);
+    const float k2 = 2.f / total;
+    float se = 0.f;
+    if (p < npx) {
+        const int py = (int)(p / g.W), px = (int)(p - (int64_t)py * g.W);
+        const float *o = raw + (int64_t)b * 3 * npx + p;
+        const float *T = tgt + (int64_t)b * tstride;
+        float *go = graw + (int64_t)b * 3 * npx + p;
+#pragma unroll
+        for (int c = 0; c < 3; ++c) {
+            bool used = true;
+            int64_t ti = c * npx + p;
+            if (yuv420 && c > 0) {
+                used = (py % 2 == 0) && (px % 2 == 0) && (py / 2) < h2 && (px / 2) < w2;
+                ti = npx + (int64_t)(c - 1) * h2 * w2 + (int64_t)(py / 2) * w2 + px / 2;
+            }
+            float gv = 0.f;
+            if (used) {
+                const float v = o[c * npx], vc = fminf(fmaxf(v, 0.f), 1.f), d = vc - T[ti];
+                se += d * d;
+                gv = (v >= 0.f && v <= 1.f) ? k2 * d : 0.f;
+            }
+            go[c * npx] = gv;
+        }
+    }
+    const float s = block_sum(se, s_red);
+    if (threadIdx.x == 0) atomicAdd(&acc4[b * 4 + 0], s);
+}
+
+// g_pre = g_out * relu'(out), in place.
+__global__ void t_sp_gpre(float *__restrict__ gout, const float *__restrict__ out, int64_t n)
+{
+    const int64_t i = (int64_t)blockIdx.x * kT + threadIdx.x;
+    if (i < n && out[i] <= 0.f) gout[i] = 0.f;
+}
+
+// Replicate-padding adjoint along one axis: output positions q whose tap offset dd reads
+// input position p (clamp(q + dd) == p): at most two (borders), returned as [lo, hi].
+__device__ __forceinline__ void qrange(int p, int dd, int n, int &lo, int &hi)
+{
+    if (n == 1) {
+        lo = 0;
+        hi = 0;
+    } else if (p == 0) {
+        lo = 0;
+        hi = min(n - 1, -dd);
+    } else if (p == n - 1) {
+        lo = max(0, n - 1 - dd);
+        hi = n - 1;
+    } else {
+        lo = hi = p - dd;
+        if (lo < 0 || lo >= n) {
+            lo = 1;
+            hi = 0;
+        }
+    }
+}
+
+// 3x3 layer backward: g_in (gather) and weight / bias gradients (block reduction + atomics).
+__global__ __launch_bounds__(kT) void t_sp_bwd(const float *__restrict__ gpre, const float *__restrict__ in, Geo g,
+                                               const float *__restrict__ th, int64_t ps, int wo, int bo, int res,
+                                               float *__restrict__ gin, float *__restrict__ gth, int64_t gstride)
+{
+    __shared__ float s_red[4][84];
+    const int b = blockIdx.y;
+    const int64_t npx = (int64_t)g.H * g.W;
+    const cfloat_ptr P = (cfloat_ptr)(size_t)(th + (int64_t)b * ps);
+    const float *G = gpre + (int64_t)b * 3 * npx;
+    const float *X = in + (int64_t)b * 3 * npx;
+    float acc[84];
+#pragma unroll
+    for (int e = 0; e < 84; ++e) acc[e] = 0.f;
+    for (int64_t p = (int64_t)blockIdx.x * kT + threadIdx.x; p < npx; p += (int64_t)gridDim.x * kT) {
+        const int py = (int)(p / g.W), px = (int)(p - (int64_t)py * g.W);
+        // weight gradients at output q = p
+        float gp[3];
+#pragma unroll
+        for (int c = 0; c < 3; ++c) gp[c] = G[c * npx + p];
+#pragma unroll
+        for (int k = 0; k < 9; ++k) {
+            const int yy = clampi(py + k / 3 - 1, g.H - 1), xx = clampi(px + k % 3 - 1, g.W - 1);
+#pragma unroll
+            for (int i = 0; i < 3; ++i) {
+                const float xv = X[i * npx + (int64_t)yy * g.W + xx];
+#pragma unroll
+                for (int c = 0; c < 3; ++c) acc[(c * 3 + i) * 9 + k] = fmaf(gp[c], xv, acc[(c * 3 + i) * 9 + k]);
+            }
+        }
+#pragma unroll
+        for (int c = 0; c < 3; ++c) acc[81 + c] += gp[c];
+        // input gradient at p: sum over (q, tap) with clamp(q + tap - 1) == p
+        float gi[3] = {0.f, 0.f, 0.f};
+        for (int ky = 0; ky < 3; ++ky) {
+            int qy0, qy1;
+            qrange(py, ky - 1, g.H, qy0, qy1);
+            for (int qy = qy0; qy <= qy1; ++qy)
+                for (int kx = 0; kx < 3; ++kx) {
+                    int qx0, qx1;
+                    qrange(px, kx - 1, g.W, qx0, qx1);
+                    for (int qx = qx0; qx <= qx1; ++qx) {
+                        const int64_t q = (int64_t)qy * g.W + qx;
+#pragma unroll
+                        for (int c = 0; c < 3; ++c) {
+                            const float gq = G[c * npx + q];
+#pragma unroll
+                            for (int i = 0; i < 3; ++i) gi[i] = fmaf(P[wo + (c * 3 + i) * 9 + ky * 3 + kx], gq, gi[i]);
+                        }
+                    }
+                }
+        }
+        float *o = gin + (int64_t)b * 3 * npx + p;
+#pragma unroll
+        for (int i = 0; i < 3; ++i) o[i * npx] = gi[i] + (res ? gp[i] : 0.f);
+    }
+    // block reduction of the 84 weight / bias gradients
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+#pragma unroll
+    for (int e = 0; e < 84; ++e) {
+        float v = acc[e];
+        for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
+        if (lane == 0) s_red[wid][e] = v;
+    }
+    __syncthreads();
+    if (threadIdx.x < 84) {
+        const int e = threadIdx.x;
+        const float v = s_red[0][e] + s_red[1][e] + s_red[2][e] + s_red[3][e];
+        float *dst = gth + (int64_t)b * gstride;
+        atomicAdd(&dst[e < 81 ? wo + e : bo + (e - 81)], v);
+    }
+}
+
+// 1x1 head backward: g_dense, and the weight gradients as partial rows
+// [W0 (hid x CIN), b0 (hid), W1 (3 x hid), b1 (3)] per workgroup of kHeadT pixels.
+template <int CIN>
+__global__ __launch_bounds__(kHeadT) void t_head_bwd(const float *__restrict__ dense, const float *__restrict__ gz0, Geo g,
+                                                     const float *__restrict__ th, int64_t ps, float *__restrict__ gdense,
+                                                     float *__restrict__ part, int nblk)
+{
+    extern __shared__ float s_mem[];
+    const int b = blockIdx.y, t = threadIdx.x;
+    const int hid = g.hid;
+    const int64_t npx = (int64_t)g.H * g.W, p = (int64_t)blockIdx.x * kHeadT + t;
+    const bool valid = p < npx;
+    const cfloat_ptr P = (cfloat_ptr)(size_t)(th + (int64_t)b * ps);
+    float xv[CIN], h[64], gp1[3];
+    const float *x = dense + (int64_t)b * CIN * npx + p;
+#pragma unroll
+    for (int i = 0; i < CIN; ++i) xv[i] = valid ? x[i * npx] : 0.f;
+    float o0 = P[g.b1], o1 = P[g.b1 + 1], o2 = P[g.b1 + 2];
+#pragma unroll
+    for (int j = 0; j < 64; ++j) {
+        if (j < hid) {
+            float a = P[g.b0 + j];
+#pragma unroll
+            for (int i = 0; i < CIN; ++i) a = fmaf(P[g.w0 + j * CIN + i], xv[i], a);
+            if (g.r0) a = fmaxf(a, 0.f);
+            h[j] = a;
+            o0 = fmaf(P[g.w1 + j], a, o0);
+            o1 = fmaf(P[g.w1 + hid + j], a, o1);
+            o2 = fmaf(P[g.w1 + 2 * hid + j], a, o2);
+        } else {
+            h[j] = 0.f;
+        }
+    }
+    {
+        const float *G = gz0 + (int64_t)b * 3 * npx + p;
+        gp1[0] = valid ? G[0] : 0.f;
+        gp1[1] = valid ? G[npx] : 0.f;
+        gp1[2] = valid ? G[2 * npx] : 0.f;
+        if (g.r1) {
+            if (o0 <= 0.f) gp1[0] = 0.f;
+            if (o1 <= 0.f) gp1[1] = 0.f;
+            if (o2 <= 0.f) gp1[2] = 0.f;
+        }
+    }
+    float *row = part + ((int64_t)b * nblk + blockIdx.x) * g.P_head;
+    const int ph = hid + 1;
+    // phase A: W1 (3 x hid), b1
+    float *s_h = s_mem, *s_gp = s_mem + kHeadT * ph;
+#pragma unroll
+    for (int j = 0; j < 64; ++j)
+        if (j < hid) s_h[t * ph + j] = h[j];
+    s_gp[t * 4 + 0] = gp1[0];
+    s_gp[t * 4 + 1] = gp1[1];
+    s_gp[t * 4 + 2] = gp1[2];
+    __syncthreads();
+    const int wA = g.w1 - g.w0;
+    for (int e = t; e < 3 * hid + 3; e += kHeadT) {
+        float a = 0.f;
+        if (e < 3 * hid) {
+            const int k = e / hid, j = e - k * hid;
+            for (int r = 0; r < kHeadT; ++r) a = fmaf(s_gp[r * 4 + k], s_h[r * ph + j], a);
+        } else {
+            for (int r = 0; r < kHeadT; ++r) a += s_gp[r * 4 + (e - 3 * hid)];
+        }
+        row[wA + e] = a;
+    }
+    __syncthreads();
+    // g_h, g_x
+    float gxv[CIN];
+#pragma unroll
+    for (int i = 0; i < CIN; ++i) gxv[i] = 0.f;
+#pragma unroll
+    for (int j = 0; j < 64; ++j) {
+        if (j < hid) {
+            float gh = P[g.w1 + j] * gp1[0] + P[g.w1 + hid + j] * gp1[1] + P[g.w1 + 2 * hid + j] * gp1[2];
+            if (g.r0 && h[j] <= 0.f) gh = 0.f;
+            h[j] = gh;
+#pragma unroll
+            for (int i = 0; i < CIN; ++i) gxv[i] = fmaf(P[g.w0 + j * CIN + i], gh, gxv[i]);
+        }
+    }
+    if (valid) {
+        float *gd = gdense + (int64_t)b * CIN * npx + p;
+#pragma unroll
+        for (int i = 0; i < CIN; ++i) gd[i * npx] = gxv[i];
+    }
+    // phase B: W0 (hid x CIN), b0
+    float *s_gh = s_mem, *s_x = s_mem + kHeadT * ph;
+#pragma unroll
+    for (int j = 0; j < 64; ++j)
+        if (j < hid) s_gh[t * ph + j] = h[j];
+#pragma unroll
+    for (int i = 0; i < CIN; ++i) s_x[t * (CIN + 1) + i] = xv[i];
+    __syncthreads();
+    for (int e = t; e < hid * CIN + hid; e += kHeadT) {
+        float a = 0.f;
+        if (e < hid * CIN) {
+            const int j = e / CIN, i = e - j * CIN;
+            for (int r = 0; r < kHeadT; ++r) a = fmaf(s_gh[r * ph + j], s_x[r * (CIN + 1) + i], a);
+        } else {
+            for (int r = 0; r < kHeadT; ++r) a += s_gh[r * ph + (e - hid * CIN)];
+        }
+        row[e] = a;
+    }
+}
+
+// ------------------------------------------------------------------ upsampling backward
+// Polyphase taps of the 2x transposed conv: destination 2j + a reads source clamp(j + d)
+// with tap a + K/2 - 1 - 2d (fwd_ups.hip).
+struct UpLevel {
+    int C, hs, ws, hd, wd, K, d_lo, d_hi, sidx; // sidx: kernel slot (step % n_ups)
+};
+
+__device__ __forceinline__ float wave_block_sum_atomic(float v, float *dst)
+{
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
+    if ((threadIdx.x & 63) == 0 && v != 0.f) atomicAdd(dst, v);
+    return v;
+}
+
+// refine, horizontal pass: U[r][x] = sum_k w[k] X[r][x + k - P] (zero padding)
+__global__ void t_ref_u(const float *__restrict__ X, int64_t xs, int h, int w, const float *__restrict__ kf, int kstride,
+                        int koff, int Kp, float *__restrict__ U, int64_t us)
+{
+    const int b = blockIdx.y;
+    const int64_t n = (int64_t)h * w, i = (int64_t)blockIdx.x * kT + threadIdx.x;
+    if (i >= n) return;
+    const int r = (int)(i / w), x = (int)(i - (int64_t)r * w), P = Kp / 2;
+    const float *wk = kf + (int64_t)b * kstride + koff, *src = X + (int64_t)b * xs + (int64_t)r * w;
+    float a = 0.f;
+    for (int k = 0; k < Kp; ++k) {
+        const int xx = x + k - P;
+        if (xx >= 0 && xx < w) a = fmaf(wk[k], src[xx], a);
+    }
+    U[(int64_t)b * us + i] = a;
+}
+
+// refine, vertical adjoint: GU[r][x] = sum_k w[k] GY[r - k + P][x]; dwV[k] = sum GY[y][x] U[y + k - P][x]
+__global__ __launch_bounds__(kT) void t_ref_gu(const float *__restrict__ GY, int64_t gys, const float *__restrict__ U,
+                                               int64_t us, int h, int w, const float *__restrict__ kf, int kstride,
+                                               int koff, int Kp, float *__restrict__ GU, float *__restrict__ gth,
+                                               int64_t gstride, int hoff)
+{
+    const int b = blockIdx.y;
+    const int64_t n = (int64_t)h * w, i = (int64_t)blockIdx.x * kT + threadIdx.x;
+    const int P = Kp / 2;
+    const float *wk = kf + (int64_t)b * kstride + koff;
+    float dw[16];
+    for (int k = 0; k < 16; ++k) dw[k] = 0.f;
+    if (i < n) {
+        const int r = (int)(i / w), x = (int)(i - (int64_t)r * w);
+        const float *gy = GY + (int64_t)b * gys, *u = U + (int64_t)b * us;
+        float a = 0.f;
+        const float gyv = gy[i];
+        for (int k = 0; k < Kp; ++k) {
+            const int rr = r - k + P;
+            if (rr >= 0 && rr < h) a = fmaf(wk[k], gy[(int64_t)rr * w + x], a);
+            const int ru = r + k - P;
+            if (ru >= 0 && ru < h) dw[k] = gyv * u[(int64_t)ru * w + x];
+        }
+        GU[(int64_t)b * us + i] = a;
+    }
+    float *dst = gth + (int64_t)b * gstride + hoff;
+    for (int k = 0; k < Kp; ++k) wave_block_sum_atomic(dw[k], &dst[min(k, Kp - 1 - k)]);
+}
+
+// refine, horizontal adjoint + residual: g_x = sum_k w[k] GU[r][m - k + P] + GY; dwH[k] = sum GU[r][x] X[r][x + k - P]
+__global__ __launch_bounds__(kT) void t_ref_gx(const float *__restrict__ GU, int64_t us, const float *__restrict__ GY,
+                                               int64_t gys, const float *__restrict__ X, int64_t xs, int h, int w,
+                                               const float *__restrict__ kf, int kstride, int koff, int Kp,
+                                               float *__restrict__ GX, int64_t gxs, float *__restrict__ gth,
+                                               int64_t gstride, int hoff)
+{
+    const int b = blockIdx.y;
+    const int64_t n = (int64_t)h * w, i = (int64_t)blockIdx.x * kT + threadIdx.x;
+    const int P = Kp / 2;
+    const float *wk = kf + (int64_t)b * kstride + koff;
+    float dw[16];
+    for (int k = 0; k < 16; ++k) dw[k] = 0.f;
+    if (i < n) {
+        const int r = (int)(i / w), m = (int)(i - (int64_t)r * w);
+        const float *gu = GU + (int64_t)b * us + (int64_t)r * w, *x = X + (int64_t)b * xs + (int64_t)r * w;
+        float a = GY[(int64_t)b * gys + i];
+        const float guv = gu[m];
+        for (int k = 0; k < Kp; ++k) {
+            const int mm = m - k + P;
+            if (mm >= 0 && mm < w) a = fmaf(wk[k], gu[mm], a);
+            const int xx = m + k - P;
+            if (xx >= 0 && xx < w) dw[k] = guv * x[xx];
+        }
+        GX[(int64_t)b * gxs + i] += a;
+    }
+    float *dst = gth + (int64_t)b * gstride + hoff;
+    for (int k = 0; k < Kp; ++k) wave_block_sum_atomic(dw[k], &dst[min(k, Kp - 1 - k)]);
+}
+
+__device__ __forceinline__ int up_tap(int a, int d, int K) { return a + K / 2 - 1 - 2 * d; }
+
+// upsample, horizontal pass: U[c][r][xd] = sum_d w[tap] S[c][r][clamp(xd/2 + d)]
+__global__ void t_up_u(const float *__restrict__ S, int64_t ss, UpLevel A, const float *__restrict__ kf, int kstride,
+                       int koff, float *__restrict__ U, int64_t us)
+{
+    const int b = blockIdx.y;
+    const int64_t n = (int64_t)A.C * A.hs * A.wd, i = (int64_t)blockIdx.x * kT + threadIdx.x;
+    if (i >= n) return;
+    const int xd = (int)(i % A.wd);
+    const int64_t cr = i / A.wd; // c * hs + r
+    const float *wk = kf + (int64_t)b * kstride + koff, *src = S + (int64_t)b * ss + cr * A.ws;
+    const int j = xd >> 1, a = xd & 1;
+    float acc = 0.f;
+    for (int d = A.d_lo; d <= A.d_hi; ++d) {
+        const int t = up_tap(a, d, A.K);
+        if (t >= 0 && t < A.K) acc = fmaf(wk[t], src[clampi(j + d, A.ws - 1)], acc);
+    }
+    U[(int64_t)b * us + i] = acc;
+}
+
+// upsample, vertical adjoint: GU[c][r][xd] = sum over (yd = 2j + a, d) with clamp(j + d) == r
+__global__ void t_up_gu(const float *__restrict__ GY, int64_t gys, UpLevel A, const float *__restrict__ kf, int kstride,
+                        int koff, float *__restrict__ GU, int64_t us)
+{
+    const int b = blockIdx.y;
+    const int64_t n = (int64_t)A.C * A.hs * A.wd, i = (int64_t)blockIdx.x * kT + threadIdx.x;
+    if (i >= n) return;
+    const int xd = (int)(i % A.wd);
+    const int64_t cr = i / A.wd;
+    const int c = (int)(cr / A.hs), r = (int)(cr - (int64_t)c * A.hs);
+    const float *wk = kf + (int64_t)b * kstride + koff;
+    const float *gy = GY + (int64_t)b * gys + (int64_t)(c + 1) * A.hd * A.wd + xd; // channel c+1 of the dest stack
+    const int nj = (A.hd + 1) >> 1;
+    float acc = 0.f;
+    for (int d = A.d_lo; d <= A.d_hi; ++d) {
+        int jlo = r == 0 ? 0 : r - d, jhi = r == A.hs - 1 ? nj - 1 : r - d;
+        jlo = max(jlo, 0);
+        jhi = min(jhi, nj - 1);
+        for (int j = jlo; j <= jhi; ++j) {
+            if (clampi(j + d, A.hs - 1) != r) continue;
+            for (int a = 0; a < 2; ++a) {
+                const int yd = 2 * j + a, t = up_tap(a, d, A.K);
+                if (yd < A.hd && t >= 0 && t < A.K) acc = fmaf(wk[t], gy[(int64_t)yd * A.wd], acc);
+            }
+        }
+    }
+    GU[(int64_t)b * us + i] = acc;
+}
+
+// upsample, vertical kernel gradient: over destination pixels (c, yd, xd)
+__global__ __launch_bounds__(kT) void t_up_dwv(const float *__restrict__ GY, int64_t gys, const float *__restrict__ U,
+                                               int64_t us, UpLevel A, float *__restrict__ gth, int64_t gstride, int hoff)
+{
+    const int b = blockIdx.y;
+    const int64_t n = (int64_t)A.C * A.hd * A.wd, i = (int64_t)blockIdx.x * kT + threadIdx.x;
+    float dw[16];
+    for (int k = 0; k < 16; ++k) dw[k] = 0.f;
+    if (i < n) {
+        const int xd = (int)(i % A.wd);
+        const int64_t cy = i / A.wd;
+        const int c = (int)(cy / A.hd), yd = (int)(cy - (int64_t)c * A.hd);
+        const float gv = GY[(int64_t)b * gys + (int64_t)(c + 1) * A.hd * A.wd + (int64_t)yd * A.wd + xd];
+        const float *u = U + (int64_t)b * us + (int64_t)c * A.hs * A.wd + xd;
+        const int j = yd >> 1, a = yd & 1;
+        for (int d = A.d_lo; d <= A.d_hi; ++d) {
+            const int t = up_tap(a, d, A.K);
+            if (t >= 0 && t < A.K) dw[t] = gv * u[(int64_t)clampi(j + d, A.hs - 1) * A.wd];
+        }
+    }
+    float *dst = gth + (int64_t)b * gstride + hoff;
+    for (int k = 0; k < A.K; ++k) wave_block_sum_atomic(dw[k], &dst[min(k, A.K - 1 - k)]);
+}
+
+// upsample, horizontal adjoint: GS[c][r][m] (+= into the source gradient)
+__global__ void t_up_gs(const float *__restrict__ GU, int64_t us, UpLevel A, const float *__restrict__ kf, int kstride,
+                        int koff, float *__restrict__ GS, int64_t gss, int accumulate)
+{
+    const int b = blockIdx.y;
+    const int64_t n = (int64_t)A.C * A.hs * A.ws, i = (int64_t)blockIdx.x * kT + threadIdx.x;
+    if (i >= n) return;
+    const int m = (int)(i % A.ws);
+    const int64_t cr = i / A.ws;
+    const float *wk = kf + (int64_t)b * kstride + koff;
+    const float *gu = GU + (int64_t)b * us + cr * A.wd;
+    const int nj = (A.wd + 1) >> 1;
+    float acc = 0.f;
+    for (int d = A.d_lo; d <= A.d_hi; ++d) {
+        int jlo = m == 0 ? 0 : m - d, jhi = m == A.ws - 1 ? nj - 1 : m - d;
+        jlo = max(jlo, 0);
+        jhi = min(jhi, nj - 1);
+        for (int j = jlo; j <= jhi; ++j) {
+            if (clampi(j + d, A.ws - 1) != m) continue;
+            for (int a = 0; a < 2; ++a) {
+                const int xd = 2 * j + a, t = up_tap(a, d, A.K);
+                if (xd < A.wd && t >= 0 && t < A.K) acc = fmaf(wk[t], gu[xd], acc);
+            }
+        }
+    }
+    float *o = GS + (int64_t)b * gss + i;
+    *o = accumulate ? *o + acc : acc;
+}
+
+// upsample, horizontal kernel gradient: over (c, r, xd)
+__global__ __launch_bounds__(kT) void t_up_dwh(const float *__restrict__ GU, int64_t us, const float *__restrict__ S,
+                                               int64_t ss, UpLevel A, float *__restrict__ gth, int64_t gstride, int hoff)
+{
+    const int b = blockIdx.y;
+    const int64_t n = (int64_t)A.C * A.hs * A.wd, i = (int64_t)blockIdx.x * kT + threadIdx.x;
+    float dw[16];
+    for (int k = 0; k < 16; ++k) dw[k] = 0.f;
+    if (i < n) {
+        const int xd = (int)(i % A.wd);
+        const int64_t cr = i / A.wd;
+        const float gv = GU[(int64_t)b * us + i];
+        const float *src = S + (int64_t)b * ss + cr * A.ws;
+        const int j = xd >> 1, a = xd & 1;
+        for (int d = A.d_lo; d <= A.d_hi; ++d) {
+            const int t = up_tap(a, d, A.K);
+            if (t >= 0 && t < A.K) dw[t] = gv * src[clampi(j + d, A.ws - 1)];
+        }
+    }
+    float *dst = gth + (int64_t)b * gstride + hoff;
+    for (int k = 0; k < A.K; ++k) wave_block_sum_atomic(dw[k], &dst[min(k, A.K - 1 - k)]);
+}
+
+// ------------------------------------------------------------------ latents, norm, Adam
+__global__ void t_latgrad(const float *__restrict__ gq, const float *__restrict__ dq, int N, float *__restrict__ G,
+                          int64_t gstride)
+{
+    const int b = blockIdx.y, i = blockIdx.x * kT + threadIdx.x;
+    if (i < N) G[(int64_t)b * gstride + i] = gq[(int64_t)b * N + i] * dq[(int64_t)b * N + i];
+}
+
+__global__ __launch_bounds__(kT) void t_sumsq(const float *__restrict__ G, int64_t n, int64_t gstride, float *__restrict__ acc4)
+{
+    __shared__ float s_red[8];
+    const int b = blockIdx.y;
+    float s = 0.f;
+    for (int64_t i = (int64_t)blockIdx.x * kT + threadIdx.x; i < n; i += (int64_t)gridDim.x * kT) {
+        const float v = G[(int64_t)b * gstride + i];
+        s = fmaf(v, v, s);
+    }
+    s = block_sum(s, s_red);
+    if (threadIdx.x == 0) atomicAdd(&acc4[b * 4 + 2], s);
+}
+
+struct AdamArgs {
+    float lr_bc1, inv_sqrt_bc2, beta1, beta2, eps, clip;
+    int N;
+    int64_t n, gstride, ls, ps, ms;
+};
+
+// torch.optim.Adam (_single_tensor_adam, no weight decay / amsgrad) after clip_grad_norm_
+__global__ void t_adam(const float *__restrict__ G, float *__restrict__ lat, float *__restrict__ th, float *__restrict__ m,
+                       float *__restrict__ v, const float *__restrict__ acc4, AdamArgs A)
+{
+    const int b = blockIdx.y;
+    const int64_t i = (int64_t)blockIdx.x * kT + threadIdx.x;
+    if (i >= A.n) return;
+    float coef = 1.f;
+    if (A.clip > 0.f) coef = fminf(A.clip / (sqrtf(acc4[b * 4 + 2]) + 1e-6f), 1.f);
+    const float g = G[(int64_t)b * A.gstride + i] * coef;
+    const int64_t mi = (int64_t)b * A.ms + i;
+    const float mm = A.beta1 * m[mi] + (1.f - A.beta1) * g;
+    const float vv = A.beta2 * v[mi] + (1.f - A.beta2) * g * g;
+    m[mi] = mm;
+    v[mi] = vv;
+    const float denom = sqrtf(vv) * A.inv_sqrt_bc2 + A.eps;
+    float *p = i < A.N ? lat + (int64_t)b * A.ls + i : th + (int64_t)b * A.ps + (i - A.N);
+    *p -= A.lr_bc1 * mm / denom;
+}
+
+__global__ void t_finish(const float *__restrict__ acc4, float inv_total, float lam_px, float *__restrict__ out, int B)
+{
+    const int b = threadIdx.x;
+    if (b >= B) return;
+    const float mse = acc4[b * 4 + 0] * inv_total, rate = acc4[b * 4 + 1];
+    out[b * 4 + 0] = mse + lam_px * rate;
+    out[b * 4 + 1] = mse;
+    out[b * 4 + 2] = rate;
+    out[b * 4 + 3] = sqrtf(acc4[b * 4 + 2]);
+}
+
+// ------------------------------------------------------------------ host planning
+size_t align256(size_t v) { return (v + 255) / 256 * 256; }
+
+struct Plan {
+    Geo g;
+    ArmTiles at;
+    int B, nblk_arm, nblk_head;
+    // workspace offsets (bytes)
+    size_t yq, dq, gq, kf, stacks, stacks_bytes, dense, z[kMaxSp + 1], graw, gbuf[2], gdense, gstack, tmpU, tmpG, G,
+        part_arm, part_head, acc4, total;
+    int64_t gstack_off[CCMI_MAX_GRIDS]; // per level k (1..L-2) inside gstack, elements per frame
+    int64_t gstack_per, stack_per, tmp_per;
+};
+
+int make_plan(const ccmi_train_args *a, Plan &pl)
+{
+    Geo &g = pl.g;
+    g = Geo{};
+    const int L = a->n_grids;
+    if (a->batch < 1) return ccmi_set_error(CCMI_ERR_ARG, "train: batch must be >= 1");
+    if (L < 2 || L > CCMI_MAX_GRIDS) return ccmi_set_error(CCMI_ERR_ARG, "train: n_grids %d", L);
+    g.L = L;
+    int off = 0;
+    for (int l = 0; l < L; ++l) {
+        g.h[l] = a->h[l];
+        g.w[l] = a->w[l];
+        if (g.h[l] < 1 || g.w[l] < 1) return ccmi_set_error(CCMI_ERR_ARG, "train: grid %d is %dx%d", l, g.h[l], g.w[l]);
+        if (l > 0 && (g.h[l] != (g.h[l - 1] + 1) / 2 || g.w[l] != (g.w[l - 1] + 1) / 2))
+            return ccmi_set_error(CCMI_ERR_ARG, "train: grid %d is not ceil(half) of grid %d", l, l - 1);
+        g.off[l] = off;
+        off += g.h[l] * g.w[l];
+    }
+    g.N = off;
+    g.H = g.h[0];
+    g.W = g.w[0];
+    if (a->latent_stride < g.N) return ccmi_set_error(CCMI_ERR_ARG, "train: latent_stride < %d", g.N);
+    g.d = a->dim_arm;
+    g.nh = a->n_hidden;
+    if ((g.d != 8 && g.d != 16 && g.d != 24 && g.d != 32) || g.nh < 0 || g.nh > 3)
+        return ccmi_set_error(CCMI_ERR_UNSUPPORTED, "train: ARM dim %d with %d hidden layers", g.d, g.nh);
+    g.P_arm = g.nh * (g.d * g.d + g.d) + 2 * g.d + 2;
+    g.K = a->ups_k;
+    g.n_ups = a->n_ups;
+    g.Kp = a->pre_k;
+    g.n_pre = a->n_pre;
+    if (g.K < 4 || g.K > 16 || g.K % 2 || g.Kp < 1 || g.Kp > 15 || g.Kp % 2 == 0 || g.n_ups < 1 || g.n_pre < 1)
+        return ccmi_set_error(CCMI_ERR_UNSUPPORTED, "train: upsampling kernels %d / %d", g.K, g.Kp);
+    g.hu = (g.K + 1) / 2;
+    g.hp = (g.Kp + 1) / 2;
+    g.up_off = g.P_arm;
+    g.pre_off = g.up_off + g.n_ups * g.hu;
+    g.syn_off = g.pre_off + g.n_pre * g.hp;
+    g.kfull = g.n_ups * g.K + g.n_pre * g.Kp;
+    // synthesis: 1x1 (C -> hid) + 1x1 (hid -> 3), then <= 3 3x3 layers 3 -> 3
+    const int ns = a->n_syn_layers;
+    if (ns < 2 || ns > 2 + kMaxSp) return ccmi_set_error(CCMI_ERR_UNSUPPORTED, "train: %d synthesis layers", ns);
+    const ccmi_syn_layer *S = a->syn;
+    if (S[0].ks != 1 || S[1].ks != 1 || S[0].residual || S[1].residual || S[1].n_out != 3 || S[0].n_out < 1 ||
+        S[0].n_out > 64)
+        return ccmi_set_error(CCMI_ERR_UNSUPPORTED, "train: synthesis head must be 1x1 (C -> <=64) then 1x1 (-> 3)");
+    g.hid = S[0].n_out;
+    g.r0 = S[0].relu;
+    g.r1 = S[1].relu;
+    int p = g.syn_off;
+    g.w0 = p;
+    p += g.hid * L;
+    g.b0 = p;
+    p += g.hid;
+    g.w1 = p;
+    p += 3 * g.hid;
+    g.b1 = p;
+    p += 3;
+    g.P_head = p - g.syn_off;
+    g.n_sp = ns - 2;
+    for (int i = 0; i < g.n_sp; ++i) {
+        const ccmi_syn_layer &l = S[2 + i];
+        if (l.ks != 3 || l.n_out != 3) return ccmi_set_error(CCMI_ERR_UNSUPPORTED, "train: layer %d must be 3x3, 3 -> 3", 2 + i);
+        g.sp_w[i] = p;
+        p += 81;
+        g.sp_b[i] = p;
+        p += 3;
+        g.sp_res[i] = l.residual;
+        g.sp_relu[i] = l.relu;
+    }
+    g.P = p;
+    if (a->param_stride < g.P) return ccmi_set_error(CCMI_ERR_ARG, "train: param_stride < %d", g.P);
+
+    pl.B = a->batch;
+    ArmTiles &at = pl.at;
+    at = ArmTiles{};
+    at.n = L;
+    int tiles = 0;
+    for (int l = 0; l < L; ++l) {
+        at.tiles_x[l] = ccmi_div_up(g.w[l], kATX);
+        at.start[l] = tiles;
+        tiles += at.tiles_x[l] * ccmi_div_up(g.h[l], kATY);
+    }
+    at.start[L] = tiles;
+    pl.nblk_arm = tiles;
+    const int64_t npx = (int64_t)g.H * g.W;
+    pl.nblk_head = (int)((npx + kHeadT - 1) / kHeadT);
+
+    // buffers
+    const size_t B = (size_t)pl.B;
+    size_t o = 0;
+    auto take = [&](size_t bytes) { const size_t r = o; o += align256(bytes); return r; };
+    pl.yq = take(4 * B * g.N);
+    pl.dq = take(4 * B * g.N);
+    pl.gq = take(4 * B * g.N);
+    pl.kf = take(4 * B * g.kfull);
+    pl.stack_per = 0;
+    for (int k = 1; k <= L - 2; ++k) pl.stack_per += (int64_t)(L - k) * g.h[k] * g.w[k];
+    pl.stacks_bytes = 4 * B * (size_t)pl.stack_per;
+    pl.stacks = take(pl.stacks_bytes + 4);
+    pl.dense = take(4 * B * L * npx);
+    for (int i = 0; i <= g.n_sp; ++i) pl.z[i] = take(4 * B * 3 * npx);
+    pl.graw = take(4 * B * 3 * npx);
+    pl.gbuf[0] = take(4 * B * 3 * npx);
+    pl.gbuf[1] = take(4 * B * 3 * npx);
+    pl.gdense = take(4 * B * L * npx);
+    pl.gstack_per = pl.stack_per;
+    {
+        int64_t so = 0;
+        for (int k = 1; k <= L - 2; ++k) {
+            pl.gstack_off[k] = so;
+            so += (int64_t)(L - k) * g.h[k] * g.w[k];
+        }
+    }
+    pl.gstack = take(4 * B * pl.gstack_per + 4);
+    int64_t tmax = 0;
+    for (int k = 1; k <= L - 1; ++k) {
+        tmax = std::max(tmax, (int64_t)(L - k) * g.h[k] * g.w[k - 1]); // upsample temps: C x hs x wd
+        tmax = std::max(tmax, (int64_t)g.h[k - 1] * g.w[k - 1]);       // refine temps: hd x wd
+    }
+    pl.tmp_per = tmax;
+    pl.tmpU = take(4 * B * tmax);
+    pl.tmpG = take(4 * B * tmax);
+    pl.G = take(4 * B * ((size_t)g.N + g.P));
+    pl.part_arm = take(4 * B * (size_t)pl.nblk_arm * g.P_arm);
+    pl.part_head = take(4 * B * (size_t)pl.nblk_head * g.P_head);
+    pl.acc4 = take(4 * B * 4);
+    pl.total = o;
+    return CCMI_OK;
+}
+
+template <int D>
+int launch_arm_d(int nh, dim3 grid, hipStream_t s, const float *yq, const Geo &g, const ArmTiles &at, const float *th,
+                 int64_t ps, float lam_px, float *gq, float *part, int nblk, float *acc4)
+{
+    switch (nh) {
+    case 0: hipLaunchKernelGGL((t_arm<D, 0>), grid, dim3(kT), 0, s, yq, g, at, th, ps, lam_px, gq, part, nblk, acc4); break;
+    case 1: hipLaunchKernelGGL((t_arm<D, 1>), grid, dim3(kT), 0, s, yq, g, at, th, ps, lam_px, gq, part, nblk, acc4); break;
+    case 2: hipLaunchKernelGGL((t_arm<D, 2>), grid, dim3(kT), 0, s, yq, g, at, th, ps, lam_px, gq, part, nblk, acc4); break;
+    default: hipLaunchKernelGGL((t_arm<D, 3>), grid, dim3(kT), 0, s, yq, g, at, th, ps, lam_px, gq, part, nblk, acc4); break;
+    }
+    return CCMI_OK;
+}
+
+template <int CIN>
+void launch_head(bool bwd, dim3 grid, hipStream_t s, const float *dense, const float *gz0, const Geo &g, const float *th,
+                 int64_t ps, float *z0_or_gdense, float *part, int nblk)
+{
+    if (!bwd) {
+        hipLaunchKernelGGL((t_head_fwd<CIN>), grid, dim3(kT), 0, s, dense, g, th, ps, z0_or_gdense);
+    } else {
+        const size_t lds = sizeof(float) * kHeadT * ((g.hid + 1) + std::max(4, CIN + 1));
+        hipLaunchKernelGGL((t_head_bwd<CIN>), grid, dim3(kHeadT), lds, s, dense, gz0, g, th, ps, z0_or_gdense, part,
+                           nblk);
+    }
+}
+
+void head_dispatch(int cin, bool bwd, dim3 grid, hipStream_t s, const float *dense, const float *gz0, const Geo &g,
+                   const float *th, int64_t ps, float *o, float *part, int nblk)
+{
+    switch (cin) {
+    case 2: launch_head<2>(bwd, grid, s, dense, gz0, g, th, ps, o, part, nblk); break;
+    case 3: launch_head<3>(bwd, grid, s, dense, gz0, g, th, ps, o, part, nblk); break;
+    case 4: launch_head<4>(bwd, grid, s, dense, gz0, g, th, ps, o, part, nblk); break;
+    case 5: launch_head<5>(bwd, grid, s, dense, gz0, g, th, ps, o, part, nblk); break;
+    case 6: launch_head<6>(bwd, grid, s, dense, gz0, g, th, ps, o, part, nblk); break;
+    case 7: launch_head<7>(bwd, grid, s, dense, gz0, g, th, ps, o, part, nblk); break;
+    default: launch_head<8>(bwd, grid, s, dense, gz0, g, th, ps, o, part, nblk); break;
+    }
+}
+
+dim3 grid1(int64_t n, int B) { return dim3((unsigned)((n + kT - 1) / kT), (unsigned)B); }
+
+} // namespace
+
+extern "C" size_t ccmi_train_param_count(const ccmi_train_args *a)
+{
+    if (!a) return 0;
+    ccmi_train_args t = *a;
+    t.latent_stride = 1 << 30;
+    t.param_stride = 1 << 30;
+    t.batch = 1;
+    Plan pl;
+    if (make_plan(&t, pl)) return 0;
+    return (size_t)pl.g.P;
+}
+
+extern "C" size_t ccmi_train_workspace_bytes(const ccmi_train_args *a)
+{
+    if (!a) return 0;
+    Plan pl;
+    if (make_plan(a, pl)) return 0;
+    return pl.total;
+}
+
+extern "C" int ccmi_train_step(const ccmi_train_args *a, void *stream)
+{
+    if (!a || !a->latent || !a->params || !a->target) return ccmi_set_error(CCMI_ERR_ARG, "train: null argument");
+    Plan pl;
+    if (int rc = make_plan(a, pl)) return rc;
+    if (!a->workspace || a->workspace_bytes < pl.total)
+        return ccmi_set_error(CCMI_ERR_ARG, "train: workspace of %zu bytes needed", pl.total);
+    if (a->update && (!a->adam_m || !a->adam_v || a->step < 1))
+        return ccmi_set_error(CCMI_ERR_ARG, "train: Adam state and step >= 1 needed to update");
+    if ((a->quantizer == CCMI_Q_SOFTROUND || a->quantizer == CCMI_Q_SOFTROUND_ALONE || a->quantizer == CCMI_Q_STE) &&
+        !(a->temperature > 0.f))
+        return ccmi_set_error(CCMI_ERR_ARG, "train: soft-round temperature must be > 0");
+    if (a->noise == CCMI_NOISE_KUMARASWAMY && !(a->noise_param > 0.f))
+        return ccmi_set_error(CCMI_ERR_ARG, "train: kumaraswamy parameter must be > 0");
+    hipStream_t s = static_cast<hipStream_t>(stream);
+    const Geo &g = pl.g;
+    const int B = pl.B;
+    uint8_t *ws = static_cast<uint8_t *>(a->workspace);
+    auto F = [&](size_t off) { return reinterpret_cast<float *>(ws + off); };
+    float *yq = F(pl.yq), *dq = F(pl.dq), *gq = F(pl.gq), *kf = F(pl.kf), *dense = F(pl.dense), *graw = F(pl.graw);
+    float *gd = F(pl.gdense), *gst = F(pl.gstack), *U = F(pl.tmpU), *GU = F(pl.tmpG), *acc4 = F(pl.acc4);
+    const int64_t GS = (int64_t)g.N + g.P; // gradient row per frame: latents then parameters
+    float *G = a->grad_out ? a->grad_out : F(pl.G);
+    float *Gth = G + g.N;
+    const int64_t npx = (int64_t)g.H * g.W;
+    const float lam_px = a->lmbda / (float)npx;
+
+    CCMI_HIP_CHECK(hipMemsetAsync(acc4, 0, sizeof(float) * 4 * B, s));
+    CCMI_HIP_CHECK(hipMemsetAsync(G, 0, sizeof(float) * GS * B, s));
+
+    // ---- forward
+    hipLaunchKernelGGL(t_expand, grid1(g.kfull, B), dim3(kT), 0, s, a->params, a->param_stride, g, kf);
+    hipLaunchKernelGGL(t_quant, grid1(g.N, B), dim3(kT), 0, s, a->latent, a->latent_stride, g.N, a->gain, a->quantizer,
+                       a->noise, a->temperature, a->noise_param, (uint64_t)a->seed, a->step, a->noise_in, yq, dq, gq);
+    {
+        dim3 grid(pl.nblk_arm, B);
+        float *part = F(pl.part_arm);
+        switch (g.d) {
+        case 8: launch_arm_d<8>(g.nh, grid, s, yq, g, pl.at, a->params, a->param_stride, lam_px, gq, part, pl.nblk_arm, acc4); break;
+        case 16: launch_arm_d<16>(g.nh, grid, s, yq, g, pl.at, a->params, a->param_stride, lam_px, gq, part, pl.nblk_arm, acc4); break;
+        case 24: launch_arm_d<24>(g.nh, grid, s, yq, g, pl.at, a->params, a->param_stride, lam_px, gq, part, pl.nblk_arm, acc4); break;
+        default: launch_arm_d<32>(g.nh, grid, s, yq, g, pl.at, a->params, a->param_stride, lam_px, gq, part, pl.nblk_arm, acc4); break;
+        }
+        CCMI_HIP_CHECK(hipGetLastError());
+        hipLaunchKernelGGL(t_colsum, dim3(ccmi_div_up(g.P_arm, 64), ccmi_div_up(pl.nblk_arm, 256), B), dim3(64, 4), 0, s,
+                           part, pl.nblk_arm, g.P_arm, Gth, GS);
+    }
+    {
+        ccmi_ups_args u{};
+        u.latent = yq;
+        u.latent_stride = g.N;
+        u.n_grids = g.L;
+        for (int l = 0; l < g.L; ++l) {
+            u.h[l] = g.h[l];
+            u.w[l] = g.w[l];
+        }
+        u.gain = 1.f;
+        u.quantize = 0;
+        u.ups_k = g.K;
+        u.n_ups = g.n_ups;
+        u.pre_k = g.Kp;
+        u.n_pre = g.n_pre;
+        u.params = kf;
+        u.param_stride = g.kfull;
+        u.out = dense;
+        u.out_stride = (int64_t)g.L * npx;
+        u.workspace = F(pl.stacks);
+        u.workspace_bytes = pl.stacks_bytes + 4;
+        u.batch = B;
+        if (int rc = ccmi_launch_ups_f32(&u, s)) return rc;
+    }
+    head_dispatch(g.L, false, grid1(npx, B), s, dense, nullptr, g, a->params, a->param_stride, F(pl.z[0]), nullptr, 0);
+    for (int i = 0; i < g.n_sp; ++i)
+        hipLaunchKernelGGL(t_sp_fwd, grid1(npx, B), dim3(kT), 0, s, F(pl.z[i]), g, a->params, a->param_stride, g.sp_w[i],
+                           g.sp_b[i], g.sp_res[i], g.sp_relu[i], F(pl.z[i + 1]));
+    hipLaunchKernelGGL(t_loss, grid1(npx, B), dim3(kT), 0, s, F(pl.z[g.n_sp]), g, a->target, a->target_stride, a->yuv420,
+                       graw, acc4);
+
+    // ---- synthesis backward
+    float *gcur = graw;
+    for (int i = g.n_sp - 1; i >= 0; --i) {
+        if (g.sp_relu[i])
+            hipLaunchKernelGGL(t_sp_gpre, grid1(3 * npx * B, 1), dim3(kT), 0, s, gcur, F(pl.z[i + 1]), 3 * npx * B);
+        float *gin = F(pl.gbuf[i & 1]);
+        const int nb = (int)std::min<int64_t>((npx + kT - 1) / kT, 1024);
+        hipLaunchKernelGGL(t_sp_bwd, dim3(nb, B), dim3(kT), 0, s, gcur, F(pl.z[i]), g, a->params, a->param_stride,
+                           g.sp_w[i], g.sp_b[i], g.sp_res[i], gin, Gth, GS);
+        gcur = gin;
+    }
+    {
+        float *part = F(pl.part_head);
+        head_dispatch(g.L, true, dim3(pl.nblk_head, B), s, dense, gcur, g, a->params, a->param_stride, gd, part,
+                      pl.nblk_head);
+        hipLaunchKernelGGL(t_colsum, dim3(ccmi_div_up(g.P_head, 64), ccmi_div_up(pl.nblk_head, 256), B), dim3(64, 4), 0,
+                           s, part, pl.nblk_head, g.P_head, Gth + g.syn_off, GS);
+    }
+
+    // ---- upsampling backward, finest level first (step L-2 .. 0)
+    const int K2 = g.K / 2;
+    for (int step = g.L - 2; step >= 0; --step) {
+        const int k = g.L - 1 - step; // source level; destination level k-1
+        const int hd = g.h[k - 1], wd = g.w[k - 1];
+        const int C = g.L - k;
+        const float *GY = (k - 1 == 0) ? gd : gst + pl.gstack_off[k - 1];
+        const int64_t gys = (k - 1 == 0) ? (int64_t)g.L * npx : pl.gstack_per;
+        // refine of y_hat(k-1): channel 0 of the destination stack
+        {
+            const float *X = yq + g.off[k - 1];
+            const int koff = g.n_ups * g.K + (step % g.n_pre) * g.Kp;
+            const int hoff = g.pre_off + (step % g.n_pre) * g.hp;
+            const int64_t n = (int64_t)hd * wd;
+            hipLaunchKernelGGL(t_ref_u, grid1(n, B), dim3(kT), 0, s, X, (int64_t)g.N, hd, wd, kf, g.kfull, koff, g.Kp, U,
+                               pl.tmp_per);
+            hipLaunchKernelGGL(t_ref_gu, grid1(n, B), dim3(kT), 0, s, GY, gys, U, pl.tmp_per, hd, wd, kf, g.kfull, koff,
+                               g.Kp, GU, Gth, GS, hoff);
+            hipLaunchKernelGGL(t_ref_gx, grid1(n, B), dim3(kT), 0, s, GU, pl.tmp_per, GY, gys, X, (int64_t)g.N, hd, wd,
+                               kf, g.kfull, koff, g.Kp, gq + g.off[k - 1], (int64_t)g.N, Gth, GS, hoff);
+        }
+        // transposed-conv upsampling of the source stack: channels 1..C
+        {
+            UpLevel A{C, g.h[k], g.w[k], hd, wd, g.K, -((K2 + 1) / 2), K2 / 2, step % g.n_ups};
+            const float *S = (k == g.L - 1) ? yq + g.off[k] : F(pl.stacks) + 0;
+            int64_t ss = (k == g.L - 1) ? (int64_t)g.N : 0;
+            if (k != g.L - 1) {
+                // stacks laid out by ccmi_launch_ups_f32: level k at sum_{k'<k} (L-k') h w, [batch][...]
+                int64_t so = 0;
+                for (int kk = 1; kk < k; ++kk) so += (int64_t)(g.L - kk) * g.h[kk] * g.w[kk] * B;
+                S = F(pl.stacks) + so;
+                ss = (int64_t)(g.L - k) * g.h[k] * g.w[k];
+            }
+            const int koff = A.sidx * g.K;
+            const int hoff = g.up_off + A.sidx * g.hu;
+            const int64_t nu = (int64_t)C * A.hs * wd;
+            hipLaunchKernelGGL(t_up_u, grid1(nu, B), dim3(kT), 0, s, S, ss, A, kf, g.kfull, koff, U, pl.tmp_per);
+            hipLaunchKernelGGL(t_up_gu, grid1(nu, B), dim3(kT), 0, s, GY, gys, A, kf, g.kfull, koff, GU, pl.tmp_per);
+            hipLaunchKernelGGL(t_up_dwv, grid1((int64_t)C * hd * wd, B), dim3(kT), 0, s, GY, gys, U, pl.tmp_per, A, Gth, GS,
+                               hoff);
+            hipLaunchKernelGGL(t_up_dwh, grid1(nu, B), dim3(kT), 0, s, GU, pl.tmp_per, S, ss, A, Gth, GS, hoff);
+            float *GSd = (k == g.L - 1) ? gq + g.off[k] : gst + pl.gstack_off[k];
+            const int64_t gss = (k == g.L - 1) ? (int64_t)g.N : pl.gstack_per;
+            hipLaunchKernelGGL(t_up_gs, grid1((int64_t)C * A.hs * A.ws, B), dim3(kT), 0, s, GU, pl.tmp_per, A, kf, g.kfull,
+                               koff, GSd, gss, k == g.L - 1 ? 1 : 0);
+        }
+    }
+    CCMI_HIP_CHECK(hipGetLastError());
+
+    // ---- latent gradients, norm, Adam
+    hipLaunchKernelGGL(t_latgrad, grid1(g.N, B), dim3(kT), 0, s, gq, dq, g.N, G, GS);
+    hipLaunchKernelGGL(t_sumsq, dim3((unsigned)std::min<int64_t>(ccmi_div_up((int)std::min<int64_t>(GS, 1 << 30), kT), 512), B),
+                       dim3(kT), 0, s, G, GS, GS, acc4);
+    const float total = a->yuv420 ? (float)(npx + 2 * (int64_t)(g.H / 2) * (g.W / 2)) : (float)(3 * npx);
+    if (a->loss_out) hipLaunchKernelGGL(t_finish, dim3(1), dim3(std::max(64, B)), 0, s, acc4, 1.f / total, lam_px, a->loss_out, B);
+    if (a->update) {
+        const double bc1 = 1.0 - std::pow((double)a->beta1, a->step), bc2 = 1.0 - std::pow((double)a->beta2, a->step);
+        AdamArgs A{(float)(a->lr / bc1), (float)(1.0 / std::sqrt(bc2)), a->beta1, a->beta2, a->eps, a->clip, g.N, GS, GS,
+                   a->latent_stride, a->param_stride, (int64_t)a->latent_stride + a->param_stride};
+        hipLaunchKernelGGL(t_adam, grid1(GS, B), dim3(kT), 0, s, G, a->latent, a->params, a->adam_m, a->adam_v, acc4, A);
+    }
+    CCMI_HIP_CHECK(hipGetLastError());
+    return CCMI_OK;
+}

@@ -289,6 +289,61 @@ int ccmi_arm_forward_i32(const ccmi_arm_i32_args *args, void *stream);
 int ccmi_encode_frame(ccmi_cool_desc *desc, const int32_t *latent_dev, uint8_t *out, size_t cap, size_t *len,
                       void *stream);
 
+/* ------------------------------------------------------------------------- */
+/* Encoder overfit step: training forward + backward + clip + Adam, on the GPU  */
+/* ------------------------------------------------------------------------- */
+
+/* Quantizer / noise selectors (quantizer.py:104-232). */
+enum { CCMI_Q_NONE = 0, CCMI_Q_SOFTROUND_ALONE, CCMI_Q_SOFTROUND, CCMI_Q_HARDROUND, CCMI_Q_STE, CCMI_Q_TRUE_STE };
+enum { CCMI_NOISE_NONE = 0, CCMI_NOISE_KUMARASWAMY, CCMI_NOISE_GAUSSIAN };
+
+/* One optimisation step of enc/training/train.py:238-262 for `batch` independent frames
+ * of the same size and architecture (each its own latents, networks and Adam state):
+ *   quantize (quantizer.py) -> ARM + Laplace rate -> upsampling -> synthesis ->
+ *   FrameEncoder train-mode output (frame.py:175-183: 420 nearest, clamp) ->
+ *   loss = MSE + lmbda * rate_bits / (H*W) (loss.py) -> backward -> clip_grad_norm_(clip)
+ *   -> Adam (torch.optim.Adam).
+ * params per frame (float32): ARM (as ccmi_arm_args), then the trainable HALF kernels of
+ * the n_ups upsampling filters ((ups_k+1)/2 taps each, upsampling.py:46-68), then the
+ * n_pre refine filters ((pre_k+1)/2 each), then the synthesis (as ccmi_syn_args).
+ * Supported synthesis: a 1x1 head of 2 non-residual layers (C -> hid <= 64 -> 3), then
+ * 0..3 3x3 layers 3 -> 3 (replicate padding).  Adam moments: [batch][latent_stride +
+ * param_stride], each row N latents then P parameters.  grad_out rows: [N + P], same
+ * order.  target: 444 [3][H][W] or 420 Y[H][W], U, V[H/2][W/2]. */
+typedef struct ccmi_train_args {
+    int batch;
+    int n_grids;
+    int h[CCMI_MAX_GRIDS_PUBLIC];
+    int w[CCMI_MAX_GRIDS_PUBLIC];
+    int dim_arm, n_hidden;
+    int ups_k, n_ups, pre_k, n_pre;
+    int n_syn_layers;
+    ccmi_syn_layer syn[CCMI_MAX_SYN_LAYERS];
+    float gain;
+    float *latent;          /* [batch][latent_stride], updated in place */
+    int64_t latent_stride;
+    float *params;          /* [batch][param_stride], updated in place */
+    int64_t param_stride;
+    float *adam_m, *adam_v; /* [batch][latent_stride + param_stride] */
+    const float *target;    /* [batch][target_stride] */
+    int64_t target_stride;
+    int yuv420;
+    int quantizer, noise;   /* CCMI_Q_*, CCMI_NOISE_* */
+    float temperature, noise_param, lmbda;
+    float lr, beta1, beta2, eps, clip;  /* clip <= 0: no gradient clipping */
+    int step;               /* Adam step t >= 1 (bias correction) */
+    uint64_t seed;          /* noise: counter-based RNG keyed by (seed, step, frame, index) */
+    const float *noise_in;  /* optional [batch][latent_stride]: additive noise used as is */
+    float *grad_out;        /* optional [batch][N + P]: raw gradients (before clipping) */
+    float *loss_out;        /* optional [batch][4]: loss, mse, rate_bits, grad_norm */
+    int update;             /* 0: loss and gradients only (no clip, no Adam) */
+    void *workspace;        /* ccmi_train_workspace_bytes() */
+    size_t workspace_bytes;
+} ccmi_train_args;
+size_t ccmi_train_param_count(const ccmi_train_args *args);
+size_t ccmi_train_workspace_bytes(const ccmi_train_args *args);
+int ccmi_train_step(const ccmi_train_args *args, void *stream);
+
 #ifdef __cplusplus
 }
 #endif

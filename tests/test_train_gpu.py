@@ -1,0 +1,156 @@
+"""GPU encoder overfit step (ccmi_train_step) against the reference and the CPU oracle.
+
+* tests/golden/train_*.npz (reference modules, tools/gen_golden_train.py): loss, every
+  parameter gradient, and the parameters after two clipped-Adam steps;
+* oracle/train_oracle.py (torch autograd on CPU, pinned to the same goldens) for the
+  paths the goldens cannot hold: quantisation noise (given to both as the same tensor),
+  other quantizers, batches of frames with their own networks.
+Tolerances (fp32, different summation order): gradients rtol 2e-4 with an absolute floor
+of 2e-4 x the largest gradient of the tensor; parameters after Adam 2e-3 x lr absolute
+(Adam moves each parameter by ~lr g/|g|, ill-conditioned for near-zero gradients).
+"""
+from pathlib import Path
+
+import numpy as np
+import pytest
+import torch
+
+GOLDEN = Path(__file__).resolve().parent / "golden"
+FILES = sorted(GOLDEN.glob("train_*.npz"))
+
+pytestmark = pytest.mark.gpu
+
+
+def _setup(z, gpu, batch=1):
+    import train_oracle as to
+    from ccmi import train as T
+    st, target, meta = to.from_golden(z)
+    mp = st.mp
+    arch = T.Arch(H=mp.H, W=mp.W, dim_arm=mp.dim_arm, n_hidden=mp.n_hidden, layers=tuple(mp.layers),
+                  n_grids=mp.n_grids, gain=mp.gain)
+    params = T.pack_params(mp.arm, mp.ups_half, mp.pre_half, mp.syn)
+    lat = torch.cat([x.reshape(-1) for x in st.lat]).detach()
+    if meta["yuv420"]:
+        tgt = torch.cat([target[c].reshape(-1) for c in "yuv"])
+    else:
+        tgt = target.reshape(-1)
+    of = T.Overfitter(arch, lat.repeat(batch, 1).to(gpu), params.repeat(batch, 1).to(gpu),
+                      tgt.repeat(batch, 1).to(gpu), yuv420=meta["yuv420"])
+    return of, st, target, meta
+
+
+def _flat_grads(st):
+    return torch.cat([p.grad.reshape(-1) for p in st.params()]).numpy()
+
+
+def _check_grads(got, st, names):
+    o = 0
+    for name, p in zip(names, st.params()):
+        n = p.numel()
+        ref = p.grad.reshape(-1).numpy()
+        np.testing.assert_allclose(got[o:o + n], ref, rtol=2e-4, atol=1e-7 + 2e-4 * np.abs(ref).max(), err_msg=name)
+        o += n
+
+
+@pytest.mark.parametrize("f", FILES, ids=lambda f: f.stem)
+def test_gpu_gradients_match_reference(f, gpu):
+    import train_oracle as to
+    z = np.load(f)
+    of, st, target, meta = _setup(z, gpu)
+    g = torch.zeros(1, of.N + of.P, device=gpu)
+    loss = of.step(meta["quantizer_type"], "none", meta["temperature"], 0.0, meta["lmbda"], update=False, grad_out=g)
+    torch.cuda.synchronize()
+    L, mse, rate, _ = loss[0].tolist()
+    assert abs(L - float(z["loss"])) <= 1e-5 * abs(float(z["loss"]))
+    assert abs(rate - float(z["rate_bit"])) <= 2e-5 * float(z["rate_bit"])
+    # reference gradients (golden) in TrainState order
+    names = to.golden_param_names(meta)
+    got = g[0].cpu().numpy()
+    o = 0
+    for name, p in zip(names, st.params()):
+        n = p.numel()
+        ref = z[f"g/{name}"].reshape(-1)
+        np.testing.assert_allclose(got[o:o + n], ref, rtol=2e-4, atol=1e-7 + 2e-4 * np.abs(ref).max(), err_msg=name)
+        o += n
+
+
+@pytest.mark.parametrize("f", FILES, ids=lambda f: f.stem)
+def test_gpu_two_adam_steps_match_reference(f, gpu):
+    import train_oracle as to
+    z = np.load(f)
+    of, st, target, meta = _setup(z, gpu)
+    for s in (1, 2):
+        of.step(meta["quantizer_type"], "none", meta["temperature"], 0.0, meta["lmbda"], lr=meta["lr"], clip=0.1)
+        torch.cuda.synchronize()
+        lat = of.latents[0].cpu().numpy()
+        prm = of.params[0].cpu().numpy()
+        flat = np.concatenate([lat, prm])
+        o = 0
+        for name, p in zip(to.golden_param_names(meta), st.params()):
+            n = p.numel()
+            ref = z[f"s{s}/{name}"].reshape(-1)
+            np.testing.assert_allclose(flat[o:o + n], ref, rtol=1e-5, atol=2e-3 * meta["lr"], err_msg=f"step {s} {name}")
+            o += n
+
+
+@pytest.mark.parametrize("qtype,ntype", [("softround", "kumaraswamy"), ("softround", "gaussian"), ("none", "kumaraswamy"),
+                                         ("ste", "none"), ("true_ste", "none")])
+def test_gpu_noise_and_quantizers_match_oracle(qtype, ntype, gpu):
+    import train_oracle as to
+    z = np.load(FILES[0])
+    of, st, target, meta = _setup(z, gpu)
+    g = torch.Generator().manual_seed(3)
+    N = of.N
+    if ntype == "kumaraswamy":
+        noise = to.kumaraswamy(torch.rand(N, generator=g), 2.0)
+    elif ntype == "gaussian":
+        noise = 0.25 * torch.randn(N, generator=g)
+    else:
+        noise = torch.zeros(N)
+    to.grads(st, target, qtype, 0.3, meta["lmbda"], meta["yuv420"], noise=noise)
+    gout = torch.zeros(1, N + of.P, device=gpu)
+    of.step(qtype, ntype, 0.3, 2.0, meta["lmbda"], update=False, noise=noise[None].to(gpu), grad_out=gout)
+    torch.cuda.synchronize()
+    _check_grads(gout[0].cpu().numpy(), st, to.golden_param_names(meta))
+
+
+def test_gpu_batch_of_frames_each_with_own_network(gpu):
+    """Frames in a batch are independent: frame b's gradient equals a batch-of-1 run."""
+    z = np.load(FILES[1])
+    of, st, target, meta = _setup(z, gpu, batch=3)
+    torch.manual_seed(0)
+    of.params[1] += 0.01 * torch.randn_like(of.params[1])
+    of.latents[2] += 0.05 * torch.randn_like(of.latents[2])
+    g3 = torch.zeros(3, of.N + of.P, device=gpu)
+    of.step(meta["quantizer_type"], "none", meta["temperature"], 0.0, meta["lmbda"], update=False, grad_out=g3)
+    for b in range(3):
+        of1, _, _, _ = _setup(z, gpu)
+        of1.params.copy_(of.params[b:b + 1])
+        of1.latents.copy_(of.latents[b:b + 1])
+        g1 = torch.zeros(1, of.N + of.P, device=gpu)
+        of1.step(meta["quantizer_type"], "none", meta["temperature"], 0.0, meta["lmbda"], update=False, grad_out=g1)
+        torch.cuda.synchronize()
+        a, r = g3[b].cpu().numpy(), g1[0].cpu().numpy()
+        np.testing.assert_allclose(a, r, rtol=1e-4, atol=1e-6 * np.abs(r).max())
+
+
+def test_gpu_overfit_reduces_loss(gpu):
+    """A short c3x-like phase (softround + kumaraswamy noise from the in-kernel RNG, Adam
+    1e-2) lowers the eval loss of a 64x96 frame."""
+    import forward_oracle as fo
+    from ccmi import train as T
+    mp = fo.ModelParams.random(64, 96, seed=5)
+    arch = T.Arch(64, 96)
+    params = T.pack_params(mp.arm, mp.ups_half, mp.pre_half, mp.syn)
+    g = torch.Generator().manual_seed(0)
+    lat = 0.01 * torch.randn(1, arch.n_latents, generator=g)
+    yy, xx = torch.meshgrid(torch.linspace(0, 1, 64), torch.linspace(0, 1, 96), indexing="ij")
+    img = torch.stack([0.5 + 0.3 * torch.sin(6 * xx + 3 * yy), 0.5 + 0.2 * torch.cos(5 * yy), 0.4 + 0.2 * xx])
+    tgt = torch.cat([img[0].reshape(-1), img[1, ::2, ::2].reshape(-1), img[2, ::2, ::2].reshape(-1)])[None]
+    of = T.Overfitter(arch, lat.to(gpu), params[None].to(gpu), tgt.to(gpu), yuv420=True, seed=1)
+    first = of.step("softround", "kumaraswamy", 0.3, 2.0, 1e-3, lr=1e-2).clone()
+    for _ in range(200):
+        last = of.step("softround", "kumaraswamy", 0.3, 2.0, 1e-3, lr=1e-2)
+    torch.cuda.synchronize()
+    assert torch.isfinite(last).all()
+    assert float(last[0, 0]) < 0.5 * float(first[0, 0])
