@@ -656,13 +656,6 @@ struct UpLevel {
     int C, hs, ws, hd, wd, K, d_lo, d_hi, sidx; // sidx: kernel slot (step % n_ups)
 };
 
-__device__ __forceinline__ float wave_block_sum_atomic(float v, float *dst)
-{
-    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
-    if ((threadIdx.x & 63) == 0 && v != 0.f) atomicAdd(dst, v);
-    return v;
-}
-
 // refine, horizontal pass: U[r][x] = sum_k w[k] X[r][x + k - P] (zero padding)
 __global__ void t_ref_u(const float *__restrict__ X, int64_t xs, int h, int w, const float *__restrict__ kf, int kstride,
                         int koff, int Kp, float *__restrict__ U, int64_t us)
@@ -680,63 +673,93 @@ __global__ void t_ref_u(const float *__restrict__ X, int64_t xs, int h, int w, c
     U[(int64_t)b * us + i] = a;
 }
 
-// refine, vertical adjoint: GU[r][x] = sum_k w[k] GY[r - k + P][x]; dwV[k] = sum GY[y][x] U[y + k - P][x]
-__global__ __launch_bounds__(kT) void t_ref_gu(const float *__restrict__ GY, int64_t gys, const float *__restrict__ U,
-                                               int64_t us, int h, int w, const float *__restrict__ kf, int kstride,
-                                               int koff, int Kp, float *__restrict__ GU, float *__restrict__ gth,
-                                               int64_t gstride, int hoff)
+// refine, vertical adjoint: GU[r][x] = sum_k w[k] GY[r - k + P][x]
+__global__ void t_ref_gu(const float *__restrict__ GY, int64_t gys, int h, int w, const float *__restrict__ kf,
+                         int kstride, int koff, int Kp, float *__restrict__ GU, int64_t us)
 {
     const int b = blockIdx.y;
     const int64_t n = (int64_t)h * w, i = (int64_t)blockIdx.x * kT + threadIdx.x;
+    if (i >= n) return;
     const int P = Kp / 2;
     const float *wk = kf + (int64_t)b * kstride + koff;
-    float dw[16];
-    for (int k = 0; k < 16; ++k) dw[k] = 0.f;
-    if (i < n) {
-        const int r = (int)(i / w), x = (int)(i - (int64_t)r * w);
-        const float *gy = GY + (int64_t)b * gys, *u = U + (int64_t)b * us;
-        float a = 0.f;
-        const float gyv = gy[i];
-        for (int k = 0; k < Kp; ++k) {
-            const int rr = r - k + P;
-            if (rr >= 0 && rr < h) a = fmaf(wk[k], gy[(int64_t)rr * w + x], a);
-            const int ru = r + k - P;
-            if (ru >= 0 && ru < h) dw[k] = gyv * u[(int64_t)ru * w + x];
-        }
-        GU[(int64_t)b * us + i] = a;
+    const int r = (int)(i / w), x = (int)(i - (int64_t)r * w);
+    const float *gy = GY + (int64_t)b * gys;
+    float a = 0.f;
+    for (int k = 0; k < Kp; ++k) {
+        const int rr = r - k + P;
+        if (rr >= 0 && rr < h) a = fmaf(wk[k], gy[(int64_t)rr * w + x], a);
     }
-    float *dst = gth + (int64_t)b * gstride + hoff;
-    for (int k = 0; k < Kp; ++k) wave_block_sum_atomic(dw[k], &dst[min(k, Kp - 1 - k)]);
+    GU[(int64_t)b * us + i] = a;
 }
 
-// refine, horizontal adjoint + residual: g_x = sum_k w[k] GU[r][m - k + P] + GY; dwH[k] = sum GU[r][x] X[r][x + k - P]
-__global__ __launch_bounds__(kT) void t_ref_gx(const float *__restrict__ GU, int64_t us, const float *__restrict__ GY,
-                                               int64_t gys, const float *__restrict__ X, int64_t xs, int h, int w,
-                                               const float *__restrict__ kf, int kstride, int koff, int Kp,
-                                               float *__restrict__ GX, int64_t gxs, float *__restrict__ gth,
-                                               int64_t gstride, int hoff)
+// refine, horizontal adjoint + residual: GX += sum_k w[k] GU[r][m - k + P] + GY
+__global__ void t_ref_gx(const float *__restrict__ GU, int64_t us, const float *__restrict__ GY, int64_t gys, int h,
+                         int w, const float *__restrict__ kf, int kstride, int koff, int Kp, float *__restrict__ GX,
+                         int64_t gxs)
 {
     const int b = blockIdx.y;
     const int64_t n = (int64_t)h * w, i = (int64_t)blockIdx.x * kT + threadIdx.x;
+    if (i >= n) return;
     const int P = Kp / 2;
     const float *wk = kf + (int64_t)b * kstride + koff;
-    float dw[16];
-    for (int k = 0; k < 16; ++k) dw[k] = 0.f;
-    if (i < n) {
-        const int r = (int)(i / w), m = (int)(i - (int64_t)r * w);
-        const float *gu = GU + (int64_t)b * us + (int64_t)r * w, *x = X + (int64_t)b * xs + (int64_t)r * w;
-        float a = GY[(int64_t)b * gys + i];
-        const float guv = gu[m];
-        for (int k = 0; k < Kp; ++k) {
-            const int mm = m - k + P;
-            if (mm >= 0 && mm < w) a = fmaf(wk[k], gu[mm], a);
-            const int xx = m + k - P;
-            if (xx >= 0 && xx < w) dw[k] = guv * x[xx];
-        }
-        GX[(int64_t)b * gxs + i] += a;
+    const int r = (int)(i / w), m = (int)(i - (int64_t)r * w);
+    const float *gu = GU + (int64_t)b * us + (int64_t)r * w;
+    float a = GY[(int64_t)b * gys + i];
+    for (int k = 0; k < Kp; ++k) {
+        const int mm = m - k + P;
+        if (mm >= 0 && mm < w) a = fmaf(wk[k], gu[mm], a);
     }
-    float *dst = gth + (int64_t)b * gstride + hoff;
-    for (int k = 0; k < Kp; ++k) wave_block_sum_atomic(dw[k], &dst[min(k, Kp - 1 - k)]);
+    GX[(int64_t)b * gxs + i] += a;
+}
+
+// Sum of per-thread tap gradients over the workgroup, folded onto the symmetric half
+// kernel (upsampling.py:46-68): one atomic per half tap per workgroup.
+template <int K>
+__device__ __forceinline__ void reduce_taps(float (&dw)[K], float *__restrict__ dst)
+{
+    __shared__ float s_r[kT / 64][K];
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+#pragma unroll
+    for (int k = 0; k < K; ++k) {
+        float v = dw[k];
+        for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
+        if (lane == 0) s_r[wid][k] = v;
+    }
+    __syncthreads();
+    if (threadIdx.x < K) {
+        float v = 0.f;
+#pragma unroll
+        for (int i = 0; i < kT / 64; ++i) v += s_r[i][threadIdx.x];
+        atomicAdd(&dst[min((int)threadIdx.x, K - 1 - (int)threadIdx.x)], v);
+    }
+}
+
+// refine kernel gradient over the level's pixels: vertical taps (GY x U) + horizontal taps (GU x X)
+template <int KP>
+__global__ __launch_bounds__(kT) void t_ref_dw(const float *__restrict__ GY, int64_t gys, const float *__restrict__ U,
+                                               const float *__restrict__ GU, int64_t us, const float *__restrict__ X,
+                                               int64_t xs, int h, int w, float *__restrict__ gth, int64_t gstride,
+                                               int hoff)
+{
+    constexpr int P = KP / 2;
+    const int b = blockIdx.y;
+    const int64_t n = (int64_t)h * w;
+    const float *gy = GY + (int64_t)b * gys, *u = U + (int64_t)b * us, *gu = GU + (int64_t)b * us;
+    const float *x = X + (int64_t)b * xs;
+    float dw[KP];
+#pragma unroll
+    for (int k = 0; k < KP; ++k) dw[k] = 0.f;
+    for (int64_t i = (int64_t)blockIdx.x * kT + threadIdx.x; i < n; i += (int64_t)gridDim.x * kT) {
+        const int r = (int)(i / w), c = (int)(i - (int64_t)r * w);
+        const float gv = gy[i], guv = gu[i];
+#pragma unroll
+        for (int k = 0; k < KP; ++k) {
+            const int ru = r + k - P, cx = c + k - P;
+            if (ru >= 0 && ru < h) dw[k] = fmaf(gv, u[(int64_t)ru * w + c], dw[k]);
+            if (cx >= 0 && cx < w) dw[k] = fmaf(guv, x[(int64_t)r * w + cx], dw[k]);
+        }
+    }
+    reduce_taps<KP>(dw, gth + (int64_t)b * gstride + hoff);
 }
 
 __device__ __forceinline__ int up_tap(int a, int d, int K) { return a + K / 2 - 1 - 2 * d; }
@@ -789,30 +812,6 @@ __global__ void t_up_gu(const float *__restrict__ GY, int64_t gys, UpLevel A, co
     GU[(int64_t)b * us + i] = acc;
 }
 
-// upsample, vertical kernel gradient: over destination pixels (c, yd, xd)
-__global__ __launch_bounds__(kT) void t_up_dwv(const float *__restrict__ GY, int64_t gys, const float *__restrict__ U,
-                                               int64_t us, UpLevel A, float *__restrict__ gth, int64_t gstride, int hoff)
-{
-    const int b = blockIdx.y;
-    const int64_t n = (int64_t)A.C * A.hd * A.wd, i = (int64_t)blockIdx.x * kT + threadIdx.x;
-    float dw[16];
-    for (int k = 0; k < 16; ++k) dw[k] = 0.f;
-    if (i < n) {
-        const int xd = (int)(i % A.wd);
-        const int64_t cy = i / A.wd;
-        const int c = (int)(cy / A.hd), yd = (int)(cy - (int64_t)c * A.hd);
-        const float gv = GY[(int64_t)b * gys + (int64_t)(c + 1) * A.hd * A.wd + (int64_t)yd * A.wd + xd];
-        const float *u = U + (int64_t)b * us + (int64_t)c * A.hs * A.wd + xd;
-        const int j = yd >> 1, a = yd & 1;
-        for (int d = A.d_lo; d <= A.d_hi; ++d) {
-            const int t = up_tap(a, d, A.K);
-            if (t >= 0 && t < A.K) dw[t] = gv * u[(int64_t)clampi(j + d, A.hs - 1) * A.wd];
-        }
-    }
-    float *dst = gth + (int64_t)b * gstride + hoff;
-    for (int k = 0; k < A.K; ++k) wave_block_sum_atomic(dw[k], &dst[min(k, A.K - 1 - k)]);
-}
-
 // upsample, horizontal adjoint: GS[c][r][m] (+= into the source gradient)
 __global__ void t_up_gs(const float *__restrict__ GU, int64_t us, UpLevel A, const float *__restrict__ kf, int kstride,
                         int koff, float *__restrict__ GS, int64_t gss, int accumulate)
@@ -842,27 +841,56 @@ __global__ void t_up_gs(const float *__restrict__ GU, int64_t us, UpLevel A, con
     *o = accumulate ? *o + acc : acc;
 }
 
-// upsample, horizontal kernel gradient: over (c, r, xd)
-__global__ __launch_bounds__(kT) void t_up_dwh(const float *__restrict__ GU, int64_t us, const float *__restrict__ S,
-                                               int64_t ss, UpLevel A, float *__restrict__ gth, int64_t gstride, int hoff)
+// upsample kernel gradient: vertical taps over destination row pairs (c, j, xd),
+// horizontal taps over destination column pairs (c, r, j); taps are compile-time per
+// parity: destination 2j + a, source offset d -> tap a + K/2 - 1 - 2d.
+template <int K>
+__global__ __launch_bounds__(kT) void t_up_dw(const float *__restrict__ GY, int64_t gys, const float *__restrict__ U,
+                                              const float *__restrict__ GU, int64_t us, const float *__restrict__ S,
+                                              int64_t ss, UpLevel A, float *__restrict__ gth, int64_t gstride, int hoff)
 {
+    constexpr int K2 = K / 2, DLO = -((K2 + 1) / 2), DHI = K2 / 2;
     const int b = blockIdx.y;
-    const int64_t n = (int64_t)A.C * A.hs * A.wd, i = (int64_t)blockIdx.x * kT + threadIdx.x;
-    float dw[16];
-    for (int k = 0; k < 16; ++k) dw[k] = 0.f;
-    if (i < n) {
+    float dw[K];
+#pragma unroll
+    for (int k = 0; k < K; ++k) dw[k] = 0.f;
+    const int njy = (A.hd + 1) >> 1, njx = (A.wd + 1) >> 1;
+    const float *gyb = GY + (int64_t)b * gys, *ub = U + (int64_t)b * us, *gub = GU + (int64_t)b * us;
+    const float *sb = S + (int64_t)b * ss;
+    const int64_t nv = (int64_t)A.C * njy * A.wd;
+    for (int64_t i = (int64_t)blockIdx.x * kT + threadIdx.x; i < nv; i += (int64_t)gridDim.x * kT) {
         const int xd = (int)(i % A.wd);
-        const int64_t cr = i / A.wd;
-        const float gv = GU[(int64_t)b * us + i];
-        const float *src = S + (int64_t)b * ss + cr * A.ws;
-        const int j = xd >> 1, a = xd & 1;
-        for (int d = A.d_lo; d <= A.d_hi; ++d) {
-            const int t = up_tap(a, d, A.K);
-            if (t >= 0 && t < A.K) dw[t] = gv * src[clampi(j + d, A.ws - 1)];
+        const int64_t cj = i / A.wd;
+        const int c = (int)(cj / njy), j = (int)(cj - (int64_t)c * njy);
+        const float *gy = gyb + (int64_t)(c + 1) * A.hd * A.wd + xd;
+        const float ge = gy[(int64_t)(2 * j) * A.wd];
+        const float go = 2 * j + 1 < A.hd ? gy[(int64_t)(2 * j + 1) * A.wd] : 0.f;
+        const float *u = ub + (int64_t)c * A.hs * A.wd + xd;
+#pragma unroll
+        for (int d = DLO; d <= DHI; ++d) {
+            const float uv = u[(int64_t)clampi(j + d, A.hs - 1) * A.wd];
+            const int te = K2 - 1 - 2 * d, to = K2 - 2 * d;
+            if (te >= 0 && te < K) dw[te] = fmaf(ge, uv, dw[te]);
+            if (to >= 0 && to < K) dw[to] = fmaf(go, uv, dw[to]);
         }
     }
-    float *dst = gth + (int64_t)b * gstride + hoff;
-    for (int k = 0; k < A.K; ++k) wave_block_sum_atomic(dw[k], &dst[min(k, A.K - 1 - k)]);
+    const int64_t nh = (int64_t)A.C * A.hs * njx;
+    for (int64_t i = (int64_t)blockIdx.x * kT + threadIdx.x; i < nh; i += (int64_t)gridDim.x * kT) {
+        const int j = (int)(i % njx);
+        const int64_t cr = i / njx;
+        const float *gu = gub + cr * A.wd;
+        const float ge = gu[2 * j];
+        const float go = 2 * j + 1 < A.wd ? gu[2 * j + 1] : 0.f;
+        const float *src = sb + cr * A.ws;
+#pragma unroll
+        for (int d = DLO; d <= DHI; ++d) {
+            const float sv = src[clampi(j + d, A.ws - 1)];
+            const int te = K2 - 1 - 2 * d, to = K2 - 2 * d;
+            if (te >= 0 && te < K) dw[te] = fmaf(ge, sv, dw[te]);
+            if (to >= 0 && to < K) dw[to] = fmaf(go, sv, dw[to]);
+        }
+    }
+    reduce_taps<K>(dw, gth + (int64_t)b * gstride + hoff);
 }
 
 // ------------------------------------------------------------------ latents, norm, Adam
@@ -968,7 +996,8 @@ int make_plan(const ccmi_train_args *a, Plan &pl)
     g.n_ups = a->n_ups;
     g.Kp = a->pre_k;
     g.n_pre = a->n_pre;
-    if (g.K < 4 || g.K > 16 || g.K % 2 || g.Kp < 1 || g.Kp > 15 || g.Kp % 2 == 0 || g.n_ups < 1 || g.n_pre < 1)
+    if ((g.K != 4 && g.K != 6 && g.K != 8) || (g.Kp != 1 && g.Kp != 3 && g.Kp != 5 && g.Kp != 7 && g.Kp != 9) ||
+        g.n_ups < 1 || g.n_pre < 1)
         return ccmi_set_error(CCMI_ERR_UNSUPPORTED, "train: upsampling kernels %d / %d", g.K, g.Kp);
     g.hu = (g.K + 1) / 2;
     g.hp = (g.Kp + 1) / 2;
@@ -1109,6 +1138,9 @@ void head_dispatch(int cin, bool bwd, dim3 grid, hipStream_t s, const float *den
 }
 
 dim3 grid1(int64_t n, int B) { return dim3((unsigned)((n + kT - 1) / kT), (unsigned)B); }
+// workgroups for a grid-stride reduction over n items: enough to fill the chip with a
+// batch of frames, few enough that the per-workgroup atomics stay cheap
+unsigned red_blocks(int64_t n) { return (unsigned)std::max<int64_t>(1, std::min<int64_t>((n + kT - 1) / kT, 64)); }
 
 } // namespace
 
@@ -1245,10 +1277,18 @@ extern "C" int ccmi_train_step(const ccmi_train_args *a, void *stream)
             const int64_t n = (int64_t)hd * wd;
             hipLaunchKernelGGL(t_ref_u, grid1(n, B), dim3(kT), 0, s, X, (int64_t)g.N, hd, wd, kf, g.kfull, koff, g.Kp, U,
                                pl.tmp_per);
-            hipLaunchKernelGGL(t_ref_gu, grid1(n, B), dim3(kT), 0, s, GY, gys, U, pl.tmp_per, hd, wd, kf, g.kfull, koff,
-                               g.Kp, GU, Gth, GS, hoff);
-            hipLaunchKernelGGL(t_ref_gx, grid1(n, B), dim3(kT), 0, s, GU, pl.tmp_per, GY, gys, X, (int64_t)g.N, hd, wd,
-                               kf, g.kfull, koff, g.Kp, gq + g.off[k - 1], (int64_t)g.N, Gth, GS, hoff);
+            hipLaunchKernelGGL(t_ref_gu, grid1(n, B), dim3(kT), 0, s, GY, gys, hd, wd, kf, g.kfull, koff, g.Kp, GU,
+                               pl.tmp_per);
+            const dim3 gr(red_blocks(n), B);
+            switch (g.Kp) {
+            case 1: hipLaunchKernelGGL(t_ref_dw<1>, gr, dim3(kT), 0, s, GY, gys, U, GU, pl.tmp_per, X, (int64_t)g.N, hd, wd, Gth, GS, hoff); break;
+            case 3: hipLaunchKernelGGL(t_ref_dw<3>, gr, dim3(kT), 0, s, GY, gys, U, GU, pl.tmp_per, X, (int64_t)g.N, hd, wd, Gth, GS, hoff); break;
+            case 5: hipLaunchKernelGGL(t_ref_dw<5>, gr, dim3(kT), 0, s, GY, gys, U, GU, pl.tmp_per, X, (int64_t)g.N, hd, wd, Gth, GS, hoff); break;
+            case 7: hipLaunchKernelGGL(t_ref_dw<7>, gr, dim3(kT), 0, s, GY, gys, U, GU, pl.tmp_per, X, (int64_t)g.N, hd, wd, Gth, GS, hoff); break;
+            default: hipLaunchKernelGGL(t_ref_dw<9>, gr, dim3(kT), 0, s, GY, gys, U, GU, pl.tmp_per, X, (int64_t)g.N, hd, wd, Gth, GS, hoff); break;
+            }
+            hipLaunchKernelGGL(t_ref_gx, grid1(n, B), dim3(kT), 0, s, GU, pl.tmp_per, GY, gys, hd, wd, kf, g.kfull, koff,
+                               g.Kp, gq + g.off[k - 1], (int64_t)g.N);
         }
         // transposed-conv upsampling of the source stack: channels 1..C
         {
@@ -1267,9 +1307,12 @@ extern "C" int ccmi_train_step(const ccmi_train_args *a, void *stream)
             const int64_t nu = (int64_t)C * A.hs * wd;
             hipLaunchKernelGGL(t_up_u, grid1(nu, B), dim3(kT), 0, s, S, ss, A, kf, g.kfull, koff, U, pl.tmp_per);
             hipLaunchKernelGGL(t_up_gu, grid1(nu, B), dim3(kT), 0, s, GY, gys, A, kf, g.kfull, koff, GU, pl.tmp_per);
-            hipLaunchKernelGGL(t_up_dwv, grid1((int64_t)C * hd * wd, B), dim3(kT), 0, s, GY, gys, U, pl.tmp_per, A, Gth, GS,
-                               hoff);
-            hipLaunchKernelGGL(t_up_dwh, grid1(nu, B), dim3(kT), 0, s, GU, pl.tmp_per, S, ss, A, Gth, GS, hoff);
+            const dim3 gr(red_blocks((int64_t)C * hd * wd), B);
+            switch (g.K) {
+            case 4: hipLaunchKernelGGL(t_up_dw<4>, gr, dim3(kT), 0, s, GY, gys, U, GU, pl.tmp_per, S, ss, A, Gth, GS, hoff); break;
+            case 6: hipLaunchKernelGGL(t_up_dw<6>, gr, dim3(kT), 0, s, GY, gys, U, GU, pl.tmp_per, S, ss, A, Gth, GS, hoff); break;
+            default: hipLaunchKernelGGL(t_up_dw<8>, gr, dim3(kT), 0, s, GY, gys, U, GU, pl.tmp_per, S, ss, A, Gth, GS, hoff); break;
+            }
             float *GSd = (k == g.L - 1) ? gq + g.off[k] : gst + pl.gstack_off[k];
             const int64_t gss = (k == g.L - 1) ? (int64_t)g.N : pl.gstack_per;
             hipLaunchKernelGGL(t_up_gs, grid1((int64_t)C * A.hs * A.ws, B), dim3(kT), 0, s, GU, pl.tmp_per, A, kf, g.kfull,
