@@ -247,6 +247,59 @@ def bench_bitexact_encode(reps: int = 2):
             "data": "15 shipped JVET class-E .cool bitstreams re-encoded from their decoded latents"}
 
 
+def synthetic_frame(H, W, seed):
+    """Seeded smooth image (sum of 2-D sinusoids + N(0, 0.02) noise), YUV420 target layout."""
+    g = torch.Generator().manual_seed(seed)
+    yy, xx = torch.meshgrid(torch.linspace(0, 1, H), torch.linspace(0, 1, W), indexing="ij")
+    f = 3 + seed % 5
+    img = torch.stack([0.5 + 0.25 * torch.sin(f * 6.28 * xx) * torch.cos(2 * 6.28 * yy) + 0.1 * torch.sin(19 * xx * yy),
+                       0.5 + 0.1 * torch.cos(3 * 6.28 * yy), 0.5 + 0.1 * torch.sin(2 * 6.28 * xx)])
+    img = (img + 0.02 * torch.randn(img.shape, generator=g)).clamp(0, 1)
+    return torch.cat([img[0].reshape(-1), img[1, ::2, ::2].reshape(-1), img[2, ::2, ::2].reshape(-1)])
+
+
+def bench_encoder(images: int, scale: float, rank: int, dev):
+    """Encoder overfit: the c3x schedule (warm-up candidates + 3 phases, ccmi.train.overfit)
+    for `images` synthetic 512x768 YUV420 frames trained together on this GPU."""
+    from ccmi import train as T
+    H_, W_ = 512, 768
+    arch = T.Arch(H_, W_)
+    tg = torch.stack([synthetic_frame(H_, W_, 100 * rank + i) for i in range(images)]).to(dev)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    of, best = T.overfit(arch, tg, lmbda=1e-3, scale=scale, seed=rank)
+    torch.cuda.synchronize()
+    dt = time.perf_counter() - t0
+    mse = best[:, 1].double()
+    return {"seconds": dt, "images": images, "psnr_db": float((-10 * torch.log10(mse)).mean()),
+            "rate_bpp": float((best[:, 2].double() / (H_ * W_)).mean()), "iterations": T.c3x_iterations(scale)}
+
+
+def cpu_encoder_baseline(iters: int = 2):
+    """The CPU oracle (torch fp32 autograd restatement of the training step, same math) at
+    512x768: seconds per iteration on this host's cores, projected onto the c3x schedule."""
+    import forward_oracle as fo
+    import train_oracle as to
+    from ccmi import train as T
+    mp = fo.ModelParams.random(512, 768, seed=0)
+    g = torch.Generator().manual_seed(0)
+    st = to.TrainState(mp, [0.01 * torch.randn(h, w, generator=g) for h, w in mp.sizes])
+    tgt = {"y": torch.rand(512, 768), "u": torch.rand(256, 384), "v": torch.rand(256, 384)}
+    opt = to.Adam(st.params(), 1e-2)
+    to.grads(st, tgt, "softround", 0.3, 1e-3, True)
+    t0 = time.perf_counter()
+    for _ in range(iters):
+        to.grads(st, tgt, "softround", 0.3, 1e-3, True)
+        opt.step()
+    per = (time.perf_counter() - t0) / iters
+    # per image: 5 x 400 + 2 x 400 warm-up candidate iterations + 13,100 phase iterations
+    per_image = per * (5 * 400 + 2 * 400 + 13100)
+    return {"value": round(3600.0 / per_image, 3), "unit": "images/hr", "cores": torch.get_num_threads(),
+            "kind": "port", "sample": f"{iters} training iterations at 512x768 (oracle/train_oracle.py, torch fp32 "
+                                      f"autograd on CPU, {torch.get_num_threads()} threads): {per * 1e3:.0f} ms/iteration, "
+                                      f"projected onto the 15,900 image-iterations of c3x"}
+
+
 def cpu_decode_baseline(budget_s=10.0):
     """The reference C decoder (oracle/_ref, built from /root/reference sources) -- or the C oracle
     when that binary is absent -- decoding the class-E streams, one process per core."""
@@ -300,6 +353,8 @@ def main():
     ap.add_argument("--decode-reps", type=int, default=8, help="class-E stream copies for the bit-exact decode leg")
     ap.add_argument("--staged", action="store_true",
                     help="run upsampling / synthesis / post as separate kernels (module-boundary path)")
+    ap.add_argument("--encode-images", type=int, default=8, help="frames overfitted together per GPU (0: skip)")
+    ap.add_argument("--encode-scale", type=float, default=1.0, help="fraction of the c3x schedule to run")
     ap.add_argument("--serial", action="store_true",
                     help="one stream: no overlap of the ARM with the decode tail")
     args = ap.parse_args()
@@ -394,6 +449,24 @@ def main():
             dec["cpu_baseline"] = cpu_decode_baseline()
         res["bitexact_decode"] = dec
         res["bitexact_encode"] = bench_bitexact_encode()
+    if args.encode_images > 0:
+        enc = bench_encoder(args.encode_images, args.encode_scale, rank, dev)
+        per_gpu = enc["images"] / enc["seconds"] * 3600.0
+        tot = per_gpu
+        if dist:
+            t = torch.tensor([per_gpu], device=dev, dtype=torch.float64)
+            dist.all_reduce(t)
+            tot = float(t.item())
+        res["encoder_overfit"] = {
+            "metric": "encoder images/hr (c3x schedule, 512x768 YUV420, all GPUs)", "value": round(tot, 2),
+            "per_gpu": round(per_gpu, 2), "unit": "images/hr", "n_gpus": world,
+            "images_per_gpu": enc["images"], "seconds": round(enc["seconds"], 2),
+            "schedule": f"c3x x{args.encode_scale:g}: warm-up 5x400 + 2x400 candidates, phases 10600 + 1500 + 1000 "
+                        f"iterations ({enc['iterations']} per image); quantize_model not run",
+            "psnr_db_mean": round(enc["psnr_db"], 3), "rate_bpp_mean": round(enc["rate_bpp"], 4),
+            "data": "synthetic 512x768 frames (seeded sinusoids + N(0, 0.02) noise), lmbda 1e-3"}
+        if rank == 0 and world == 1 and not args.no_cpu_baseline:
+            res["encoder_overfit"]["cpu_baseline"] = cpu_encoder_baseline()
     if rank == 0:
         print(json.dumps(res), flush=True)
     if dist:

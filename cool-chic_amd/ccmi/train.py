@@ -80,6 +80,34 @@ class Arch:
         return sum(h * w for h, w in self.sizes)
 
 
+def init_params(arch: Arch, generator: torch.Generator | None = None) -> torch.Tensor:
+    """Parameter block of a freshly constructed CoolChicEncoder: ARM residual layers zero,
+    output layer N(0, 1/C_out^4) (arm.py:66-84); upsampling bicubic / bilinear half kernels
+    (upsampling.py:262-292) and Dirac refine kernels (:131-150); synthesis residual layers
+    zero, others U(-a, a), a = 1 / (C_out^2 sqrt(C_in k^2)) (synthesis.py:86-116); biases 0."""
+    g = generator or torch.Generator().manual_seed(0)
+    d = arch.dim_arm
+    arm = [(torch.zeros(d, d), torch.zeros(d)) for _ in range(arch.n_hidden)]
+    arm.append((torch.randn(2, d, generator=g) / 2 ** 2, torch.zeros(2)))
+    hu, hp = (arch.ups_k + 1) // 2, (arch.pre_k + 1) // 2
+    core = torch.tensor([1.0 / 4.0, 3.0 / 4.0]) if arch.ups_k < 8 else \
+        torch.tensor([0.0351562, 0.1054687, -0.2617187, -0.8789063])
+    up = torch.zeros(hu)
+    up[hu - core.numel():] = core
+    pre = torch.zeros(hp)
+    pre[-1] = 1.0
+    syn, c = [], arch.n_grids
+    for n_out, k, res, _ in arch.layers:
+        if res:
+            W = torch.zeros(n_out, c, k, k)
+        else:
+            a = math.sqrt(1.0 / (c * k * k)) / n_out ** 2
+            W = (torch.rand(n_out, c, k, k, generator=g) - 0.5) * 2 * a
+        syn.append((W, torch.zeros(n_out)))
+        c = n_out
+    return pack_params(arm, [up] * (arch.n_grids - 1), [pre] * (arch.n_grids - 1), syn)
+
+
 def pack_params(arm, ups_half, pre_half, syn) -> torch.Tensor:
     """[(W, b)...], [half...], [half...], [(W, b)...] -> flat float32 parameter block."""
     parts = [t.reshape(-1).float() for wb in arm for t in wb]
@@ -115,6 +143,30 @@ class Overfitter:
         self.loss = torch.zeros(self.B, 4, device=dev)
         self.ws = torch.empty(L.ccmi_train_workspace_bytes(C.byref(a)), dtype=torch.uint8, device=dev)
 
+    def reset_optimizer(self):
+        """A new torch.optim.Adam: every training phase builds its own (train.py:184)."""
+        self.m.zero_()
+        self.v.zero_()
+        self.t = 0
+
+    def keep(self, idx: torch.Tensor):
+        """Keep frames idx (a [B'] index tensor) of the batch, in that order."""
+        idx = idx.to(self.latents.device)
+        self.latents = self.latents[idx].contiguous()
+        self.params = self.params[idx].contiguous()
+        self.targets = self.targets[idx].contiguous()
+        self.m, self.v = self.m[idx].contiguous(), self.v[idx].contiguous()
+        self.B = int(idx.numel())
+        self.loss = torch.zeros(self.B, 4, device=self.latents.device)
+        a = self._args()
+        self.ws = torch.empty(_bind().ccmi_train_workspace_bytes(C.byref(a)), dtype=torch.uint8,
+                              device=self.latents.device)
+
+    def validate(self, lmbda: float) -> torch.Tensor:
+        """Loss of the hard-rounded forward (train.py test(): quantizer "hardround", no
+        noise), without the eval-mode 8-bit rounding of the decoded image."""
+        return self.step("hardround", "none", 1.0, 1.0, lmbda, update=False).clone()
+
     def _args(self) -> TrainArgs:
         ar = self.arch
         a = TrainArgs()
@@ -135,7 +187,8 @@ class Overfitter:
 
     def step(self, quantizer_type="softround", quantizer_noise_type="kumaraswamy", soft_round_temperature=0.3,
              noise_parameter=1.0, lmbda=1e-3, lr=1e-2, clip=0.1, update=True, noise=None, grad_out=None):
-        """One iteration; returns [B, 4] (loss, mse, rate_bits, grad_norm) of this step's forward."""
+        """One iteration; returns [B, 4] (loss, mse, rate_bits, grad_norm) of this step's forward.
+        update: False (gradients only), True / "all" (Adam on everything), "latent"."""
         a = self._args()
         if update:
             self.t += 1
@@ -154,7 +207,7 @@ class Overfitter:
                 raise ValueError("grad_out: contiguous [B, N + P] expected")
             a.grad_out = grad_out.data_ptr()
         a.loss_out = self.loss.data_ptr()
-        a.update = int(update)
+        a.update = 2 if update == "latent" else int(bool(update))
         a.workspace, a.workspace_bytes = self.ws.data_ptr(), self.ws.numel()
         check(_bind().ccmi_train_step(C.byref(a), torch.cuda.current_stream(self.latents.device).cuda_stream))
         return self.loss
@@ -173,4 +226,100 @@ def linear(a: float, b: float, it: int, max_it: int) -> float:
     return a + (b - a) * it / max_it
 
 
-__all__ = ["Arch", "Overfitter", "pack_params", "cosine_lr", "linear", "Q_TYPES", "NOISE_TYPES"]
+@dataclass
+class Phase:
+    """TrainerPhase (enc/training/presets.py:25-110)."""
+    lr: float = 1e-2
+    max_itr: int = 5000
+    freq_valid: int = 100
+    patience: int = 10000
+    schedule_lr: bool = False
+    end_lr: float = 1e-5
+    softround_temperature: tuple = (0.3, 0.3)
+    noise_parameter: tuple = (1.0, 1.0)
+    quantizer_noise_type: str = "kumaraswamy"
+    quantizer_type: str = "softround"
+    optimized_module: str = "all"
+    quantize_model: bool = False
+
+
+# preset_cfg/c3x.yaml
+C3X_WARMUP = [(5, Phase(lr=1e-2, max_itr=400, freq_valid=400, patience=100000, noise_parameter=(2.0, 2.0))),
+              (2, Phase(lr=1e-2, max_itr=400, freq_valid=400, patience=100000, noise_parameter=(2.0, 2.0)))]
+C3X_PHASES = [
+    Phase(lr=1e-2, max_itr=10600, patience=5000, schedule_lr=True, quantizer_noise_type="gaussian",
+          softround_temperature=(0.3, 0.1), noise_parameter=(0.25, 0.1)),
+    Phase(lr=1e-4, max_itr=1500, patience=1500, schedule_lr=True, quantizer_type="ste", quantizer_noise_type="none",
+          softround_temperature=(1e-4, 1e-4), quantize_model=True),
+    Phase(lr=1e-4, max_itr=1000, patience=50, quantizer_type="ste", quantizer_noise_type="none",
+          optimized_module="latent", freq_valid=10, softround_temperature=(1e-4, 1e-4)),
+]
+
+
+def c3x_iterations(scale: float = 1.0) -> int:
+    """Training iterations per image of the c3x preset (x scale): warm-up candidates
+    trained in parallel count once per surviving image."""
+    return sum(max(1, int(p.max_itr * scale)) for _, p in C3X_WARMUP) + \
+        sum(max(1, int(p.max_itr * scale)) for p in C3X_PHASES)
+
+
+def run_phase(of: Overfitter, ph: Phase, lmbda: float, scale: float = 1.0) -> torch.Tensor:
+    """train() (enc/training/train.py:86-374) for every frame of the batch at once: Adam
+    restarted, cosine learning rate stepped every freq_valid iterations, linear soft-round
+    temperature / noise schedules, validation every freq_valid iterations keeping each
+    frame's best parameters (restored at the end of the phase).  Patience-based early
+    stopping is not applied (the batch runs max_itr).  Returns the best validation [B, 4]."""
+    n = max(1, int(ph.max_itr * scale))
+    freq = max(1, int(ph.freq_valid * scale)) if scale < 1 else ph.freq_valid
+    of.reset_optimizer()
+    best = of.validate(lmbda)
+    best_lat, best_prm = of.latents.clone(), of.params.clone()
+    T = ph.softround_temperature[0]
+    nz = ph.noise_parameter[0]
+    upd = "latent" if ph.optimized_module == "latent" else True
+    for cnt in range(n):
+        lr = cosine_lr(ph.lr, ph.end_lr, cnt, n, freq) if ph.schedule_lr else ph.lr
+        of.step(ph.quantizer_type, ph.quantizer_noise_type, T, nz, lmbda, lr=lr, update=upd)
+        if (cnt + 1) % freq == 0 or cnt + 1 == n:
+            cur = of.validate(lmbda)
+            better = cur[:, 0] < best[:, 0]
+            if bool(better.any()):
+                best = torch.where(better[:, None], cur, best)
+                best_lat = torch.where(better[:, None], of.latents, best_lat)
+                best_prm = torch.where(better[:, None], of.params, best_prm)
+            T = linear(ph.softround_temperature[0], ph.softround_temperature[1], cnt, n)
+            nz = linear(ph.noise_parameter[0], ph.noise_parameter[1], cnt, n)
+    of.latents.copy_(best_lat)
+    of.params.copy_(best_prm)
+    return best
+
+
+def overfit(arch: Arch, targets: torch.Tensor, lmbda: float, yuv420: bool = True, scale: float = 1.0,
+            seed: int = 0, warmup=C3X_WARMUP, phases=C3X_PHASES) -> tuple[Overfitter, torch.Tensor]:
+    """The c3x encoding schedule (enc/training/warmup.py + train.py phases) for a batch of
+    frames [B, target_len] on one GPU.  Warm-up candidates of every frame train together
+    as one batch; after each warm-up stage each frame keeps its best candidates.
+    Network quantisation (quantize_model) is not run.  Returns (state, best validation)."""
+    dev = targets.device
+    B = targets.shape[0]
+    n0 = warmup[0][0] if warmup else 1
+    g = torch.Generator().manual_seed(seed)
+    params = torch.stack([init_params(arch, g) for _ in range(B * n0)]).to(dev)
+    lat = torch.zeros(B * n0, arch.n_latents, device=dev)
+    of = Overfitter(arch, lat, params, targets.repeat_interleave(n0, dim=0), yuv420=yuv420, seed=seed)
+    ncand = n0
+    for i, (_, ph) in enumerate(warmup):
+        res = run_phase(of, ph, lmbda, scale)
+        keep = warmup[i + 1][0] if i + 1 < len(warmup) else 1
+        order = torch.argsort(res[:, 0].view(B, ncand), dim=1)[:, :keep]
+        idx = (order + torch.arange(B, device=order.device)[:, None] * ncand).reshape(-1)
+        of.keep(idx)
+        ncand = keep
+    best = None
+    for ph in phases:
+        best = run_phase(of, ph, lmbda, scale)
+    return of, best
+
+
+__all__ = ["Arch", "Overfitter", "Phase", "C3X_WARMUP", "C3X_PHASES", "c3x_iterations", "run_phase", "overfit",
+           "init_params", "pack_params", "cosine_lr", "linear", "Q_TYPES", "NOISE_TYPES"]

@@ -916,7 +916,7 @@ __global__ __launch_bounds__(kT) void t_sumsq(const float *__restrict__ G, int64
 
 struct AdamArgs {
     float lr_bc1, inv_sqrt_bc2, beta1, beta2, eps, clip;
-    int N;
+    int N, latents_only;
     int64_t n, gstride, ls, ps, ms;
 };
 
@@ -926,7 +926,7 @@ __global__ void t_adam(const float *__restrict__ G, float *__restrict__ lat, flo
 {
     const int b = blockIdx.y;
     const int64_t i = (int64_t)blockIdx.x * kT + threadIdx.x;
-    if (i >= A.n) return;
+    if (i >= A.n || (A.latents_only && i >= A.N)) return;
     float coef = 1.f;
     if (A.clip > 0.f) coef = fminf(A.clip / (sqrtf(acc4[b * 4 + 2]) + 1e-6f), 1.f);
     const float g = G[(int64_t)b * A.gstride + i] * coef;
@@ -1329,7 +1329,8 @@ extern "C" int ccmi_train_step(const ccmi_train_args *a, void *stream)
     if (a->loss_out) hipLaunchKernelGGL(t_finish, dim3(1), dim3(std::max(64, B)), 0, s, acc4, 1.f / total, lam_px, a->loss_out, B);
     if (a->update) {
         const double bc1 = 1.0 - std::pow((double)a->beta1, a->step), bc2 = 1.0 - std::pow((double)a->beta2, a->step);
-        AdamArgs A{(float)(a->lr / bc1), (float)(1.0 / std::sqrt(bc2)), a->beta1, a->beta2, a->eps, a->clip, g.N, GS, GS,
+        AdamArgs A{(float)(a->lr / bc1), (float)(1.0 / std::sqrt(bc2)), a->beta1, a->beta2, a->eps, a->clip, g.N,
+                   a->update == 2 ? 1 : 0, GS, GS,
                    a->latent_stride, a->param_stride, (int64_t)a->latent_stride + a->param_stride};
         hipLaunchKernelGGL(t_adam, grid1(GS, B), dim3(kT), 0, s, G, a->latent, a->params, a->adam_m, a->adam_v, acc4, A);
     }

@@ -336,7 +336,8 @@ typedef struct ccmi_train_args {
     const float *noise_in;  /* optional [batch][latent_stride]: additive noise used as is */
     float *grad_out;        /* optional [batch][N + P]: raw gradients (before clipping) */
     float *loss_out;        /* optional [batch][4]: loss, mse, rate_bits, grad_norm */
-    int update;             /* 0: loss and gradients only (no clip, no Adam) */
+    int update;             /* 0: loss and gradients only; 1: Adam on everything; 2: Adam on the
+                               latents only (optimized_module ["latent"]; the norm still covers all) */
     void *workspace;        /* ccmi_train_workspace_bytes() */
     size_t workspace_bytes;
 } ccmi_train_args;

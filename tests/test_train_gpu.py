@@ -165,3 +165,26 @@ def test_gpu_overfit_reduces_loss(gpu):
     torch.cuda.synchronize()
     assert torch.isfinite(last).all()
     assert float(last[0, 0]) < 0.5 * float(first[0, 0])
+
+
+def test_gpu_c3x_schedule_short(gpu):
+    """The c3x schedule driver (warm-up candidates as one batch, then the three phases) at
+    2 % of its iterations on two 48x64 frames: runs end to end, keeps one network per frame
+    and improves on the initial loss."""
+    from ccmi import train as T
+    arch = T.Arch(48, 64)
+    g = torch.Generator().manual_seed(1)
+    yy, xx = torch.meshgrid(torch.linspace(0, 1, 48), torch.linspace(0, 1, 64), indexing="ij")
+    imgs = []
+    for k in range(2):
+        img = torch.stack([0.5 + 0.3 * torch.sin((4 + k) * xx + 2 * yy), 0.5 + 0.1 * torch.cos(3 * yy), 0.5 + 0.1 * xx])
+        img = (img + 0.01 * torch.randn(img.shape, generator=g)).clamp(0, 1)
+        imgs.append(torch.cat([img[0].reshape(-1), img[1, ::2, ::2].reshape(-1), img[2, ::2, ::2].reshape(-1)]))
+    tg = torch.stack(imgs).to(gpu)
+    of0 = T.Overfitter(arch, torch.zeros(2, arch.n_latents, device=gpu),
+                       torch.stack([T.init_params(arch, torch.Generator().manual_seed(0))] * 2).to(gpu), tg)
+    init = of0.validate(1e-3)
+    of, best = T.overfit(arch, tg, 1e-3, scale=0.02, seed=3)
+    torch.cuda.synchronize()
+    assert of.B == 2 and torch.isfinite(best).all()
+    assert bool((best[:, 0] < init[:, 0]).all())
