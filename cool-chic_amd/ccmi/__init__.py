@@ -28,7 +28,7 @@ EXPORTED = [
     "ccmi_decode_file", "ccmi_decode_batch", "ccmi_decode_output_size", "ccmi_decode_last_timing",
     "ccmi_decode_latents",
     "ccmi_cool_parse", "ccmi_code_wb", "ccmi_decode_wb", "ccmi_code_latent_layer", "ccmi_arm_forward_i32",
-    "ccmi_encode_frame", "ccmi_train_param_count", "ccmi_train_workspace_bytes", "ccmi_train_step",
+    "ccmi_encode_frame", "ccmi_row_reduce_f32", "ccmi_train_param_count", "ccmi_train_workspace_bytes", "ccmi_train_step",
 ]
 
 

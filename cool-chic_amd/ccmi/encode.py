@@ -222,5 +222,49 @@ def encode_frame(frame: CoolFrame, latent, search_counts: bool = False) -> bytes
     return out
 
 
-__all__ = ["CoolDesc", "CoolFrame", "parse", "code_wb", "decode_wb", "code_latent_layer", "arm_forward_i32",
+def write_cool(arch, latent, qm, yuv420: bool = True, bitdepth: int = 8, hls_sig_blksize: int = -16) -> bytes:
+    """Turn a trained, quantize_model-ed frame into a .cool stream (encode.py:221-623,
+    header.py:236-392): latent [N] float (GPU, before gain), qm a ccmi.quantize.QuantizedModel
+    with the ccmi.train parameter layout."""
+    import torch
+    from .quantize import Layout
+    lay = Layout.of(arch)
+    p = np.asarray(qm.params, dtype=np.float32)
+
+    def sent(idx, q):  # the integers cc_code_wb_bac codes: round(v / q_step), exact here
+        return np.round(p[idx] / np.float32(q)).astype(np.int64)
+
+    nn = {
+        "arm_w": sent(lay.arm_w, qm.q_step["arm"][0]), "arm_b": sent(lay.arm_b, qm.q_step["arm"][1]),
+        "ups_w": sent(lay.ups_w, qm.q_step["upsampling"][0]), "ups_b": np.zeros(0, np.int64),
+        "syn_w": sent(lay.syn_w, qm.q_step["synthesis"][0]), "syn_b": sent(lay.syn_b, qm.q_step["synthesis"][1]),
+    }
+    d = CoolDesc()
+    d.h, d.w = arch.sizes[0]
+    d.bitdepth, d.frame_data_type = bitdepth, 1 if yuv420 else 0
+    d.intra_period = d.p_period = d.display_index = 0
+    d.dim_arm, d.n_hidden_arm = arch.dim_arm, arch.n_hidden
+    d.n_ups = d.n_pre = arch.n_grids - 1
+    d.ups_k, d.pre_k = arch.ups_k, arch.pre_k
+    d.n_branches, d.n_syn_layers = 1, len(arch.layers)
+    for i, (n, k, res, relu) in enumerate(arch.layers):
+        d.syn_out[i], d.syn_ks[i] = int(n), int(k)
+        d.syn_type[i] = 16 * int(bool(res)) + int(bool(relu))  # mode index * 16 + non-linearity index
+    d.flow_gain = 1
+    # get_ac_max_val_nn also counts the (zero) upsampling biases the reference keeps
+    d.ac_max_val_nn = int(np.ceil(max(int(np.abs(v).max(initial=0)) for v in nn.values()) + 2))
+    yq = torch.round(latent.detach().float() * arch.gain).to(torch.int32).contiguous()
+    d.ac_max_val_latent = int(yq.abs().max().item()) + 2
+    d.hls_sig_blksize = hls_sig_blksize
+    qi = [qm.q_index["arm"][0], qm.q_index["arm"][1], qm.q_index["upsampling"][0], 0,
+          qm.q_index["synthesis"][0], qm.q_index["synthesis"][1]]
+    ec = [qm.expgol["arm"][0], qm.expgol["arm"][1], qm.expgol["upsampling"][0], 0,
+          qm.expgol["synthesis"][0], qm.expgol["synthesis"][1]]
+    for k in range(6):
+        d.q_step_index[k], d.expgol_count[k] = qi[k], ec[k]
+    d.n_grids = arch.n_grids
+    return encode_frame(CoolFrame(desc=d, nn=nn), yq)
+
+
+__all__ = ["CoolDesc", "CoolFrame", "parse", "write_cool", "code_wb", "decode_wb", "code_latent_layer", "arm_forward_i32",
            "encode_frame", "NN_SLOTS"]

@@ -261,7 +261,7 @@ int ccmi_launch_arm_f32(const ccmi_arm_args *a, hipStream_t s)
         off += a->h[l] * a->w[l];
     }
     g.tile_start[a->n_grids] = tiles;
-    if (a->latent_stride < off || (a->out_stride < off))
+    if ((a->latent_stride != 0 && a->latent_stride < off) || a->out_stride < off)
         return ccmi_set_error(CCMI_ERR_ARG, "arm: stride smaller than the %d latents of a frame", off);
     dim3 grid(tiles, a->batch);
 #define CCMI_ARM_LAUNCH(DD)                                                                                     \

@@ -297,7 +297,7 @@ int ccmi_fwd::ups_pyramid(const ccmi_ups_args *a, hipStream_t s, LevelArgs *last
     int off[CCMI_MAX_GRIDS];
     int total = 0;
     for (int l = 0; l < L; ++l) { off[l] = total; total += a->h[l] * a->w[l]; }
-    if (a->latent_stride < total) return ccmi_set_error(CCMI_ERR_ARG, "ups: latent_stride < %d", total);
+    if (a->latent_stride != 0 && a->latent_stride < total) return ccmi_set_error(CCMI_ERR_ARG, "ups: latent_stride < %d", total);
 
     // workspace layout: stack of level k (1..L-2) for all frames: [batch][L-k][h_k][w_k]
     float *ws_base = static_cast<float *>(a->workspace);

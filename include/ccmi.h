@@ -54,7 +54,7 @@ int ccmi_device_count(void);
  * params per frame, float32: for each hidden layer l < n_hidden: W_l [d][d] (out,in)
  * then b_l [d]; then W_out [2][d], b_out [2]  (= arm.mlp state_dict order). */
 typedef struct ccmi_arm_args {
-    const float *latent;    /* [batch][latent_stride], N = sum h[l]*w[l] used */
+    const float *latent;    /* [batch][latent_stride], N = sum h[l]*w[l] used; stride 0: shared */
     int64_t latent_stride;
     int n_grids;
     int h[CCMI_MAX_GRIDS_PUBLIC];
@@ -207,6 +207,12 @@ int ccmi_decode_last_timing(float *ms4);
 /* The integer latents of one intra stream (ARM + CABAC decode on the GPU; values, not
  * shifted), grids flattened in order: out needs sum_l h_l * w_l int32 (host buffer). */
 int ccmi_decode_latents(const uint8_t *stream, size_t len, int32_t *out, size_t cap, void *stream_handle);
+
+/* Row reductions for batched evaluation (quantize_model search, validation):
+ * mode 0: out[b] = sum_i a[b][i];  mode 1: out[b] = sum_i (a[b][i] - t[b][i])^2, t_stride
+ * 0 = one target for every row.  Accumulated in double.  Device pointers. */
+int ccmi_row_reduce_f32(const float *a, int64_t a_stride, const float *t, int64_t t_stride, int64_t len, int batch,
+                        int mode, double *out, void *stream);
 
 /* Byte size of the decoded output of one stream (header parse only). */
 int ccmi_decode_output_size(const uint8_t *stream, size_t len, int out_bitdepth,
