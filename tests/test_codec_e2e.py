@@ -60,6 +60,12 @@ def test_gpu_encode_quantize_write_decode(gpu, oracle_c, tmp_path):
     p.write_bytes(stream)
     assert oracle_c.cco_decode_file(str(p).encode(), str(tmp_path / "o.yuv").encode(), 0, 0, 0) == 0
     assert y_gpu == (tmp_path / "o.yuv").read_bytes()
+    ref = Path(__file__).resolve().parents[1] / "oracle" / "_ref" / "ccdec_ref"
+    if ref.exists():  # the reference decoder itself, compiled from its sources (oracle/Makefile)
+        import subprocess
+        subprocess.run([str(ref), f"--input={p}", f"--output={tmp_path / 'r.yuv'}"], check=True,
+                       stdout=subprocess.DEVNULL)
+        assert y_gpu == (tmp_path / "r.yuv").read_bytes()
     # quality: decoded 8-bit picture vs the float eval of the quantised model
     dec = torch.frombuffer(bytearray(y_gpu), dtype=torch.uint8).float() / 255
     mse_dec = float(((dec - tgt[0].cpu()) ** 2).mean())
