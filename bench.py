@@ -350,7 +350,7 @@ def main():
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--batch", type=int, default=8, help="720p frames per step per GPU")
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--decode-reps", type=int, default=8, help="class-E stream copies for the bit-exact decode leg")
+    ap.add_argument("--decode-reps", type=int, default=64, help="class-E stream copies for the bit-exact decode leg")
     ap.add_argument("--staged", action="store_true",
                     help="run upsampling / synthesis / post as separate kernels (module-boundary path)")
     ap.add_argument("--encode-images", type=int, default=8, help="frames overfitted together per GPU (0: skip)")

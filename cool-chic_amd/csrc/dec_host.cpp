@@ -6,6 +6,7 @@
 // :673-857 (cc_decode_* driver, output formats).  All latent-layer decoding, upsampling,
 // synthesis and output conversion run on the GPU (dec_kernels.hip).
 #include <stdio.h>
+#include <stdlib.h>
 #include <string.h>
 
 #include <algorithm>
@@ -350,6 +351,11 @@ int decode_many(const uint8_t *const *streams, const size_t *lens, int n, uint8_
     }
     const size_t desc_off = tot;
     tot += align_up(sizeof(ArmStreamDesc) * (size_t)n * CCMI_MAX_GRIDS, 256);
+    // batched-tail argument tables: bounded by one single-frame table per frame
+    size_t tail_cap = 0;
+    for (int i = 0; i < n; ++i) tail_cap += dec_tail_table_bytes(fr[i].n_layers, 1);
+    const size_t tail_off = tot;
+    tot += align_up(tail_cap, 256);
 #if defined(CCMI_ARM_STAMPS)
     const size_t dbg_off = tot;
     tot += align_up(8 * 8 * (size_t)n * CCMI_MAX_GRIDS, 256);
@@ -439,21 +445,16 @@ int decode_many(const uint8_t *const *streams, const size_t *lens, int n, uint8_
     if (!all.empty())
         CCMI_HIP_CHECK(hipMemcpyAsync(dev + desc_off, all.data(), all.size() * sizeof(ArmStreamDesc),
                                       hipMemcpyHostToDevice, s));
-    ev.rec(1, s);
-    if (!all.empty()) {
-        for (auto &g : groups) {
-            const ArmStreamDesc *dd = reinterpret_cast<const ArmStreamDesc *>(dev + desc_off) + dpos;
-            if (int rc = launch_dec_arm(dd, (int)g.second.size(), max_w, max_blocks, g.first.d, g.first.nh, s)) return rc;
-            dpos += g.second.size();
-        }
-    }
 
-    ev.rec(2, s);
-    // ---- per frame: upsampling, synthesis (+ blend), output bytes
+    // ---- decoder tail arguments; frames of one geometry with a fused synthesis (single
+    // branch) share one launch per stage (CCMI_DEC_TAIL_SERIAL=1: one frame at a time)
+    std::vector<DecTailFrame> tail(n);
     for (int i = 0; i < n; ++i) {
         FrameHost &f = fr[i];
         DevPlan &p = pl[i];
-        DecUpsArgs ua{};
+        DecTailFrame &t = tail[i];
+        DecUpsArgs &ua = t.ups;
+        ua = DecUpsArgs{};
         ua.lat = reinterpret_cast<const int32_t *>(dev + p.lat_off);
         ua.n_layers = f.n_layers;
         int off = 0;
@@ -470,23 +471,75 @@ int decode_many(const uint8_t *const *streams, const size_t *lens, int n, uint8_
         ua.n_pre = f.n_pre;
         ua.workspace = reinterpret_cast<int32_t *>(dev + p.ws_off);
         ua.out = reinterpret_cast<int32_t *>(dev + p.dense_off);
-        if (int rc = launch_dec_ups(ua, s)) return rc;
+        DecSynArgs &sa = t.syn;
+        sa = DecSynArgs{};
+        sa.in = ua.out;
+        sa.c_in = f.n_layers;
+        sa.h = f.h;
+        sa.w = f.w;
+        sa.n_layers = (int)f.layers.size();
+        for (int l = 0; l < sa.n_layers; ++l) sa.layers[l] = f.layers[l];
+        sa.params = reinterpret_cast<const int32_t *>(dev + p.syn_off);
+        sa.out = reinterpret_cast<int32_t *>(dev + p.synout_off);
+        sa.workspace = reinterpret_cast<int32_t *>(dev + p.synws_off);
+        t.bitdepth = of[i].bitdepth;
+        t.kind = of[i].kind;
+        t.dst = dev + p.out_off;
+    }
+    static const bool tail_serial = getenv("CCMI_DEC_TAIL_SERIAL") != nullptr;
+    std::vector<std::vector<int>> tgroups;
+    std::vector<char> batched(n, 0);
+    for (int i = 0; i < n && !tail_serial; ++i) {
+        if (fr[i].n_branches != 1 || !dec_tail_batchable(tail[i])) continue;
+        auto it = std::find_if(tgroups.begin(), tgroups.end(), [&](const std::vector<int> &g) {
+            return g.size() < 65535 && dec_tail_same_group(tail[g[0]], tail[i]);
+        });
+        if (it == tgroups.end()) {
+            tgroups.emplace_back();
+            it = tgroups.end() - 1;
+        }
+        it->push_back(i);
+        batched[i] = 1;
+    }
+    std::vector<size_t> tg_off(tgroups.size());
+    std::vector<uint8_t> tab(tail_cap > 0 ? tail_cap : 1);
+    size_t tpos = 0;
+    for (size_t g = 0; g < tgroups.size(); ++g) {
+        std::vector<const DecTailFrame *> ptr;
+        for (int i : tgroups[g]) ptr.push_back(&tail[i]);
+        tg_off[g] = tpos;
+        dec_tail_fill(ptr.data(), (int)ptr.size(), tab.data() + tpos);
+        tpos += dec_tail_table_bytes(tail[tgroups[g][0]].ups.n_layers, (int)ptr.size());
+    }
+    if (tpos) CCMI_HIP_CHECK(hipMemcpyAsync(dev + tail_off, tab.data(), tpos, hipMemcpyHostToDevice, s));
+    ev.rec(1, s);
+    if (!all.empty()) {
+        for (auto &g : groups) {
+            const ArmStreamDesc *dd = reinterpret_cast<const ArmStreamDesc *>(dev + desc_off) + dpos;
+            if (int rc = launch_dec_arm(dd, (int)g.second.size(), max_w, max_blocks, g.first.d, g.first.nh, s)) return rc;
+            dpos += g.second.size();
+        }
+    }
+
+    ev.rec(2, s);
+    // ---- upsampling, synthesis (+ blend), output bytes: batched groups, then the rest per frame
+    for (size_t g = 0; g < tgroups.size(); ++g)
+        if (int rc = launch_dec_tail_batch(tail[tgroups[g][0]], (int)tgroups[g].size(), dev + tail_off + tg_off[g], s))
+            return rc;
+    for (int i = 0; i < n; ++i) {
+        if (batched[i]) continue;
+        FrameHost &f = fr[i];
+        DevPlan &p = pl[i];
+        if (int rc = launch_dec_ups(tail[i].ups, s)) return rc;
 
         const int nout = f.layers.back().n_out;
         const int64_t plane = (int64_t)f.h * f.w;
         size_t per_branch = f.syn.size() / f.n_branches;
         int32_t *synout = reinterpret_cast<int32_t *>(dev + p.synout_off);
         for (int b = 0; b < f.n_branches; ++b) {
-            DecSynArgs sa{};
-            sa.in = ua.out;
-            sa.c_in = f.n_layers;
-            sa.h = f.h;
-            sa.w = f.w;
-            sa.n_layers = (int)f.layers.size();
-            for (int l = 0; l < sa.n_layers; ++l) sa.layers[l] = f.layers[l];
-            sa.params = reinterpret_cast<const int32_t *>(dev + p.syn_off) + per_branch * b;
+            DecSynArgs sa = tail[i].syn;
+            sa.params += per_branch * b;
             sa.out = synout + (size_t)b * nout * plane;
-            sa.workspace = reinterpret_cast<int32_t *>(dev + p.synws_off);
             if (int rc = launch_dec_syn(sa, s)) return rc;
             if (b >= 1) // run_syn (cc-frame-decoder.cpp:1044-1149): blends on 3 planes
                 if (int rc = launch_dec_blend(synout, synout + (size_t)b * nout * plane, 3 * plane,

@@ -97,4 +97,21 @@ int launch_dec_blend(int32_t *acc, const int32_t *x, int64_t n, int32_t b_acc, i
 // kind: 0 yuv420, 1 yuv444, 2 ppm payload (interleaved RGB).  bps = 1 or 2 bytes/sample.
 int launch_dec_output(const int32_t *syn, int h, int w, int bitdepth, int kind, uint8_t *dst, hipStream_t s);
 
+// Batched decoder tail: frames with the same geometry and a fused-synthesis architecture
+// (single branch) share one launch per pyramid step, one synthesis and one output launch
+// (grid.y = frame) instead of ~8 launches per frame.  The per-frame argument tables live
+// in device memory: dec_tail_table_bytes() sizes them, dec_tail_fill() writes them on the
+// host (device pointers inside), the caller uploads them, launch_dec_tail_batch() runs.
+struct DecTailFrame {
+    DecUpsArgs ups;
+    DecSynArgs syn;
+    int bitdepth, kind;
+    uint8_t *dst;
+};
+bool dec_tail_batchable(const DecTailFrame &f);
+bool dec_tail_same_group(const DecTailFrame &a, const DecTailFrame &b);
+size_t dec_tail_table_bytes(int n_layers, int n);
+void dec_tail_fill(const DecTailFrame *const *fr, int n, void *host_tab);
+int launch_dec_tail_batch(const DecTailFrame &f0, int n, const void *dev_tab, hipStream_t s);
+
 } // namespace ccmi

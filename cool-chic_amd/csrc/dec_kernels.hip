@@ -614,10 +614,26 @@ struct DecLevel {
     int tiles_x;
 };
 
+__device__ __forceinline__ void ups_level_body(const DecLevel &A, int32_t *s_in, int32_t *s_tmp);
+
 __global__ __launch_bounds__(kThreads) void dec_ups_level(DecLevel A)
 {
     __shared__ int32_t s_in[(kTY + kMaxKs) * (kTX + kMaxKs)];
     __shared__ int32_t s_tmp[(kTY + kMaxKs) * kTX];
+    ups_level_body(A, s_in, s_tmp);
+}
+
+// frames of a batch (identical geometry): blockIdx.y = frame
+__global__ __launch_bounds__(kThreads) void dec_ups_level_batch(const DecLevel *__restrict__ As)
+{
+    __shared__ int32_t s_in[(kTY + kMaxKs) * (kTX + kMaxKs)];
+    __shared__ int32_t s_tmp[(kTY + kMaxKs) * kTX];
+    const DecLevel A = As[blockIdx.y];
+    ups_level_body(A, s_in, s_tmp);
+}
+
+__device__ __forceinline__ void ups_level_body(const DecLevel &A, int32_t *s_in, int32_t *s_tmp)
+{
     const int y0 = (blockIdx.x / A.tiles_x) * kTY;
     const int x0 = (blockIdx.x % A.tiles_x) * kTX;
     const int tid = threadIdx.x;
@@ -706,9 +722,26 @@ struct DecSynFused {
 };
 
 template <int CIN, int CMID>
+__device__ __forceinline__ void syn_fused_body(const DecSynFused &A, int32_t (*s_buf)[CMID][kRegion]);
+
+template <int CIN, int CMID>
 __global__ __launch_bounds__(kThreads) void dec_syn_fused(DecSynFused A)
 {
     __shared__ int32_t s_buf[2][CMID][kRegion];
+    syn_fused_body<CIN, CMID>(A, s_buf);
+}
+
+template <int CIN, int CMID>
+__global__ __launch_bounds__(kThreads) void dec_syn_fused_batch(const DecSynFused *__restrict__ As)
+{
+    __shared__ int32_t s_buf[2][CMID][kRegion];
+    const DecSynFused A = As[blockIdx.y];
+    syn_fused_body<CIN, CMID>(A, s_buf);
+}
+
+template <int CIN, int CMID>
+__device__ __forceinline__ void syn_fused_body(const DecSynFused &A, int32_t (*s_buf)[CMID][kRegion])
+{
     const int halo = A.n_sp;
     const int TX = kRW - 2 * halo, TY = kRH - 2 * halo;
     const int y0 = (blockIdx.x / A.tiles_x) * TY, x0 = (blockIdx.x % A.tiles_x) * TX;
@@ -850,8 +883,29 @@ __global__ __launch_bounds__(kThreads) void dec_blend_kernel(int32_t *acc, const
 }
 
 // ------------------------------------------------------------------ output bytes
+struct DecOut {
+    const int32_t *syn;
+    int H, W, maxv, kind, bps;
+    uint8_t *dst;
+};
+
+__device__ __forceinline__ void output_body(const int32_t *__restrict__ syn, int H, int W, int maxv, int kind, int bps,
+                                            uint8_t *__restrict__ dst);
+
 __global__ __launch_bounds__(kThreads) void dec_output_kernel(const int32_t *__restrict__ syn, int H, int W, int maxv,
                                                               int kind, int bps, uint8_t *__restrict__ dst)
+{
+    output_body(syn, H, W, maxv, kind, bps, dst);
+}
+
+__global__ __launch_bounds__(kThreads) void dec_output_batch(const DecOut *__restrict__ Os)
+{
+    const DecOut O = Os[blockIdx.y];
+    output_body(O.syn, O.H, O.W, O.maxv, O.kind, O.bps, O.dst);
+}
+
+__device__ __forceinline__ void output_body(const int32_t *__restrict__ syn, int H, int W, int maxv, int kind, int bps,
+                                            uint8_t *__restrict__ dst)
 {
     const int64_t plane = (int64_t)H * W;
     const int64_t p = (int64_t)blockIdx.x * kThreads + threadIdx.x;
@@ -927,11 +981,15 @@ size_t dec_ups_workspace_elems(const int *lh, const int *lw, int L)
     return n;
 }
 
-int launch_dec_ups(const DecUpsArgs &a, hipStream_t s)
+static bool ups_ks_ok(const DecUpsArgs &a)
+{
+    return a.ups_ks >= 2 && a.ups_ks <= kMaxKs && a.pre_ks >= 1 && a.pre_ks <= kMaxKs - 1;
+}
+
+// kernel arguments of every pyramid step of one frame (coarsest first); returns the step count
+static int make_levels(const DecUpsArgs &a, DecLevel *lv)
 {
     const int L = a.n_layers;
-    if (a.ups_ks < 2 || a.ups_ks > kMaxKs || a.pre_ks < 1 || a.pre_ks > kMaxKs - 1)
-        return ccmi_set_error(CCMI_ERR_UNSUPPORTED, "dec: upsampling kernel sizes %d/%d", a.ups_ks, a.pre_ks);
     int32_t *stack[CCMI_MAX_GRIDS] = {};
     int32_t *ws = a.workspace;
     for (int k = 1; k <= L - 2; ++k) {
@@ -940,7 +998,8 @@ int launch_dec_ups(const DecUpsArgs &a, hipStream_t s)
     }
     for (int step = 0; step < L - 1; ++step) {
         const int k = L - 1 - step;
-        DecLevel A{};
+        DecLevel &A = lv[step];
+        A = DecLevel{};
         A.src = k == L - 1 ? a.lat + a.off[k] : stack[k];
         A.C = L - k;
         A.hs = a.lh[k];
@@ -956,6 +1015,18 @@ int launch_dec_ups(const DecUpsArgs &a, hipStream_t s)
         A.kpre = a.kernels + a.n_ups * a.ups_ks + ((L - 2 - (k - 1)) % a.n_pre) * a.pre_ks;
         A.ks = a.pre_ks;
         A.tiles_x = ccmi_div_up(A.wd, kTX);
+    }
+    return L > 1 ? L - 1 : 0;
+}
+
+int launch_dec_ups(const DecUpsArgs &a, hipStream_t s)
+{
+    if (!ups_ks_ok(a))
+        return ccmi_set_error(CCMI_ERR_UNSUPPORTED, "dec: upsampling kernel sizes %d/%d", a.ups_ks, a.pre_ks);
+    DecLevel lv[CCMI_MAX_GRIDS];
+    const int steps = make_levels(a, lv);
+    for (int step = 0; step < steps; ++step) {
+        const DecLevel &A = lv[step];
         hipLaunchKernelGGL(dec_ups_level, dim3(A.tiles_x * ccmi_div_up(A.hd, kTY)), dim3(kThreads), 0, s, A);
         CCMI_HIP_CHECK(hipGetLastError());
     }
@@ -1082,6 +1153,122 @@ int launch_dec_output(const int32_t *syn, int h, int w, int bitdepth, int kind, 
     const int64_t plane = (int64_t)h * w;
     hipLaunchKernelGGL(dec_output_kernel, dim3((unsigned)((plane + kThreads - 1) / kThreads)), dim3(kThreads), 0, s,
                        syn, h, w, (1 << bitdepth) - 1, kind, bitdepth <= 8 ? 1 : 2, dst);
+    CCMI_HIP_CHECK(hipGetLastError());
+    return CCMI_OK;
+}
+
+// ------------------------------------------------------------------ batched decoder tail
+// fused-synthesis kernel arguments of one frame (syn_fast architectures only); the same
+// weight walk as launch_dec_syn
+static DecSynFused make_syn_fused(const DecSynArgs &a)
+{
+    const int32_t *wp[CCMI_MAX_SYN_LAYERS], *bp[CCMI_MAX_SYN_LAYERS];
+    const int32_t *q = a.params;
+    int c = a.c_in;
+    for (int l = 0; l < a.n_layers; ++l) {
+        wp[l] = q;
+        q += (size_t)a.layers[l].n_out * c * a.layers[l].ks * a.layers[l].ks;
+        bp[l] = q;
+        q += a.layers[l].n_out;
+        c = a.layers[l].n_out;
+    }
+    DecSynFused F{};
+    F.in = a.in;
+    F.cin = a.c_in;
+    F.H = a.h;
+    F.W = a.w;
+    F.hid = a.layers[0].n_out;
+    F.w0 = wp[0];
+    F.b0 = bp[0];
+    F.w1 = wp[1];
+    F.b1 = bp[1];
+    F.n_sp = a.n_layers - 2;
+    for (int i = 0; i < F.n_sp; ++i) {
+        F.wsp[i] = wp[2 + i];
+        F.bsp[i] = bp[2 + i];
+        F.res[i] = a.layers[2 + i].residual;
+        F.relu[i] = a.layers[2 + i].relu;
+    }
+    F.out = a.out;
+    F.tiles_x = ccmi_div_up(a.w, kRW - 2 * F.n_sp);
+    return F;
+}
+
+bool dec_tail_batchable(const DecTailFrame &f)
+{
+    int cm;
+    return f.ups.n_layers >= 2 && ups_ks_ok(f.ups) && f.syn.c_in == f.ups.n_layers && syn_fast(f.syn, &cm);
+}
+
+// launch geometry only: the grids depend on the plane sizes, the synthesis halo and the
+// synthesis input width (template); everything else is per-frame table data
+bool dec_tail_same_group(const DecTailFrame &a, const DecTailFrame &b)
+{
+    if (a.ups.n_layers != b.ups.n_layers) return false;
+    for (int l = 0; l < a.ups.n_layers; ++l)
+        if (a.ups.lh[l] != b.ups.lh[l] || a.ups.lw[l] != b.ups.lw[l]) return false;
+    return a.syn.n_layers == b.syn.n_layers && a.syn.c_in == b.syn.c_in && a.syn.h == b.syn.h && a.syn.w == b.syn.w;
+}
+
+static size_t al16(size_t x) { return (x + 15) & ~(size_t)15; }
+
+// table of a group of n frames: [step][frame] DecLevel, [frame] DecSynFused, [frame] DecOut
+size_t dec_tail_table_bytes(int n_layers, int n)
+{
+    const size_t steps = n_layers > 1 ? (size_t)(n_layers - 1) : 0;
+    return al16(sizeof(DecLevel) * steps * n) + al16(sizeof(DecSynFused) * (size_t)n) + al16(sizeof(DecOut) * (size_t)n);
+}
+
+void dec_tail_fill(const DecTailFrame *const *fr, int n, void *host_tab)
+{
+    const int steps = fr[0]->ups.n_layers - 1;
+    uint8_t *p = static_cast<uint8_t *>(host_tab);
+    DecLevel *lv = reinterpret_cast<DecLevel *>(p);
+    DecSynFused *sf = reinterpret_cast<DecSynFused *>(p + al16(sizeof(DecLevel) * (size_t)steps * n));
+    DecOut *oo = reinterpret_cast<DecOut *>(reinterpret_cast<uint8_t *>(sf) + al16(sizeof(DecSynFused) * (size_t)n));
+    for (int i = 0; i < n; ++i) {
+        DecLevel tmp[CCMI_MAX_GRIDS];
+        make_levels(fr[i]->ups, tmp);
+        for (int st = 0; st < steps; ++st) lv[(size_t)st * n + i] = tmp[st];
+        sf[i] = make_syn_fused(fr[i]->syn);
+        const DecSynArgs &sa = fr[i]->syn;
+        const int bd = fr[i]->bitdepth;
+        oo[i] = DecOut{sa.out, sa.h, sa.w, (1 << bd) - 1, fr[i]->kind, bd <= 8 ? 1 : 2, fr[i]->dst};
+    }
+}
+
+int launch_dec_tail_batch(const DecTailFrame &f0, int n, const void *dev_tab, hipStream_t s)
+{
+    if (n < 1 || n > 65535) return ccmi_set_error(CCMI_ERR_ARG, "dec: tail batch of %d frames", n);
+    const int L = f0.ups.n_layers, steps = L - 1;
+    const uint8_t *p = static_cast<const uint8_t *>(dev_tab);
+    const DecLevel *lv = reinterpret_cast<const DecLevel *>(p);
+    const DecSynFused *sf = reinterpret_cast<const DecSynFused *>(p + al16(sizeof(DecLevel) * (size_t)steps * n));
+    const DecOut *oo =
+        reinterpret_cast<const DecOut *>(reinterpret_cast<const uint8_t *>(sf) + al16(sizeof(DecSynFused) * (size_t)n));
+    for (int st = 0; st < steps; ++st) {
+        const int k = L - 1 - st;
+        const int hd = f0.ups.lh[k - 1], wd = f0.ups.lw[k - 1];
+        const dim3 grid(ccmi_div_up(wd, kTX) * ccmi_div_up(hd, kTY), n);
+        hipLaunchKernelGGL(dec_ups_level_batch, grid, dim3(kThreads), 0, s, lv + (size_t)st * n);
+        CCMI_HIP_CHECK(hipGetLastError());
+    }
+    const int halo = f0.syn.n_layers - 2;
+    const dim3 sg(ccmi_div_up(f0.syn.w, kRW - 2 * halo) * ccmi_div_up(f0.syn.h, kRH - 2 * halo), n);
+    switch (f0.syn.c_in) {
+    case 1: hipLaunchKernelGGL((dec_syn_fused_batch<1, 3>), sg, dim3(kThreads), 0, s, sf); break;
+    case 2: hipLaunchKernelGGL((dec_syn_fused_batch<2, 3>), sg, dim3(kThreads), 0, s, sf); break;
+    case 3: hipLaunchKernelGGL((dec_syn_fused_batch<3, 3>), sg, dim3(kThreads), 0, s, sf); break;
+    case 4: hipLaunchKernelGGL((dec_syn_fused_batch<4, 3>), sg, dim3(kThreads), 0, s, sf); break;
+    case 5: hipLaunchKernelGGL((dec_syn_fused_batch<5, 3>), sg, dim3(kThreads), 0, s, sf); break;
+    case 6: hipLaunchKernelGGL((dec_syn_fused_batch<6, 3>), sg, dim3(kThreads), 0, s, sf); break;
+    case 7: hipLaunchKernelGGL((dec_syn_fused_batch<7, 3>), sg, dim3(kThreads), 0, s, sf); break;
+    default: hipLaunchKernelGGL((dec_syn_fused_batch<8, 3>), sg, dim3(kThreads), 0, s, sf); break;
+    }
+    CCMI_HIP_CHECK(hipGetLastError());
+    const int64_t plane = (int64_t)f0.syn.h * f0.syn.w;
+    hipLaunchKernelGGL(dec_output_batch, dim3((unsigned)((plane + kThreads - 1) / kThreads), n), dim3(kThreads), 0, s,
+                       oo);
     CCMI_HIP_CHECK(hipGetLastError());
     return CCMI_OK;
 }

@@ -40,6 +40,17 @@ def test_hip_decode_batch_bit_exact(gpu, ccmi_lib):
 
 
 @pytest.mark.gpu
+def test_hip_decode_batch_repeated_streams(gpu, ccmi_lib):
+    """Copies of the same streams in one call: the batched decoder tail runs each geometry
+    as one group (grid.y = frame); every copy stays bit-exact."""
+    from ccmi import decode
+    fs = [f for f in FILES if f.name[:2] in ("E-", "D-")][:6]
+    outs = decode.decode_batch([f.read_bytes() for f in fs] * 3)
+    for f, o in zip(fs * 3, outs):
+        assert hashlib.md5(o).hexdigest() == MD5[_key(f)]["md5"], f.name
+
+
+@pytest.mark.gpu
 @pytest.mark.parametrize("bd,chroma,ext", [(10, 420, ".yuv"), (8, 444, ".yuv"), (10, 444, ".yuv"), (8, 0, ".ppm"),
                                            (16, 0, ".ppm")])
 def test_hip_output_variants_match_oracle(bd, chroma, ext, gpu, ccmi_lib, oracle_c, tmp_path):
