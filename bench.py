@@ -355,8 +355,11 @@ def main():
                     help="run upsampling / synthesis / post as separate kernels (module-boundary path)")
     ap.add_argument("--encode-images", type=int, default=8, help="frames overfitted together per GPU (0: skip)")
     ap.add_argument("--encode-scale", type=float, default=1.0, help="fraction of the c3x schedule to run")
-    ap.add_argument("--serial", action="store_true",
-                    help="one stream: no overlap of the ARM with the decode tail")
+    ap.add_argument("--overlap", action="store_true",
+                    help="run the ARM on a second HIP stream concurrently with the decode tail (the "
+                         "step rate is the same within noise on MI355X; kernels then share CUs, so the "
+                         "roofline kernel's duration is no longer its own)")
+    ap.add_argument("--serial", action="store_true", help="(default) one stream, kernels back to back")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -376,7 +379,7 @@ def main():
 
     mode = "staged" if args.staged else "fused"
     names = Pipeline.STAGES[mode]
-    overlap = not args.serial
+    overlap = args.overlap and not args.serial
     for _ in range(args.warmup):
         pipe.step(mode=mode, overlap=overlap)
     torch.cuda.synchronize()

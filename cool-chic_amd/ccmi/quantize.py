@@ -93,6 +93,7 @@ class QuantizedModel:
     q_index: dict = field(default_factory=dict)  # module -> (weight index, bias index)
     q_step: dict = field(default_factory=dict)   # module -> (weight step, bias step)
     expgol: dict = field(default_factory=dict)   # module -> (weight count, bias count)
+    nn_bits: dict = field(default_factory=dict)  # module -> Exp-Golomb bits of its weights + biases
     loss: float = 0.0
 
 
@@ -245,9 +246,26 @@ def quantize_model(arch: Arch, latent: torch.Tensor, params: torch.Tensor, targe
         res.q_index[module] = (iw, ib)
         res.q_step[module] = (qw, qb)
         res.expgol[module] = counts[k]
+        res.nn_bits[module] = float(nn_rate[k])
         res.loss = float(loss[k])
     res.params = cur
     return res
 
 
-__all__ = ["quantize_model", "QuantizedModel", "Layout", "POSSIBLE_Q_STEP", "exp_golomb_nbins", "best_count"]
+def evaluate(arch: Arch, latent: torch.Tensor, params: torch.Tensor, target: torch.Tensor, yuv420: bool = True,
+             bitdepth: int = 8) -> tuple[float, float]:
+    """test() of enc/training/test.py:370-438 for one frame, on the GPU: MSE of the eval
+    forward (hard-rounded latents, output on the 2^bitdepth - 1 grid, 420 subsampling) and
+    the latent rate in bits.  The network rate of a quantised model is
+    QuantizedModel.nn_bits."""
+    lay = Layout.of(arch)
+    ev = _Eval(arch, latent.float(), target.float(), yuv420, bitdepth)
+    p = params.detach().float().reshape(1, -1).to(ev.dev).contiguous()
+    rate = float(ev.rate_sum(p)[0])
+    dense = ev.dense(_full_kernels(arch, p, lay))
+    mse = float(ev.mse(dense, p[:, lay.syn_off:].contiguous())[0])
+    return mse, rate
+
+
+__all__ = ["quantize_model", "QuantizedModel", "Layout", "POSSIBLE_Q_STEP", "exp_golomb_nbins", "best_count",
+           "evaluate"]

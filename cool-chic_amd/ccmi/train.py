@@ -256,6 +256,18 @@ C3X_PHASES = [
 ]
 
 
+# preset "debug" (enc/training/presets.py:380-432): the schedule of the reference's sanity check
+DEBUG_WARMUP = [(3, Phase(max_itr=10)), (2, Phase(max_itr=10))]
+DEBUG_PHASES = [
+    Phase(lr=1e-2, max_itr=50, patience=100000, schedule_lr=True, quantizer_noise_type="gaussian",
+          softround_temperature=(0.3, 0.1), noise_parameter=(0.25, 0.1)),
+    Phase(lr=1e-4, max_itr=10, patience=10, quantizer_type="ste", quantizer_noise_type="none", quantize_model=True,
+          softround_temperature=(1e-4, 1e-4)),
+    Phase(lr=1e-4, max_itr=10, patience=50, optimized_module="latent", freq_valid=5, quantizer_type="ste",
+          quantizer_noise_type="none", softround_temperature=(1e-4, 1e-4)),
+]
+
+
 def c3x_iterations(scale: float = 1.0) -> int:
     """Training iterations per image of the c3x preset (x scale): warm-up candidates
     trained in parallel count once per surviving image."""
@@ -295,11 +307,14 @@ def run_phase(of: Overfitter, ph: Phase, lmbda: float, scale: float = 1.0) -> to
 
 
 def overfit(arch: Arch, targets: torch.Tensor, lmbda: float, yuv420: bool = True, scale: float = 1.0,
-            seed: int = 0, warmup=C3X_WARMUP, phases=C3X_PHASES) -> tuple[Overfitter, torch.Tensor]:
+            seed: int = 0, warmup=C3X_WARMUP, phases=C3X_PHASES, bitdepth: int = 8) -> tuple[Overfitter, torch.Tensor]:
     """The c3x encoding schedule (enc/training/warmup.py + train.py phases) for a batch of
     frames [B, target_len] on one GPU.  Warm-up candidates of every frame train together
-    as one batch; after each warm-up stage each frame keeps its best candidates.
-    Network quantisation (quantize_model) is not run.  Returns (state, best validation)."""
+    as one batch; after each warm-up stage each frame keeps its best candidates.  After a
+    phase flagged quantize_model, every frame's networks are quantised
+    (ccmi.quantize.quantize_model, as video.py:302-310) and later phases train with them;
+    the per-frame QuantizedModel list is state.quantized (None if no phase asks for it).
+    Returns (state, best validation)."""
     dev = targets.device
     B = targets.shape[0]
     n0 = warmup[0][0] if warmup else 1
@@ -316,10 +331,20 @@ def overfit(arch: Arch, targets: torch.Tensor, lmbda: float, yuv420: bool = True
         of.keep(idx)
         ncand = keep
     best = None
+    of.quantized = None
     for ph in phases:
         best = run_phase(of, ph, lmbda, scale)
+        if ph.quantize_model:
+            from .quantize import quantize_model
+            qms = []
+            for b in range(of.B):
+                qm = quantize_model(arch, of.latents[b], of.params[b], of.targets[b], lmbda, yuv420, bitdepth)
+                of.params[b].copy_(torch.from_numpy(qm.params).to(of.params.device))
+                qms.append(qm)
+            of.quantized = qms
+            best = of.validate(lmbda).clone()
     return of, best
 
 
-__all__ = ["Arch", "Overfitter", "Phase", "C3X_WARMUP", "C3X_PHASES", "c3x_iterations", "run_phase", "overfit",
+__all__ = ["Arch", "Overfitter", "Phase", "C3X_WARMUP", "C3X_PHASES", "DEBUG_WARMUP", "DEBUG_PHASES", "c3x_iterations", "run_phase", "overfit",
            "init_params", "pack_params", "cosine_lr", "linear", "Q_TYPES", "NOISE_TYPES"]

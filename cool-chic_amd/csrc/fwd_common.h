@@ -42,11 +42,7 @@ struct FusedArgs {
     int tiles_x;
     float qmax;          // > 0: write the post-processed frame (2^bitdepth - 1)
     int yuv420;
-    int mfma_head;       // 2-layer head: first layer on the matrix cores (0: packed-VALU form)
 };
-
-// 0 when CCMI_SYN_VALU_HEAD is set (A/B timing of the two head forms), else 1.
-int mfma_head_enabled();
 
 struct Plan {
     bool fused;

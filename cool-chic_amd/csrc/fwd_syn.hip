@@ -19,8 +19,6 @@
 //
 // Any other architecture runs the generic per-layer kernel (one launch per layer,
 // ping-pong through the caller's workspace).
-#include <stdlib.h>
-
 #include <type_traits>
 
 #include "fwd_common.h"
@@ -30,7 +28,6 @@ using namespace ccmi_fwd;
 namespace {
 
 constexpr int kThreads = 256;
-typedef float v4f __attribute__((ext_vector_type(4)));
 
 
 // Fused head + 3x3 tail.  The workgroup's working region is a fixed 32 x 64 window
@@ -140,13 +137,11 @@ __global__ __launch_bounds__(kFThreads) void syn_fused_kernel(FusedArgs A, Level
     const int gx = ox + c;
     const int cxg = clampi(gx, A.W - 1);
 
-    // (rounded up to whole quads of zero units: the MFMA head takes hidden units 4 at a time)
     if (A.n_head == 2)
-        for (int i = threadIdx.x; i < ((A.hid + 3) & ~3) * 16; i += kFThreads) {
+        for (int i = threadIdx.x; i < A.hid * 16; i += kFThreads) {
             const int j = i >> 4, f = i & 15;
             float v = 0.f;
-            if (j >= A.hid) v = 0.f;
-            else if (f < CIN) v = prm[A.w0_off + j * CIN + f];
+            if (f < CIN) v = prm[A.w0_off + j * CIN + f];
             else if (f == CIN) v = prm[A.b0_off + j];
             else if (f <= CIN + CMID) v = prm[A.w1_off + (f - CIN - 1) * A.hid + j];
             s_head[j][f] = v;
@@ -344,58 +339,7 @@ __global__ __launch_bounds__(kFThreads) void syn_fused_kernel(FusedArgs A, Level
         // the raw tiles (region 0) are overwritten by the head output below
         if constexpr (UPS) __syncthreads();
         FSTAMP(2);
-        if (A.n_head == 2 && A.mfma_head) {
-            // First layer on the matrix cores.  v_mfma_f32_4x4x1_16b_f32 treats the wave as
-            // 16 blocks of 4 lanes: lane 4b+i supplies A = w0[4q+i][k] (unit i of hidden quad
-            // q) and B = x_k of its own pixel, and register i of lane 4b+j receives
-            // w0[4q+i][k] * x_k(pixel of lane 4b+j) -- so hidden unit 4q+i of every lane's own
-            // pixel, and pixels stay on their lanes as in the VALU stages around the head.
-            // k runs over the CIN inputs, then the bias against x = 1: an fmaf chain per unit
-            // (f32 MFMA is exact f32).  The second layer (-> CMID) stays on the VALU with the
-            // quad's wave-uniform w1 columns (broadcast LDS reads).
-            const float lo0 = A.relu0 ? 0.f : -INFINITY;
-            float op[NR][CMID];
-#pragma unroll
-            for (int p = 0; p < NR; ++p)
-#pragma unroll
-                for (int m = 0; m < CMID; ++m) op[p][m] = 0.f;
-            __syncthreads(); // s_head staged
-            const int nq = (A.hid + 3) >> 2;
-            const float *arec = s_head[threadIdx.x & 3];
-            for (int q = 0; q < nq; ++q) {
-                const float *ar = arec + q * 64;
-                float a[CIN + 1];
-#pragma unroll
-                for (int k = 0; k <= CIN; ++k) a[k] = ar[k];
-                v4f acc[NR];
-#pragma unroll
-                for (int p = 0; p < NR; ++p) acc[p] = v4f{0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-                for (int k = 0; k < CIN; ++k)
-#pragma unroll
-                    for (int p = 0; p < NR; ++p) acc[p] = __builtin_amdgcn_mfma_f32_4x4x1f32(a[k], x[p][k], acc[p], 0, 0, 0);
-#pragma unroll
-                for (int p = 0; p < NR; ++p) acc[p] = __builtin_amdgcn_mfma_f32_4x4x1f32(a[CIN], 1.f, acc[p], 0, 0, 0);
-#pragma unroll
-                for (int u = 0; u < 4; ++u) {
-                    const float *w1 = s_head[4 * q + u] + CIN + 1;
-                    float w[CMID];
-#pragma unroll
-                    for (int m = 0; m < CMID; ++m) w[m] = w1[m];
-#pragma unroll
-                    for (int p = 0; p < NR; ++p) {
-                        const float hv = fmaxf(acc[p][u], lo0);
-#pragma unroll
-                        for (int m = 0; m < CMID; ++m) op[p][m] = fmaf(w[m], hv, op[p][m]);
-                    }
-                }
-            }
-            const float lo1 = A.relu1 ? 0.f : -INFINITY;
-#pragma unroll
-            for (int p = 0; p < NR; ++p)
-#pragma unroll
-                for (int m = 0; m < CMID; ++m) o[p][m] = fmaxf(op[p][m] + b1[m], lo1);
-        } else if (A.n_head == 2) {
+        if (A.n_head == 2) {
             const int hid = A.hid;
             // fmaxf(acc, lo0) is the optional ReLU without a per-element select
             const f2 lo0 = f2(A.relu0 ? 0.f : -INFINITY);
@@ -623,12 +567,6 @@ void launch_fused(dim3 grid, hipStream_t s, const FusedArgs &fa, const LevelArgs
 
 namespace ccmi_fwd {
 
-int mfma_head_enabled()
-{
-    static const int on = getenv("CCMI_SYN_VALU_HEAD") == nullptr;
-    return on;
-}
-
 void layer_offsets(const ccmi_syn_args *a, int *w_off, int *b_off, int *cin_of, int64_t *total)
 {
     int64_t o = 0;
@@ -666,7 +604,6 @@ bool make_plan(const ccmi_syn_args *a, Plan *P)
     if (cmid != 3 && cmid != 4) return false; // instantiated shapes
     FusedArgs &f = P->fa;
     f = FusedArgs{};
-    f.mfma_head = mfma_head_enabled();
     f.cin = a->c_in;
     f.H = a->h;
     f.W = a->w;

@@ -48,10 +48,13 @@ def test_gpu_encode_quantize_write_decode(gpu, oracle_c, tmp_path):
     H, W = 64, 96
     arch = train.Arch(H, W)
     tgt = _image(H, W)[None].to(gpu)
+    # c3x (shortened): quantize_model runs after its second phase, the last phase trains
+    # the latents against the quantised networks
     of, best = train.overfit(arch, tgt, lmbda=1e-3, scale=0.05, seed=0)
-    qm = quantize.quantize_model(arch, of.latents[0], of.params[0], tgt[0], lmbda=1e-3, yuv420=True)
+    qm = of.quantized[0]
     for m in ("arm", "synthesis", "upsampling"):
-        assert m in qm.q_index and m in qm.expgol
+        assert m in qm.q_index and m in qm.expgol and qm.nn_bits[m] > 0
+    assert np.array_equal(of.params[0].cpu().numpy(), qm.params)
     stream = encode.write_cool(arch, of.latents[0], qm, yuv420=True)
     assert 100 < len(stream) < H * W  # far below 8 bpp
     # bit-exact decode: GPU decoder == C oracle (== reference decoder)
