@@ -465,7 +465,7 @@ def main():
             "per_gpu": round(per_gpu, 2), "unit": "images/hr", "n_gpus": world,
             "images_per_gpu": enc["images"], "seconds": round(enc["seconds"], 2),
             "schedule": f"c3x x{args.encode_scale:g}: warm-up 5x400 + 2x400 candidates, phases 10600 + 1500 + 1000 "
-                        f"iterations ({enc['iterations']} per image); quantize_model not run",
+                        f"iterations ({enc['iterations']} per image); quantize_model after the second phase",
             "psnr_db_mean": round(enc["psnr_db"], 3), "rate_bpp_mean": round(enc["rate_bpp"], 4),
             "data": "synthetic 512x768 frames (seeded sinusoids + N(0, 0.02) noise), lmbda 1e-3"}
         if rank == 0 and world == 1 and not args.no_cpu_baseline:
