@@ -46,8 +46,8 @@ def sizes(h=H, w=W, n=N_GRIDS):
     return out
 
 
-def flops_per_frame():
-    s = sizes()
+def flops_per_frame(H=H, W=W):
+    s = sizes(H, W)
     n_lat = sum(h * w for h, w in s)
     npx = H * W
     d = DIM_ARM
@@ -64,16 +64,16 @@ def flops_per_frame():
     return {"arm": 2 * arm_mac, "ups": 2 * ups_mac, "syn": 2 * syn_mac, "n_lat": n_lat}
 
 
-def flops_fused_per_frame():
+def flops_fused_per_frame(H=H, W=W):
     """The fused kernel: last upsampling step (level 1 -> 0) + synthesis (+ post, no flops)."""
-    fl = flops_per_frame()
-    h0, w0 = sizes()[0]
+    fl = flops_per_frame(H, W)
+    h0, w0 = sizes(H, W)[0]
     last_ups = 2 * h0 * w0 * (14 + 8 * (N_GRIDS - 1))
     return last_ups + fl["syn"]
 
 
-def bytes_per_frame():
-    s = sizes()
+def bytes_per_frame(H=H, W=W):
+    s = sizes(H, W)
     n_lat = sum(h * w for h, w in s)
     npx = H * W
     h1, w1 = s[1]
@@ -85,17 +85,17 @@ def bytes_per_frame():
             "decode_fused": 4 * ((N_GRIDS - 1) * h1 * w1 + npx + npx * 3 // 2)}
 
 
-def make_inputs(B, dev, seed):
+def make_inputs(B, dev, seed, H=H, W=W):
     import forward_oracle as fo
     from ccmi import forward as F
     g = torch.Generator().manual_seed(seed)
-    lat = 0.5 * torch.randn(B, sum(h * w for h, w in sizes()), generator=g)
+    lat = 0.5 * torch.randn(B, sum(h * w for h, w in sizes(H, W)), generator=g)
     mps = [fo.ModelParams.random(H, W, DIM_ARM, N_HIDDEN, HOP, N_GRIDS, seed=seed + i) for i in range(B)]
     arm = torch.stack([F.pack_arm(m.arm) for m in mps])
     ups = torch.stack([F.pack_ups(m.ups_full(), m.pre_full()) for m in mps])
     syn = torch.stack([F.pack_syn(m.syn) for m in mps])
     return {"lat": lat.to(dev), "arm": arm.to(dev), "ups": ups.to(dev), "syn": syn.to(dev), "mps": mps,
-            "lat_cpu": lat}
+            "lat_cpu": lat, "H": H, "W": W}
 
 
 class Pipeline:
@@ -107,7 +107,8 @@ class Pipeline:
         from ccmi import forward as F
         self.L = ccmi.lib()
         self.B = B
-        s = sizes()
+        H, W = inp["H"], inp["W"]
+        s = sizes(H, W)
         n = sum(h * w for h, w in s)
         self.rate = torch.empty(B, n, device=dev)
         self.dense = torch.empty(B, N_GRIDS, H, W, device=dev)
@@ -172,6 +173,56 @@ class Pipeline:
         self.stream.wait_event(self.join)
 
 
+def measure_path_a(inp, B, steps, warmup, mode, overlap, dist, dev):
+    """Time `steps` pipeline steps (after `warmup`), barrier + synchronize on both sides;
+    returns (max-over-ranks seconds, per-stage ms per step from HIP events)."""
+    pipe = Pipeline(inp, B, dev)
+    names = Pipeline.STAGES[mode]
+    for _ in range(warmup):
+        pipe.step(mode=mode, overlap=overlap)
+    torch.cuda.synchronize()
+    # per-stage HIP events over the timed region (recorded on the stream each kernel runs on)
+    ev = [[torch.cuda.Event(enable_timing=True) for _ in range(len(names) + 3)] for _ in range(steps)]
+    if dist: dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for k in range(steps):
+        pipe.step(ev[k], mode, overlap)
+    torch.cuda.synchronize()
+    t1 = time.perf_counter()
+    if dist: dist.barrier()
+    dt = t1 - t0
+    if dist:
+        t = torch.tensor([dt], device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        dt = float(t.item())
+    nn = len(names)
+    if overlap:  # ARM timed by its own pair of events on the side stream
+        stage_ms = {"arm": sum(ev[k][nn + 1].elapsed_time(ev[k][nn + 2]) for k in range(steps)) / steps}
+        stage_ms.update({n: sum(ev[k][i].elapsed_time(ev[k][i + 1]) for k in range(steps)) / steps
+                         for i, n in enumerate(names) if i > 0})
+    else:
+        stage_ms = {n: sum(ev[k][i].elapsed_time(ev[k][i + 1]) for k in range(steps)) / steps
+                    for i, n in enumerate(names)}
+    return dt, stage_ms
+
+
+def bench_path_a_hd(B, steps, warmup, rank, world, dist, dev):
+    """The same fused float forward on synthetic 1920x1080 frames (BASELINE config 5's
+    geometry, fp32): whole-job Mpixel/s and the fused kernel's FP32 roofline fraction."""
+    Hh, Wh = 1080, 1920
+    inp = make_inputs(B, dev, seed=1000 * rank + 7, H=Hh, W=Wh)
+    dt, st = measure_path_a(inp, B, steps, warmup, "fused", False, dist, dev)
+    ach = flops_fused_per_frame(Hh, Wh) * B / (st["decode_fused"] * 1e-3) / 1e12
+    return {"metric": "decoded Mpixel/s (Synth+ARM+upsample) @1920x1080, all GPUs",
+            "value": round(B * steps * world * Hh * Wh / dt / 1e6, 2), "unit": "Mpixel/s",
+            "frames_per_step_per_gpu": B, "steps": steps, "ms_per_step": round(dt / steps * 1e3, 4),
+            "stage_ms_per_step": {k: round(v, 4) for k, v in st.items()},
+            "roofline": {"bound": "mfma", "kernel": "decode_fused", "achieved": round(ach, 3),
+                         "peak": PEAK_FP32_TFLOPS, "unit": "TFLOP/s", "frac": round(ach / PEAK_FP32_TFLOPS, 4)},
+            "data": "synthetic (seeded N(0,0.5) latents, random-init hop weights per frame), 7 latent grids"}
+
+
 def cpu_baseline(inp, budget_s=12.0, max_frames=64):
     """Oracle (torch fp32 CPU restatement of the reference forward) on whole 720p frames."""
     import forward_oracle as fo
@@ -194,14 +245,14 @@ def cpu_baseline(inp, budget_s=12.0, max_frames=64):
                       f"(oracle/forward_oracle.py, torch fp32 CPU, {torch.get_num_threads()} threads), {dt:.1f} s"}
 
 
-def bench_bitexact_decode(reps: int):
-    """Path B: the bit-exact HIP decoder on the shipped 1280x720 class-E .cool streams
-    (15 files x reps frames per ccmi_decode_batch call), output bytes checked against the
-    reference decoder's md5 list."""
+def bench_bitexact_decode(reps: int, cls: str = "E", H=H, W=W):
+    """Path B: the bit-exact HIP decoder on the shipped JVET class-`cls` .cool streams
+    (class E: 15 files at 1280x720; class B: 5 committed files at 1920x1080), reps copies
+    per ccmi_decode_batch call, output bytes checked against the reference decoder's md5s."""
     import hashlib
     from ccmi import decode
     md5 = json.loads((ROOT / "tests/golden/ref_md5.json").read_text())
-    files = sorted((ROOT / "tests/golden/cool").glob("E-*.cool"))
+    files = sorted((ROOT / "tests/golden/cool").glob(f"{cls}-*.cool"))
     streams = [f.read_bytes() for f in files]
     decode.decode_batch(streams[:2])
     batch = streams * reps
@@ -212,11 +263,11 @@ def bench_bitexact_decode(reps: int):
     exact = all(hashlib.md5(o).hexdigest() == md5["jvet/" + f.name]["md5"] for f, o in zip(files * reps, outs))
     kern_s = (tm["arm_cabac"] + tm["ups_syn_out"]) / 1e3
     n = len(batch)
-    return {"metric": "bit-exact .cool decode Mpixel/s (batch of independent 720p streams)",
+    return {"metric": f"bit-exact .cool decode Mpixel/s (batch of independent {W}x{H} streams)",
             "frames": n, "value_kernels": round(n * H * W / kern_s / 1e6, 2),
             "value_wall_pcie_inclusive": round(n * H * W / wall / 1e6, 2), "unit": "Mpixel/s",
             "stage_ms": {k: round(v, 3) for k, v in tm.items()}, "bit_exact_vs_reference_md5": exact,
-            "data": "15 shipped JVET class-E .cool bitstreams (results/image/jvet), repeated"}
+            "data": f"{len(files)} shipped JVET class-{cls} .cool bitstreams (results/image/jvet), repeated"}
 
 
 def bench_bitexact_encode(reps: int = 2):
@@ -360,6 +411,9 @@ def main():
                          "step rate is the same within noise on MI355X; kernels then share CUs, so the "
                          "roofline kernel's duration is no longer its own)")
     ap.add_argument("--serial", action="store_true", help="(default) one stream, kernels back to back")
+    ap.add_argument("--hd-steps", type=int, default=20, help="steps of the 1920x1080 float-forward leg (0: skip)")
+    ap.add_argument("--hd-decode-reps", type=int, default=64,
+                    help="class-B (1080p) stream copies for the bit-exact decode leg (0: skip)")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -375,39 +429,9 @@ def main():
 
     B = args.batch
     inp = make_inputs(B, dev, seed=1000 * rank + 1)
-    pipe = Pipeline(inp, B, dev)
-
     mode = "staged" if args.staged else "fused"
-    names = Pipeline.STAGES[mode]
     overlap = args.overlap and not args.serial
-    for _ in range(args.warmup):
-        pipe.step(mode=mode, overlap=overlap)
-    torch.cuda.synchronize()
-
-    # per-stage HIP events over the timed region (recorded on the stream each kernel runs on)
-    ev = [[torch.cuda.Event(enable_timing=True) for _ in range(len(names) + 3)] for _ in range(args.steps)]
-    if dist: dist.barrier()
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    for k in range(args.steps):
-        pipe.step(ev[k], mode, overlap)
-    torch.cuda.synchronize()
-    t1 = time.perf_counter()
-    if dist: dist.barrier()
-    dt = t1 - t0
-    if dist:
-        t = torch.tensor([dt], device=dev)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        dt = float(t.item())
-
-    nn = len(names)
-    if overlap:  # ARM timed by its own pair of events on the side stream
-        stage_ms = {"arm": sum(ev[k][nn + 1].elapsed_time(ev[k][nn + 2]) for k in range(args.steps)) / args.steps}
-        stage_ms.update({n: sum(ev[k][i].elapsed_time(ev[k][i + 1]) for k in range(args.steps)) / args.steps
-                         for i, n in enumerate(names) if i > 0})
-    else:
-        stage_ms = {n: sum(ev[k][i].elapsed_time(ev[k][i + 1]) for k in range(args.steps)) / args.steps
-                    for i, n in enumerate(names)}
+    dt, stage_ms = measure_path_a(inp, B, args.steps, args.warmup, mode, overlap, dist, dev)
     fl = flops_per_frame()
     fl["decode_fused"] = flops_fused_per_frame()
     by = bytes_per_frame()
@@ -444,6 +468,8 @@ def main():
                      "algorithmic_bytes_per_launch": by[dom] * B,
                      "note": "FP32 VALU-bound fused kernel; peak = FP32 vector rate (= f32 MFMA rate) on MI355X"},
     }
+    if args.hd_steps > 0:
+        res["path_a_1080p"] = bench_path_a_hd(B, args.hd_steps, args.warmup, rank, world, dist, dev)
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         res["cpu_baseline"] = cpu_baseline(inp)
     if rank == 0 and args.decode_reps > 0:
@@ -452,6 +478,8 @@ def main():
             dec["cpu_baseline"] = cpu_decode_baseline()
         res["bitexact_decode"] = dec
         res["bitexact_encode"] = bench_bitexact_encode()
+    if rank == 0 and args.hd_decode_reps > 0:
+        res["bitexact_decode_1080p"] = bench_bitexact_decode(args.hd_decode_reps, "B", 1080, 1920)
     if args.encode_images > 0:
         enc = bench_encoder(args.encode_images, args.encode_scale, rank, dev)
         per_gpu = enc["images"] / enc["seconds"] * 3600.0

@@ -1,6 +1,6 @@
 set -u
 O=gpurun_out/r1d_ab; mkdir -p $O
-Q="--steps 30 --warmup 5 --no-cpu-baseline --decode-reps 0 --encode-images 0"
+Q="--steps 30 --warmup 5 --no-cpu-baseline --decode-reps 0 --encode-images 0 --hd-steps 0 --hd-decode-reps 0"
 for i in 1 2 3; do
   timeout -k 10 120 env CCMI_LIB=$PWD/cool-chic_amd/lib/libccmi_base.so python bench.py $Q --serial > $O/base_serial_$i.json 2>/dev/null || exit 1
   timeout -k 10 120 python bench.py $Q --serial > $O/new_serial_$i.json 2>/dev/null || exit 1

@@ -16,7 +16,7 @@ step() { # name seconds command...
 }
 step pytest_gpu 900 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread
 step mfma_probe 60 ./tools/mfma_probe
-QUICK="--steps 20 --warmup 5 --no-cpu-baseline --decode-reps 0 --encode-images 0"
+QUICK="--steps 20 --warmup 5 --no-cpu-baseline --decode-reps 0 --encode-images 0 --hd-steps 0 --hd-decode-reps 0"
 step bench_mfma_head 300 python bench.py $QUICK
 step bench_valu_head 300 env CCMI_SYN_VALU_HEAD=1 python bench.py $QUICK
 step bench_mfma_head_serial 300 python bench.py $QUICK --serial

@@ -18,7 +18,7 @@ run() { # name seconds command...
 }
 run pytest_gpu 900 python -u -m pytest $ROOT/tests -m gpu -x -v -s --timeout 300 --timeout-method thread
 run bench 600 python3 $ROOT/bench.py
-QB="$ROOT/bench.py --steps 20 --warmup 5 --no-cpu-baseline --decode-reps 0 --encode-images 0"
+QB="$ROOT/bench.py --steps 20 --warmup 5 --no-cpu-baseline --decode-reps 0 --encode-images 0 --hd-steps 0 --hd-decode-reps 0"
 run trace 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/trace -- python3 $QB
 run pmc_size 180 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $OUT/pmc_size -- python3 $QB
 run pmc_write 180 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $OUT/pmc_write -- python3 $QB

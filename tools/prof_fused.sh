@@ -17,7 +17,7 @@ run() { # name seconds command...
     echo "   rc=$rc" | tee -a "$OUT/steps.log"
     if [ $rc -ne 0 ]; then tail -30 "$OUT/$name.log"; exit $rc; fi
 }
-BENCH="$ROOT/bench.py --steps 5 --warmup 2 --no-cpu-baseline --decode-reps 0 --encode-images 0 --serial"
+BENCH="$ROOT/bench.py --steps 5 --warmup 2 --no-cpu-baseline --decode-reps 0 --encode-images 0 --hd-steps 0 --hd-decode-reps 0 --serial"
 run stamps 120 env CCMI_LIB=$ROOT/cool-chic_amd/lib/libccmi_stamps.so python3 $ROOT/tools/prof_fused.py
 run syn_micro 120 python3 $ROOT/tools/syn_micro.py
 run trace 180 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/trace -- python3 $BENCH
