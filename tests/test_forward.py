@@ -130,7 +130,8 @@ def test_hip_psnr_within_1e5_db(gpu, ccmi_lib):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("H,W,seed", [(720, 1280, 1), (37, 53, 2), (1, 1, 3), (2, 130, 4), (129, 3, 5)])
+@pytest.mark.parametrize("H,W,seed", [(720, 1280, 1), (1080, 1920, 11), (37, 53, 2), (1, 1, 3), (2, 130, 4),
+                                      (129, 3, 5)])
 def test_hip_forward_matches_oracle_random(H, W, seed, gpu, ccmi_lib):
     mp = fo.ModelParams.random(H, W, seed=seed)
     g = torch.Generator().manual_seed(seed)
@@ -215,7 +216,7 @@ def test_fused_decode_matches_reference_golden(path, gpu, ccmi_lib):
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("H,W,seed,layers", [
-    (720, 1280, 1, None), (37, 53, 2, None), (1, 1, 3, None), (2, 130, 4, None), (129, 3, 5, None),
+    (720, 1280, 1, None), (1080, 1920, 11, None), (37, 53, 2, None), (1, 1, 3, None), (2, 130, 4, None), (129, 3, 5, None),
     (45, 70, 6, "3-1-linear-none|3-3-residual-relu"),
     (45, 70, 7, "16-1-linear-relu|3-1-linear-none"),
     (64, 96, 8, "16-1-linear-relu|4-1-linear-none|4-3-residual-relu|4-3-residual-none|4-3-linear-none"),

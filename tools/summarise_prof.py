@@ -24,6 +24,16 @@ STAGES = {"arm_fwd_kernel": "arm", "ups_level_kernel": "ups", "ups_level_fixed":
 FUSED = False  # set from the trace: a fused-decode run (syn_fused_kernel<..., true>) present
 
 
+def find(src: Path, dirs, suffix: str) -> Path:
+    """The rocprofv3 output file ending in `suffix` under src/<dir> (any run sub-directory;
+    tools/rocprof_bench.sh and tools/gpu_round.sh lay them out differently)."""
+    for d in ([dirs] if isinstance(dirs, str) else dirs):
+        hits = sorted((src / d).rglob(f"*{suffix}"))
+        if hits:
+            return hits[0]
+    raise FileNotFoundError(f"no *{suffix} under {src}/{dirs}")
+
+
 def stage_of(name: str):
     # the fused decode tail: syn_fused_kernel<CIN, CMID, true> ("Lb1E" in the mangled name)
     if "syn_fused_kernel" in name and ("Lb1E" in name or "true>" in name):
@@ -58,12 +68,13 @@ def main(src: str, tag: str):
     prof = ROOT / "profiles"
     prof.mkdir(exist_ok=True)
     global FUSED
-    shutil.copy(src / "trace" / "run_kernel_stats.csv", prof / f"{tag}_kernel_stats.csv")
+    stats_csv = find(src, "trace", "kernel_stats.csv")
+    shutil.copy(stats_csv, prof / f"{tag}_kernel_stats.csv")
     FUSED = any("syn_fused_kernel" in r["Name"] and ("Lb1E" in r["Name"] or "true>" in r["Name"])
-                for r in csv.DictReader((src / "trace" / "run_kernel_stats.csv").open()))
-    fetch = per_step_counter(src / "pmc_fetch" / "run_counter_collection.csv", "FETCH_SIZE")
-    write = per_step_counter(src / "pmc_write" / "run_counter_collection.csv", "WRITE_SIZE")
-    stats = {r["Name"]: r for r in csv.DictReader((src / "trace" / "run_kernel_stats.csv").open())}
+                for r in csv.DictReader(stats_csv.open()))
+    fetch = per_step_counter(find(src, ("pmc_fetch", "pmc_size"), "counter_collection.csv"), "FETCH_SIZE")
+    write = per_step_counter(find(src, "pmc_write", "counter_collection.csv"), "WRITE_SIZE")
+    stats = {r["Name"]: r for r in csv.DictReader(stats_csv.open())}
     avg_ns = {}
     for name, r in stats.items():
         st = stage_of(name)
