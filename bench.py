@@ -207,6 +207,41 @@ def measure_path_a(inp, B, steps, warmup, mode, overlap, dist, dev):
     return dt, stage_ms
 
 
+def measure_path_a_graph(inp, B, steps, warmup, dist, dev, per_graph=10):
+    """The fused pipeline captured in a HIP graph (`per_graph` steps per graph, one stream):
+    replays remove the host launch gaps between the step's small pyramid kernels.  Returns
+    the max-over-ranks seconds for `steps` steps (a multiple of per_graph)."""
+    pipe = Pipeline(inp, B, dev)
+    s = torch.cuda.Stream(dev)
+    s.wait_stream(torch.cuda.current_stream(dev))
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.stream(s):
+        pipe.stream = s
+        pipe.step(mode="fused", overlap=False)
+        s.synchronize()
+        with torch.cuda.graph(g, stream=s):
+            for _ in range(per_graph):
+                pipe.step(mode="fused", overlap=False)
+    torch.cuda.synchronize()
+    for _ in range(max(1, warmup // per_graph)):
+        g.replay()
+    torch.cuda.synchronize()
+    reps = max(1, steps // per_graph)
+    if dist: dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(reps):
+        g.replay()
+    torch.cuda.synchronize()
+    dt = time.perf_counter() - t0
+    if dist: dist.barrier()
+    if dist:
+        t = torch.tensor([dt], device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        dt = float(t.item())
+    return dt, reps * per_graph
+
+
 def bench_path_a_hd(B, steps, warmup, rank, world, dist, dev):
     """The same fused float forward on synthetic 1920x1080 frames (BASELINE config 5's
     geometry, fp32): whole-job Mpixel/s and the fused kernel's FP32 roofline fraction."""
@@ -411,6 +446,8 @@ def main():
                          "step rate is the same within noise on MI355X; kernels then share CUs, so the "
                          "roofline kernel's duration is no longer its own)")
     ap.add_argument("--serial", action="store_true", help="(default) one stream, kernels back to back")
+    ap.add_argument("--no-graph", action="store_true",
+                    help="time the eager launches instead of HIP-graph replays of the fused pipeline")
     ap.add_argument("--hd-steps", type=int, default=20, help="steps of the 1920x1080 float-forward leg (0: skip)")
     ap.add_argument("--hd-decode-reps", type=int, default=64,
                     help="class-B (1080p) stream copies for the bit-exact decode leg (0: skip)")
@@ -439,6 +476,16 @@ def main():
     achieved = fl[dom] * B / (stage_ms[dom] * 1e-3) / 1e12
     traffic, src = pmc_traffic(dom)
 
+    eager = None
+    graph = not (args.no_graph or args.staged or overlap)
+    if graph:
+        # headline: the same K steps replayed from HIP graphs (per-stage times and the
+        # roofline above come from the event-instrumented eager pass)
+        eager = {"value": round(B * args.steps * world * H * W / dt / 1e6, 2),
+                 "ms_per_step": round(dt / args.steps * 1e3, 4)}
+        per = 10 if args.steps % 10 == 0 else 1
+        dt, n_done = measure_path_a_graph(inp, B, args.steps, args.warmup, dist, dev, per)
+        assert n_done == args.steps
     n_frames = B * args.steps * world
     value = n_frames * H * W / dt / 1e6
     res = {
@@ -461,6 +508,8 @@ def main():
                                else "ARM | upsampling | synthesis | post")
                    + (" (ARM on a second stream, concurrent)" if overlap else " (one stream)")},
         "stage_ms_per_step": {k: round(v, 4) for k, v in stage_ms.items()},
+        "launch": "HIP graph replays (10 steps per graph)" if graph else "eager launches",
+        "eager": eager,
         "roofline": {"bound": "mfma", "kernel": dom, "achieved": round(achieved, 3), "peak": PEAK_FP32_TFLOPS,
                      "unit": "TFLOP/s", "frac": round(achieved / PEAK_FP32_TFLOPS, 4),
                      "traffic": traffic, "traffic_source": src,
