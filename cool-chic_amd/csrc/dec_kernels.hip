@@ -108,6 +108,7 @@ __device__ __forceinline__ void ctx_dydx(int i, int &dy, int &dx)
 }
 
 constexpr int kRing = 5;   // rows y-4 .. y
+constexpr int kRingS = 4;  // speculative kernel (D <= 16: contexts reach row y-3): rows y-3 .. y
 constexpr int kPad = 8;    // zero columns either side of a ring row (speculative groups read x+3+4)
 
 // int32 multiply with two's-complement wrap; the 24-bit form (v_mad_i32_i24, full rate)
@@ -360,8 +361,8 @@ __global__ __launch_bounds__(64) void dec_arm_spec_kernel(const ArmStreamDesc *_
 #endif
     extern __shared__ int32_t smem[];
     uint32_t *ctab = reinterpret_cast<uint32_t *>(smem);               // 17 x 50 x 2
-    int32_t *ring = smem + 17 * 50 * 2;                                // kRing x pitch
-    uint8_t *bmap = reinterpret_cast<uint8_t *>(ring + kRing * pitch); // block sig/flat map
+    int32_t *ring = smem + 17 * 50 * 2;                                 // kRingS x pitch
+    uint8_t *bmap = reinterpret_cast<uint8_t *>(ring + kRingS * pitch); // block sig/flat map
 
     const ArmStreamDesc S = streams[blockIdx.x];
     const int lane = threadIdx.x;
@@ -382,7 +383,7 @@ __global__ __launch_bounds__(64) void dec_arm_spec_kernel(const ArmStreamDesc *_
         }
         ctab[i] = (i & 1) ? (o & 0xFF) : o;
     }
-    for (int i = lane; i < kRing * pitch; i += 64) ring[i] = 0;
+    for (int i = lane; i < kRingS * pitch; i += 64) ring[i] = 0;
 
     int32_t Wh[NH > 0 ? NH : 1][16], Bh[NH > 0 ? NH : 1];
 #pragma unroll
@@ -448,9 +449,9 @@ __global__ __launch_bounds__(64) void dec_arm_spec_kernel(const ArmStreamDesc *_
 #endif
 
     for (int y = 0; y < h; ++y) {
-        int32_t *row = ring + (y % kRing) * pitch + kPad;
-        const int32_t *up = ring + ((y + kRing - 1) % kRing) * pitch + kPad;
-        const int32_t *crow = ring + ((y + cdy + kRing) % kRing) * pitch + kPad + cdx + grp;
+        int32_t *row = ring + (y % kRingS) * pitch + kPad;
+        const int32_t *up = ring + ((y + kRingS - 1) % kRingS) * pitch + kPad;
+        const int32_t *crow = ring + ((y + cdy + kRingS) % kRingS) * pitch + kPad + cdx + grp;
         int32_t r1 = 0, r2 = 0, r3 = 0, r4 = 0; // decoded values at x-1 .. x-4 (this row)
         const int brow = blk > 0 ? (y >> shift) * nbx : 0;
         auto push = [&](int32_t v, int x) {
@@ -943,7 +944,9 @@ int launch_dec_arm(const ArmStreamDesc *d_streams, int n_streams, int max_w, int
 {
     const int pitch = max_w + 2 * kPad;
     const size_t lds = sizeof(int32_t) * kRing * pitch + ((size_t)max_blocks + 16);
-    const size_t lds_spec = lds + sizeof(uint32_t) * 17 * 50 * 2;
+    // the speculative kernel keeps one ring row fewer (its contexts reach row y-3 only):
+    // 5 streams (waves) per CU instead of 4 at 720p
+    const size_t lds_spec = sizeof(int32_t) * kRingS * pitch + ((size_t)max_blocks + 16) + sizeof(uint32_t) * 17 * 50 * 2;
     // CCMI_ARM_NOSPEC=1 selects the one-latent-per-pass kernel (A/B measurements)
     static const bool spec_off = getenv("CCMI_ARM_NOSPEC") != nullptr;
     if (!spec_off && d <= 16 && lds_spec <= 160 * 1024) {
