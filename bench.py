@@ -215,14 +215,26 @@ def measure_path_a_graph(inp, B, steps, warmup, dist, dev, per_graph=10):
     s = torch.cuda.Stream(dev)
     s.wait_stream(torch.cuda.current_stream(dev))
     g = torch.cuda.CUDAGraph()
-    with torch.cuda.stream(s):
-        pipe.stream = s
-        pipe.step(mode="fused", overlap=False)
-        s.synchronize()
-        with torch.cuda.graph(g, stream=s):
-            for _ in range(per_graph):
-                pipe.step(mode="fused", overlap=False)
-    torch.cuda.synchronize()
+    err = None
+    try:
+        with torch.cuda.stream(s):
+            pipe.stream = s
+            pipe.step(mode="fused", overlap=False)
+            s.synchronize()
+            # thread_local: the process group's watchdog thread may query events meanwhile
+            with torch.cuda.graph(g, stream=s, capture_error_mode="thread_local"):
+                for _ in range(per_graph):
+                    pipe.step(mode="fused", overlap=False)
+        torch.cuda.synchronize()
+    except Exception as e:
+        err = f"{type(e).__name__}: {e}"
+    if dist:  # every rank takes the same branch, so the collectives below stay matched
+        ok = torch.tensor([0 if err else 1], device=dev)
+        dist.all_reduce(ok, op=dist.ReduceOp.MIN)
+        if not int(ok.item()) and not err:
+            err = "graph capture failed on another rank"
+    if err:
+        raise RuntimeError(err)
     for _ in range(max(1, warmup // per_graph)):
         g.replay()
     torch.cuda.synchronize()
@@ -457,10 +469,18 @@ def main():
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     dist = None
+    # CCMI_BENCH_BACKEND=gloo: rehearsal of the multi-rank path with several ranks on one
+    # card (RCCL needs one GPU per rank); the driver's runs use the default, RCCL
+    backend = os.environ.get("CCMI_BENCH_BACKEND", "nccl")
+    if backend != "nccl":
+        local = local % torch.cuda.device_count()
     if world > 1:
         import torch.distributed as dist
         torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        else:
+            dist.init_process_group(backend)
     dev = torch.device("cuda", local)
     torch.cuda.set_device(dev)
 
@@ -476,7 +496,7 @@ def main():
     achieved = fl[dom] * B / (stage_ms[dom] * 1e-3) / 1e12
     traffic, src = pmc_traffic(dom)
 
-    eager = None
+    eager, graph_error = None, None
     graph = not (args.no_graph or args.staged or overlap)
     if graph:
         # headline: the same K steps replayed from HIP graphs (per-stage times and the
@@ -484,8 +504,14 @@ def main():
         eager = {"value": round(B * args.steps * world * H * W / dt / 1e6, 2),
                  "ms_per_step": round(dt / args.steps * 1e3, 4)}
         per = 10 if args.steps % 10 == 0 else 1
-        dt, n_done = measure_path_a_graph(inp, B, args.steps, args.warmup, dist, dev, per)
-        assert n_done == args.steps
+        try:
+            dt, n_done = measure_path_a_graph(inp, B, args.steps, args.warmup, dist, dev, per)
+            assert n_done == args.steps
+        except Exception as e:  # report the eager timing, and say so in the line
+            graph_error = f"{type(e).__name__}: {e}"[:200]
+            graph = False
+    launch = "HIP graph replays (10 steps per graph)" if graph else (
+        "eager launches" + (f" (graph capture failed: {graph_error})" if graph_error else ""))
     n_frames = B * args.steps * world
     value = n_frames * H * W / dt / 1e6
     res = {
@@ -508,7 +534,7 @@ def main():
                                else "ARM | upsampling | synthesis | post")
                    + (" (ARM on a second stream, concurrent)" if overlap else " (one stream)")},
         "stage_ms_per_step": {k: round(v, 4) for k, v in stage_ms.items()},
-        "launch": "HIP graph replays (10 steps per graph)" if graph else "eager launches",
+        "launch": launch,
         "eager": eager,
         "roofline": {"bound": "mfma", "kernel": dom, "achieved": round(achieved, 3), "peak": PEAK_FP32_TFLOPS,
                      "unit": "TFLOP/s", "frac": round(achieved / PEAK_FP32_TFLOPS, 4),
