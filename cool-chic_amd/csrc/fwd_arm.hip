@@ -8,11 +8,12 @@
 //                scale = exp(clamp(log_scale - 4, -4.6, 5))),
 //   rate (coolchic.py:419-424 with _laplace_cdf arm.py:355-370).
 //
-// Layout: one workgroup (256 threads, 4 waves) owns an 8 x 64 tile of one grid of one
+// Layout: one workgroup (256 threads, 4 waves) owns a (4 NL) x 64 tile of one grid of one
 // frame.  The quantised tile plus its causal halo (4 rows above, 4 columns either
 // side) is staged once in LDS; each thread evaluates the MLP for NL = 2 latents of the
-// same column, so every weight (wave-uniform, held in SGPRs via scalar loads) feeds two
-// FMAs.  LDS reads are lane-consecutive (conflict-free).  Grids of all resolutions
+// same column as one packed pair, so every weight (wave-uniform, held in SGPRs via
+// scalar loads) feeds one v_pk_fma_f32 (two FMAs).  NL = 4 (two pairs per weight) was
+// measured 13 % slower: 132 VGPRs, 3 waves per SIMD instead of 7.  LDS reads are lane-consecutive (conflict-free).  Grids of all resolutions
 // share one launch through a tile prefix table (no per-grid launches).
 #include "fwd_common.h"
 
@@ -24,7 +25,11 @@ namespace {
 constexpr int kThreads = 256;
 constexpr int kTX = 64;
 constexpr int kRowsPerPass = kThreads / kTX; // 4
-constexpr int kNL = 2;                        // latents per thread
+#ifndef CCMI_ARM_NL
+#define CCMI_ARM_NL 2
+#endif
+constexpr int kNL = CCMI_ARM_NL;              // latents per thread (packed pairs)
+constexpr int kNP = kNL / 2;
 constexpr int kTY = kRowsPerPass * kNL;       // 8
 constexpr int kHalo = 4;
 constexpr int kLW = kTX + 2 * kHalo;          // 72
@@ -101,44 +106,70 @@ __global__ __launch_bounds__(kThreads) void arm_fwd_kernel(
 
     // the two latents of a thread travel as one packed pair (v_pk_fma_f32): every
     // wave-uniform weight feeds both with one instruction
-    static_assert(kNL == 2, "packed pair layout");
-    f2 a[D];
+    // pair q = rows cy0 + (2q) * kRowsPerPass and cy0 + (2q + 1) * kRowsPerPass
+    static_assert(kNL % 2 == 0, "packed pair layout");
+    f2 a[kNP][D];
 #pragma unroll
     for (int i = 0; i < D; ++i) {
         int dy, dx;
         ctx_offset<D>(i, dy, dx);
-        a[i] = f2{tile[cy0 + kHalo + dy][cx + kHalo + dx], tile[cy0 + kRowsPerPass + kHalo + dy][cx + kHalo + dx]};
+#pragma unroll
+        for (int q = 0; q < kNP; ++q)
+            a[q][i] = f2{tile[cy0 + 2 * q * kRowsPerPass + kHalo + dy][cx + kHalo + dx],
+                         tile[cy0 + (2 * q + 1) * kRowsPerPass + kHalo + dy][cx + kHalo + dx]};
     }
 
     for (int layer = 0; layer < nh; ++layer) {
         const cfloat_ptr Wl = p + layer * (D * D + D);
         const cfloat_ptr bl = Wl + D * D;
-        f2 o[D];
+        f2 o[kNP][D];
 #pragma unroll
         for (int j = 0; j < D; ++j) {
-            f2 acc = f2(0.f);
+            f2 acc[kNP];
 #pragma unroll
-            for (int i = 0; i < D; ++i) acc = __builtin_elementwise_fma(f2(Wl[j * D + i]), a[i], acc);
+            for (int q = 0; q < kNP; ++q) acc[q] = f2(0.f);
+#pragma unroll
+            for (int i = 0; i < D; ++i) {
+                const f2 wji = f2(Wl[j * D + i]);
+#pragma unroll
+                for (int q = 0; q < kNP; ++q) acc[q] = __builtin_elementwise_fma(wji, a[q][i], acc[q]);
+            }
             // F.linear(x) + x, then ReLU
-            o[j] = __builtin_elementwise_max((acc + f2(bl[j])) + a[j], f2(0.f));
+#pragma unroll
+            for (int q = 0; q < kNP; ++q)
+                o[q][j] = __builtin_elementwise_max((acc[q] + f2(bl[j])) + a[q][j], f2(0.f));
         }
 #pragma unroll
-        for (int j = 0; j < D; ++j) a[j] = o[j];
+        for (int q = 0; q < kNP; ++q)
+#pragma unroll
+            for (int j = 0; j < D; ++j) a[q][j] = o[q][j];
     }
 
     const cfloat_ptr Wo = p + nh * (D * D + D);
-    f2 m = f2(0.f), ls = f2(0.f);
+    f2 m[kNP], ls[kNP];
+#pragma unroll
+    for (int q = 0; q < kNP; ++q) {
+        m[q] = f2(0.f);
+        ls[q] = f2(0.f);
+    }
 #pragma unroll
     for (int i = 0; i < D; ++i) {
-        m = __builtin_elementwise_fma(f2(Wo[i]), a[i], m);
-        ls = __builtin_elementwise_fma(f2(Wo[D + i]), a[i], ls);
+        const f2 w0 = f2(Wo[i]), w1 = f2(Wo[D + i]);
+#pragma unroll
+        for (int q = 0; q < kNP; ++q) {
+            m[q] = __builtin_elementwise_fma(w0, a[q][i], m[q]);
+            ls[q] = __builtin_elementwise_fma(w1, a[q][i], ls[q]);
+        }
     }
-    m += f2(Wo[2 * D]);
-    ls += f2(Wo[2 * D + 1]);
+#pragma unroll
+    for (int q = 0; q < kNP; ++q) {
+        m[q] += f2(Wo[2 * D]);
+        ls[q] += f2(Wo[2 * D + 1]);
+    }
 #pragma unroll
     for (int n = 0; n < kNL; ++n) {
         const int y = y0 + cy0 + n * kRowsPerPass, x = x0 + cx;
-        const float mn = n ? m.y : m.x, lsn = n ? ls.y : ls.x;
+        const float mn = (n & 1) ? m[n >> 1].y : m[n >> 1].x, lsn = (n & 1) ? ls[n >> 1].y : ls[n >> 1].x;
         if (y < H && x < W) {
             const float sc = expf(fminf(fmaxf(lsn - 4.f, -4.6f), 5.0f));
             const float q = tile[cy0 + n * kRowsPerPass + kHalo][cx + kHalo];
