@@ -221,6 +221,7 @@ def measure_path_a_graph(inp, B, steps, warmup, dist, dev, per_graph=10):
             pipe.stream = s
             pipe.step(mode="fused", overlap=False)
             s.synchronize()
+            ref = (pipe.yuv.clone(), pipe.rate.clone())  # eager outputs, to check the replays
             # thread_local: the process group's watchdog thread may query events meanwhile
             with torch.cuda.graph(g, stream=s, capture_error_mode="thread_local"):
                 for _ in range(per_graph):
@@ -251,7 +252,13 @@ def measure_path_a_graph(inp, B, steps, warmup, dist, dev, per_graph=10):
         t = torch.tensor([dt], device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         dt = float(t.item())
-    return dt, reps * per_graph
+    # a replay recomputes the outputs from scratch: clear them, replay once, compare
+    pipe.yuv.zero_()
+    pipe.rate.zero_()
+    g.replay()
+    torch.cuda.synchronize()
+    same = bool(torch.equal(pipe.yuv, ref[0]) and torch.equal(pipe.rate, ref[1]))
+    return dt, reps * per_graph, same
 
 
 def bench_path_a_hd(B, steps, warmup, rank, world, dist, dev):
@@ -496,7 +503,7 @@ def main():
     achieved = fl[dom] * B / (stage_ms[dom] * 1e-3) / 1e12
     traffic, src = pmc_traffic(dom)
 
-    eager, graph_error = None, None
+    eager, graph_error, graph_same = None, None, None
     graph = not (args.no_graph or args.staged or overlap)
     if graph:
         # headline: the same K steps replayed from HIP graphs (per-stage times and the
@@ -505,7 +512,7 @@ def main():
                  "ms_per_step": round(dt / args.steps * 1e3, 4)}
         per = 10 if args.steps % 10 == 0 else 1
         try:
-            dt, n_done = measure_path_a_graph(inp, B, args.steps, args.warmup, dist, dev, per)
+            dt, n_done, graph_same = measure_path_a_graph(inp, B, args.steps, args.warmup, dist, dev, per)
             assert n_done == args.steps
         except Exception as e:  # report the eager timing, and say so in the line
             graph_error = f"{type(e).__name__}: {e}"[:200]
@@ -535,6 +542,7 @@ def main():
                    + (" (ARM on a second stream, concurrent)" if overlap else " (one stream)")},
         "stage_ms_per_step": {k: round(v, 4) for k, v in stage_ms.items()},
         "launch": launch,
+        "graph_outputs_equal_eager": graph_same,
         "eager": eager,
         "roofline": {"bound": "mfma", "kernel": dom, "achieved": round(achieved, 3), "peak": PEAK_FP32_TFLOPS,
                      "unit": "TFLOP/s", "frac": round(achieved / PEAK_FP32_TFLOPS, 4),
