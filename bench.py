@@ -453,7 +453,7 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=50)
     ap.add_argument("--warmup", type=int, default=5)
-    ap.add_argument("--batch", type=int, default=8, help="720p frames per step per GPU")
+    ap.add_argument("--batch", type=int, default=32, help="frames per step per GPU (720p headline and 1080p leg)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--decode-reps", type=int, default=64, help="class-E stream copies for the bit-exact decode leg")
     ap.add_argument("--staged", action="store_true",
