@@ -435,14 +435,16 @@ def cpu_decode_baseline(budget_s=10.0):
                       f"processes ({'reference ccdec --avx2' if kind == 'reference' else 'C oracle'}), {dt:.1f} s"}
 
 
-def pmc_traffic(stage: str):
-    """Per-launch HBM bytes of `stage` from the committed PMC summary, or None."""
+def pmc_traffic(stage: str, frames: int):
+    """HBM bytes of one `stage` launch over `frames` frames, from the newest committed PMC
+    summary (its per-launch bytes rescaled by the frames per launch it was measured at;
+    summaries without that field were measured at 8), or None."""
     for f in sorted((ROOT / "profiles").glob("*pmc*.json"), reverse=True):
         try:
             d = json.loads(f.read_text())
             v = d.get("per_launch_hbm_bytes", {}).get(stage)
             if v:
-                return float(v), f.name
+                return float(v) * frames / float(d.get("frames_per_launch", 8)), f.name
         except Exception:
             pass
     return None, None
@@ -501,7 +503,7 @@ def main():
     by = bytes_per_frame()
     dom = max(("arm", "decode_fused" if mode == "fused" else "syn"), key=lambda n: stage_ms[n])
     achieved = fl[dom] * B / (stage_ms[dom] * 1e-3) / 1e12
-    traffic, src = pmc_traffic(dom)
+    traffic, src = pmc_traffic(dom, B)
 
     eager, graph_error, graph_same = None, None, None
     graph = not (args.no_graph or args.staged or overlap)
