@@ -460,7 +460,7 @@ def main():
     ap.add_argument("--decode-reps", type=int, default=64, help="class-E stream copies for the bit-exact decode leg")
     ap.add_argument("--staged", action="store_true",
                     help="run upsampling / synthesis / post as separate kernels (module-boundary path)")
-    ap.add_argument("--encode-images", type=int, default=8, help="frames overfitted together per GPU (0: skip)")
+    ap.add_argument("--encode-images", type=int, default=16, help="frames overfitted together per GPU (0: skip)")
     ap.add_argument("--encode-scale", type=float, default=1.0, help="fraction of the c3x schedule to run")
     ap.add_argument("--overlap", action="store_true",
                     help="run the ARM on a second HIP stream concurrently with the decode tail (the "
