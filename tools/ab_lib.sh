@@ -15,7 +15,7 @@ step() { # name seconds command...
     echo "   rc=$rc" | tee -a "$OUT/steps.log"
     if [ $rc -ne 0 ]; then tail -40 "$OUT/$name.log"; exit $rc; fi
 }
-Q="--steps 50 --warmup 10 --no-cpu-baseline --decode-reps 0 --encode-images 0 --hd-decode-reps 0"
+Q="--steps 50 --warmup 10 --no-cpu-baseline --decode-reps 0 --encode-images 0 --hd-decode-reps 0 --hd-steps 10"
 step pytest_fwd 400 python -u -m pytest tests/test_forward.py tests/test_api_mirror.py tests/test_codec_e2e.py -m gpu -x -q --timeout 200 --timeout-method thread
 step bench_new 300 python bench.py $Q
 step bench_other 300 env CCMI_LIB=$OTHER python bench.py $Q
