@@ -58,13 +58,18 @@ constexpr int kRowsPerThread = kRH / (kFThreads / kRW); // 4
 // Output of channel m at (gy, gx): the synthesis value, or with A.qmax > 0 the
 // post-processed frame of FrameEncoder.forward (eval): round to the 2^bd - 1 grid, clamp
 // to [0, 1], and for yuv420 the chroma planes sampled at even rows / columns.
-__device__ __forceinline__ void store_out(const FusedArgs &A, float *out, int64_t plane, int m, int gy, int gx, float v)
+// lut8 (8-bit output): the 256 quotients k / 255 in LDS, so the rounded value costs a
+// lookup instead of an IEEE division; clamping k to [0, 255] first gives the same value
+// as clamping the quotient (NaN -> 0 both ways).
+__device__ __forceinline__ void store_out(const FusedArgs &A, float *out, int64_t plane, int m, int gy, int gx, float v,
+                                          const float *lut8)
 {
     if (A.qmax <= 0.f) {
         out[m * plane + (int64_t)gy * A.W + gx] = v;
         return;
     }
-    const float q = fminf(fmaxf(rintf(v * A.qmax) / A.qmax, 0.f), 1.f);
+    const float q = lut8 ? lut8[(int)fminf(fmaxf(rintf(v * 255.f), 0.f), 255.f)]
+                         : fminf(fmaxf(rintf(v * A.qmax) / A.qmax, 0.f), 1.f);
     if (!A.yuv420 || m == 0) {
         out[m * plane + (int64_t)gy * A.W + gx] = q;
     } else if (!(gy & 1) && !(gx & 1) && (gy >> 1) < (A.H >> 1) && (gx >> 1) < (A.W >> 1)) {
@@ -137,6 +142,13 @@ __global__ __launch_bounds__(kFThreads) void syn_fused_kernel(FusedArgs A, Level
     const int gx = ox + c;
     const int cxg = clampi(gx, A.W - 1);
 
+    __shared__ float s_lut8[256];
+    const float *lut8 = nullptr;
+    if (A.qmax == 255.f) {
+        s_lut8[threadIdx.x & 255] = (float)(threadIdx.x & 255) / 255.f;
+        lut8 = s_lut8;
+        __syncthreads();
+    }
     if (A.n_head == 2)
         for (int i = threadIdx.x; i < A.hid * 16; i += kFThreads) {
             const int j = i >> 4, f = i & 15;
@@ -407,7 +419,7 @@ __global__ __launch_bounds__(kFThreads) void syn_fused_kernel(FusedArgs A, Level
                 const int gy = oy + rb + p;
                 if (gy < A.H && gx < A.W)
 #pragma unroll
-                    for (int m = 0; m < CMID; ++m) store_out(A, out, plane, m, gy, gx, o[p][m]);
+                    for (int m = 0; m < CMID; ++m) store_out(A, out, plane, m, gy, gx, o[p][m], lut8);
             }
             return;
         }
@@ -477,7 +489,7 @@ __global__ __launch_bounds__(kFThreads) void syn_fused_kernel(FusedArgs A, Level
                     const float v = h ? acc.y : acc.x;
                     if (last) {
                         if (r >= t && r < kRH - t && c >= t && c < kRW - t && gy < A.H && col_in)
-                            store_out(A, out, plane, m, gy, gx, v);
+                            store_out(A, out, plane, m, gy, gx, v, lut8);
                     } else if (gy >= 0 && gy < A.H) {
                         float *dst = &buf(cur ^ 1)[m][0] + (r + 1) * kRW + c;
                         dst[0] = v;
