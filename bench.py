@@ -143,6 +143,8 @@ class Pipeline:
 
     STAGES = {"fused": ["arm", "ups_pyramid", "decode_fused"], "staged": ["arm", "ups", "syn", "post"]}
 
+    join_before_last = False  # overlap: the ARM joins before the last kernel (pyramid || ARM)
+
     def step(self, events=None, mode="fused", overlap=True):
         """events: len(STAGES[mode]) + 1 (+ 2 with overlap: the ARM's own pair on the side stream)."""
         import ccmi
@@ -167,16 +169,19 @@ class Pipeline:
         if events: events[n + 2].record(self.side)
         self.join.record(self.side)
         for i, (fn, a) in enumerate(calls[1:], start=1):
+            if self.join_before_last and i == n - 1:
+                self.stream.wait_event(self.join)
             if events: events[i].record(self.stream)
             ccmi.check(fn(br(a), self.stream.cuda_stream))
         if events: events[n].record(self.stream)
         self.stream.wait_event(self.join)
 
 
-def measure_path_a(inp, B, steps, warmup, mode, overlap, dist, dev):
+def measure_path_a(inp, B, steps, warmup, mode, overlap, dist, dev, join_before_last=False):
     """Time `steps` pipeline steps (after `warmup`), barrier + synchronize on both sides;
     returns (max-over-ranks seconds, per-stage ms per step from HIP events)."""
     pipe = Pipeline(inp, B, dev)
+    pipe.join_before_last = join_before_last
     names = Pipeline.STAGES[mode]
     for _ in range(warmup):
         pipe.step(mode=mode, overlap=overlap)
@@ -207,11 +212,12 @@ def measure_path_a(inp, B, steps, warmup, mode, overlap, dist, dev):
     return dt, stage_ms
 
 
-def measure_path_a_graph(inp, B, steps, warmup, dist, dev, per_graph=10):
+def measure_path_a_graph(inp, B, steps, warmup, dist, dev, per_graph=10, overlap=False):
     """The fused pipeline captured in a HIP graph (`per_graph` steps per graph, one stream):
     replays remove the host launch gaps between the step's small pyramid kernels.  Returns
     the max-over-ranks seconds for `steps` steps (a multiple of per_graph)."""
     pipe = Pipeline(inp, B, dev)
+    pipe.join_before_last = overlap
     s = torch.cuda.Stream(dev)
     s.wait_stream(torch.cuda.current_stream(dev))
     g = torch.cuda.CUDAGraph()
@@ -219,13 +225,13 @@ def measure_path_a_graph(inp, B, steps, warmup, dist, dev, per_graph=10):
     try:
         with torch.cuda.stream(s):
             pipe.stream = s
-            pipe.step(mode="fused", overlap=False)
+            pipe.step(mode="fused", overlap=overlap)
             s.synchronize()
             ref = (pipe.yuv.clone(), pipe.rate.clone())  # eager outputs, to check the replays
             # thread_local: the process group's watchdog thread may query events meanwhile
             with torch.cuda.graph(g, stream=s, capture_error_mode="thread_local"):
                 for _ in range(per_graph):
-                    pipe.step(mode="fused", overlap=False)
+                    pipe.step(mode="fused", overlap=overlap)
         torch.cuda.synchronize()
     except Exception as e:
         err = f"{type(e).__name__}: {e}"
@@ -467,6 +473,9 @@ def main():
                          "step rate is the same within noise on MI355X; kernels then share CUs, so the "
                          "roofline kernel's duration is no longer its own)")
     ap.add_argument("--serial", action="store_true", help="(default) one stream, kernels back to back")
+    ap.add_argument("--overlap-pyramid", action="store_true",
+                    help="ARM on a second stream concurrent with the upsampling pyramid only; the fused "
+                         "kernel starts after both (it then runs alone, so its roofline stays its own)")
     ap.add_argument("--no-graph", action="store_true",
                     help="time the eager launches instead of HIP-graph replays of the fused pipeline")
     ap.add_argument("--hd-steps", type=int, default=20, help="steps of the 1920x1080 float-forward leg (0: skip)")
@@ -496,8 +505,9 @@ def main():
     B = args.batch
     inp = make_inputs(B, dev, seed=1000 * rank + 1)
     mode = "staged" if args.staged else "fused"
-    overlap = args.overlap and not args.serial
-    dt, stage_ms = measure_path_a(inp, B, args.steps, args.warmup, mode, overlap, dist, dev)
+    ovp = args.overlap_pyramid and not args.serial and mode == "fused"
+    overlap = (args.overlap or ovp) and not args.serial
+    dt, stage_ms = measure_path_a(inp, B, args.steps, args.warmup, mode, overlap, dist, dev, join_before_last=ovp)
     fl = flops_per_frame()
     fl["decode_fused"] = flops_fused_per_frame()
     by = bytes_per_frame()
@@ -506,7 +516,7 @@ def main():
     traffic, src = pmc_traffic(dom, B)
 
     eager, graph_error, graph_same = None, None, None
-    graph = not (args.no_graph or args.staged or overlap)
+    graph = not (args.no_graph or args.staged or (overlap and not ovp))
     if graph:
         # headline: the same K steps replayed from HIP graphs (per-stage times and the
         # roofline above come from the event-instrumented eager pass)
@@ -514,7 +524,7 @@ def main():
                  "ms_per_step": round(dt / args.steps * 1e3, 4)}
         per = 10 if args.steps % 10 == 0 else 1
         try:
-            dt, n_done, graph_same = measure_path_a_graph(inp, B, args.steps, args.warmup, dist, dev, per)
+            dt, n_done, graph_same = measure_path_a_graph(inp, B, args.steps, args.warmup, dist, dev, per, ovp)
             assert n_done == args.steps
         except Exception as e:  # report the eager timing, and say so in the line
             graph_error = f"{type(e).__name__}: {e}"[:200]
@@ -541,7 +551,8 @@ def main():
                    "frames_per_step_per_gpu": B, "parallelism": f"image-parallel x{world}",
                    "kernels": ("ARM | upsampling pyramid | fused last-upsampling+synthesis+post" if mode == "fused"
                                else "ARM | upsampling | synthesis | post")
-                   + (" (ARM on a second stream, concurrent)" if overlap else " (one stream)")},
+                   + (" (ARM on a second stream, concurrent with the pyramid)" if ovp else
+                      " (ARM on a second stream, concurrent)" if overlap else " (one stream)")},
         "stage_ms_per_step": {k: round(v, 4) for k, v in stage_ms.items()},
         "launch": launch,
         "graph_outputs_equal_eager": graph_same,
