@@ -168,156 +168,233 @@ __device__ __forceinline__ void ctx_off(int i, int &dy, int &dx)
     dx = k % 9 - 4;
 }
 
-// Sum over the workgroup of g (R values) x a (D values) outer products and of g, written
-// as one partial row: [R][D] then [R].
+typedef float v4f __attribute__((ext_vector_type(4)));
+// v_mfma_f32_16x16x4_f32 (f32 in, f32 accumulate: an fmaf chain in another order).
+// Lane l supplies A[m = l & 15][k = l >> 4] and B[k = l >> 4][n = l & 15]; accumulator
+// register r of lane l is D[m = 4 (l >> 4) + r][n = l & 15].
+__device__ __forceinline__ v4f mfma4(float a, float b, v4f c) { return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0); }
+
+// One layer's weight gradient over a wave's 64 rows, on the matrix cores:
+// acc[mt][nt] += G^T A, G = [64][R] (pitch R + 1), A = [64][D] (pitch D + 1): a GEMM
+// whose K is the latent index, 4 latents per MFMA.
+// With B = 1 the same A operand also accumulates the bias gradient sum_k A[m][k] (accb).
 template <int R, int D>
-__device__ __forceinline__ void outer_reduce(const float (&gv)[R], const float (&av)[D], float *s_g, float *s_a,
-                                             float *__restrict__ row)
+__device__ __forceinline__ void mfma_outer(const float *s_g, const float *s_a, v4f (&acc)[(R + 15) / 16][(D + 15) / 16],
+                                           v4f (&accb)[(R + 15) / 16])
 {
-    const int t = threadIdx.x;
+    constexpr int MT = (R + 15) / 16, NT = (D + 15) / 16;
+    const int lane = threadIdx.x & 63, ln = lane & 15, lk = lane >> 4;
+#pragma unroll 4
+    for (int s = 0; s < 16; ++s) {
+        const int r = 4 * s + lk;
+        float bv[NT];
 #pragma unroll
-    for (int j = 0; j < R; ++j) s_g[t * (R + 1) + j] = gv[j];
+        for (int nt = 0; nt < NT; ++nt) bv[nt] = 16 * nt + ln < D ? s_a[r * (D + 1) + 16 * nt + ln] : 0.f;
 #pragma unroll
-    for (int i = 0; i < D; ++i) s_a[t * (D + 1) + i] = av[i];
-    __syncthreads();
-    for (int e = t; e < R * D + R; e += kT) {
-        float acc = 0.f;
-        if (e < R * D) {
-            const int j = e / D, i = e - j * D;
-            for (int k = 0; k < kT; ++k) acc = fmaf(s_g[k * (R + 1) + j], s_a[k * (D + 1) + i], acc);
-        } else {
-            const int j = e - R * D;
-            for (int k = 0; k < kT; ++k) acc += s_g[k * (R + 1) + j];
+        for (int mt = 0; mt < MT; ++mt) {
+            const float av = 16 * mt + ln < R ? s_g[r * (R + 1) + 16 * mt + ln] : 0.f;
+#pragma unroll
+            for (int nt = 0; nt < NT; ++nt) acc[mt][nt] = mfma4(av, bv[nt], acc[mt][nt]);
+            accb[mt] = mfma4(av, 1.f, accb[mt]);
         }
-        row[e] = acc;
     }
-    __syncthreads();
+}
+
+// Flush of mfma_outer's accumulators into a [R][D] weight-gradient block and its [R] bias.
+template <int R, int D>
+__device__ __forceinline__ void flush_outer(const v4f (&acc)[(R + 15) / 16][(D + 15) / 16], const v4f (&accb)[(R + 15) / 16],
+                                            float *__restrict__ dst, float *__restrict__ dstb)
+{
+    constexpr int MT = (R + 15) / 16, NT = (D + 15) / 16;
+    const int lane = threadIdx.x & 63, ln = lane & 15, lk = lane >> 4;
+#pragma unroll
+    for (int mt = 0; mt < MT; ++mt)
+#pragma unroll
+        for (int nt = 0; nt < NT; ++nt)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                const int m = 16 * mt + 4 * lk + r, n = 16 * nt + ln;
+                if (m < R && n < D) atomicAdd(&dst[m * D + n], acc[mt][nt][r]);
+                if (nt == 0 && m < R && ln == 0) atomicAdd(&dstb[m], accb[mt][r]);
+            }
+}
+
+// Orders a wave's LDS stores before its own later LDS loads of other lanes' rows: a wave's
+// LDS instructions execute in order, so only the compiler must not move them across.
+__device__ __forceinline__ void wave_lds_sync()
+{
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+// Sum over the wave of v, added to *dst by lane 0.
+__device__ __forceinline__ void wave_add(float v, float *dst)
+{
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
+    if ((threadIdx.x & 63) == 0) atomicAdd(dst, v);
 }
 
 template <int D, int NH>
 __global__ __launch_bounds__(kT) void t_arm(const float *__restrict__ yq, Geo g, ArmTiles at, const float *__restrict__ th,
                                             int64_t ps, float lam_px, float *__restrict__ gq,
-                                            float *__restrict__ part, int nblk, float *__restrict__ acc4)
+                                            float *__restrict__ gth, int64_t gstride, float *__restrict__ acc4)
 {
+    constexpr int NT = (D + 15) / 16, MT = (D + 15) / 16;
     __shared__ float s_y[kALH][kALW];
     __shared__ float s_gy[kALH][kALW];
     __shared__ float s_g[kT * (D + 1)];
     __shared__ float s_a[kT * (D + 1)];
-    __shared__ float s_red[8];
 
-    const int b = blockIdx.y, t = blockIdx.x;
-    int l = 0;
-#pragma unroll
-    for (int k = 1; k < CCMI_MAX_GRIDS; ++k)
-        if (k < at.n && t >= at.start[k]) l = k;
-    const int lt = t - at.start[l];
-    const int H = g.h[l], W = g.w[l];
-    const int y0 = (lt / at.tiles_x[l]) * kATY, x0 = (lt % at.tiles_x[l]) * kATX;
-    const float *src = yq + (int64_t)b * g.N + g.off[l];
-    float *gdst = gq + (int64_t)b * g.N + g.off[l];
-    for (int i = threadIdx.x; i < kALH * kALW; i += kT) {
-        const int r = i / kALW, c = i - r * kALW;
-        const int y = y0 - kAH + r, x = x0 - kAH + c;
-        s_y[r][c] = (y >= 0 && y < H && x >= 0 && x < W) ? src[y * W + x] : 0.f;
-        s_gy[r][c] = 0.f;
-    }
-    __syncthreads();
-
-    const int cx = threadIdx.x % kATX, cy = threadIdx.x / kATX;
-    const bool valid = (y0 + cy) < H && (x0 + cx) < W;
+    const int b = blockIdx.y;
+    const int w = threadIdx.x >> 6;
     const cfloat_ptr P = (cfloat_ptr)(size_t)(th + (int64_t)b * ps);
+    float *sg = s_g + 64 * w * (D + 1), *sa = s_a + 64 * w * (D + 1); // this wave's rows
+    const int cx = threadIdx.x % kATX, cy = threadIdx.x / kATX;
+    // weight-gradient accumulators (matrix cores) and bias-gradient sums (VALU), kept over
+    // every tile this workgroup visits
+    v4f acc_o[1][NT], acc_h[NH > 0 ? NH : 1][MT][NT], accb_o[1], accb_h[NH > 0 ? NH : 1][MT];
+    const v4f z4 = {0.f, 0.f, 0.f, 0.f};
+    accb_o[0] = z4;
+#pragma unroll
+    for (int nt = 0; nt < NT; ++nt) acc_o[0][nt] = z4;
+#pragma unroll
+    for (int L = 0; L < (NH > 0 ? NH : 1); ++L)
+#pragma unroll
+        for (int mt = 0; mt < MT; ++mt) {
+            accb_h[L][mt] = z4;
+#pragma unroll
+            for (int nt = 0; nt < NT; ++nt) acc_h[L][mt][nt] = z4;
+        }
+    float rsum = 0.f;
 
-    float xs[NH + 1][D];
+    for (int t = blockIdx.x; t < at.start[at.n]; t += gridDim.x) {
+        int l = 0;
 #pragma unroll
-    for (int i = 0; i < D; ++i) {
-        int dy, dx;
-        ctx_off<D>(i, dy, dx);
-        xs[0][i] = s_y[cy + kAH + dy][cx + kAH + dx];
-    }
-#pragma unroll
-    for (int L = 0; L < NH; ++L) {
-        const cfloat_ptr Wl = P + L * (D * D + D);
-#pragma unroll
-        for (int j = 0; j < D; ++j) {
-            float z = Wl[D * D + j];
-#pragma unroll
-            for (int i = 0; i < D; ++i) z = fmaf(Wl[j * D + i], xs[L][i], z);
-            z += xs[L][j];
-            xs[L + 1][j] = fmaxf(z, 0.f);
+        for (int k = 1; k < CCMI_MAX_GRIDS; ++k)
+            if (k < at.n && t >= at.start[k]) l = k;
+        const int lt = t - at.start[l];
+        const int H = g.h[l], W = g.w[l];
+        const int y0 = (lt / at.tiles_x[l]) * kATY, x0 = (lt % at.tiles_x[l]) * kATX;
+        const float *src = yq + (int64_t)b * g.N + g.off[l];
+        float *gdst = gq + (int64_t)b * g.N + g.off[l];
+        __syncthreads(); // previous tile's LDS readers are done
+        for (int i = threadIdx.x; i < kALH * kALW; i += kT) {
+            const int r = i / kALW, c = i - r * kALW;
+            const int y = y0 - kAH + r, x = x0 - kAH + c;
+            s_y[r][c] = (y >= 0 && y < H && x >= 0 && x < W) ? src[y * W + x] : 0.f;
+            s_gy[r][c] = 0.f;
         }
-    }
-    const cfloat_ptr Wo = P + NH * (D * D + D);
-    float mu = Wo[2 * D], ls = Wo[2 * D + 1];
-#pragma unroll
-    for (int i = 0; i < D; ++i) {
-        mu = fmaf(Wo[i], xs[NH][i], mu);
-        ls = fmaf(Wo[D + i], xs[NH][i], ls);
-    }
-    // scale = exp(clamp(ls - 4, -4.6, 5)) (arm.py:262-266); rate (coolchic.py:419-424)
-    const float l4 = ls - 4.f, sig = expf(fminf(fmaxf(l4, -4.6f), 5.0f));
-    const float q = s_y[cy + kAH][cx + kAH];
-    const float s1 = q + 0.5f - mu, s2 = q - 0.5f - mu;
-    const float sg1 = s1 > 0.f ? 1.f : (s1 < 0.f ? -1.f : 0.f), sg2 = s2 > 0.f ? 1.f : (s2 < 0.f ? -1.f : 0.f);
-    const float F1 = 0.5f - 0.5f * sg1 * expm1f(-fabsf(s1) / sig), F2 = 0.5f - 0.5f * sg2 * expm1f(-fabsf(s2) / sig);
-    const float Pr = F1 - F2;
-    float rate = 0.f, g_q = 0.f, g_mu = 0.f, g_ls = 0.f;
-    if (valid) {
-        rate = -log2f(fmaxf(Pr, 1.52587890625e-05f));
-        if (Pr >= 1.52587890625e-05f) { // clamp_min passes the gradient where P >= 2^-16
-            const float dLdP = -lam_px / (Pr * kLn2);
-            const float e1 = expf(-fabsf(s1) / sig), e2 = expf(-fabsf(s2) / sig);
-            // torch autograd of 0.5 - 0.5 sign(s) expm1(-|s|/sig): d/ds = 0.5 sign(s)^2 e / sig
-            const float Fs1 = 0.5f * sg1 * sg1 * e1 / sig, Fs2 = 0.5f * sg2 * sg2 * e2 / sig;
-            const float Fg1 = -0.5f * sg1 * e1 * fabsf(s1) / (sig * sig), Fg2 = -0.5f * sg2 * e2 * fabsf(s2) / (sig * sig);
-            g_q = dLdP * (Fs1 - Fs2);
-            g_mu = -g_q;
-            const float g_sig = dLdP * (Fg1 - Fg2);
-            g_ls = (l4 >= -4.6f && l4 <= 5.0f) ? g_sig * sig : 0.f;
-        }
-    }
-    // ---- backward through the MLP; weight-gradient partial rows per workgroup
-    float *row = part + ((int64_t)b * nblk + t) * g.P_arm;
-    float gx[D];
-    {
-        const float go[2] = {g_mu, g_ls};
-#pragma unroll
-        for (int i = 0; i < D; ++i) gx[i] = Wo[i] * g_mu + Wo[D + i] * g_ls;
-        outer_reduce<2, D>(go, xs[NH], s_g, s_a, row + NH * (D * D + D));
-    }
-#pragma unroll
-    for (int L = NH - 1; L >= 0; --L) {
-        const cfloat_ptr Wl = P + L * (D * D + D);
-        float gz[D];
-#pragma unroll
-        for (int j = 0; j < D; ++j) gz[j] = xs[L + 1][j] > 0.f ? gx[j] : 0.f;
-        outer_reduce<D, D>(gz, xs[L], s_g, s_a, row + L * (D * D + D));
-#pragma unroll
-        for (int i = 0; i < D; ++i) {
-            float a = gz[i]; // residual
-#pragma unroll
-            for (int j = 0; j < D; ++j) a = fmaf(Wl[j * D + i], gz[j], a);
-            gx[i] = a;
-        }
-    }
-    // ---- context gradients -> LDS tile, then one global atomic per touched position
-    if (valid) {
+        __syncthreads();
+        const bool valid = (y0 + cy) < H && (x0 + cx) < W;
+
+        float xs[NH + 1][D];
 #pragma unroll
         for (int i = 0; i < D; ++i) {
             int dy, dx;
             ctx_off<D>(i, dy, dx);
-            atomicAdd(&s_gy[cy + kAH + dy][cx + kAH + dx], gx[i]);
+            xs[0][i] = s_y[cy + kAH + dy][cx + kAH + dx];
         }
-        atomicAdd(&s_gy[cy + kAH][cx + kAH], g_q);
+#pragma unroll
+        for (int L = 0; L < NH; ++L) {
+            const cfloat_ptr Wl = P + L * (D * D + D);
+#pragma unroll
+            for (int j = 0; j < D; ++j) {
+                float z = Wl[D * D + j];
+#pragma unroll
+                for (int i = 0; i < D; ++i) z = fmaf(Wl[j * D + i], xs[L][i], z);
+                z += xs[L][j];
+                xs[L + 1][j] = fmaxf(z, 0.f);
+            }
+        }
+        const cfloat_ptr Wo = P + NH * (D * D + D);
+        float mu = Wo[2 * D], ls = Wo[2 * D + 1];
+#pragma unroll
+        for (int i = 0; i < D; ++i) {
+            mu = fmaf(Wo[i], xs[NH][i], mu);
+            ls = fmaf(Wo[D + i], xs[NH][i], ls);
+        }
+        // scale = exp(clamp(ls - 4, -4.6, 5)) (arm.py:262-266); rate (coolchic.py:419-424)
+        const float l4 = ls - 4.f, sig = expf(fminf(fmaxf(l4, -4.6f), 5.0f));
+        const float q = s_y[cy + kAH][cx + kAH];
+        const float s1 = q + 0.5f - mu, s2 = q - 0.5f - mu;
+        const float sg1 = s1 > 0.f ? 1.f : (s1 < 0.f ? -1.f : 0.f), sg2 = s2 > 0.f ? 1.f : (s2 < 0.f ? -1.f : 0.f);
+        const float F1 = 0.5f - 0.5f * sg1 * expm1f(-fabsf(s1) / sig), F2 = 0.5f - 0.5f * sg2 * expm1f(-fabsf(s2) / sig);
+        const float Pr = F1 - F2;
+        float g_q = 0.f, g_mu = 0.f, g_ls = 0.f;
+        if (valid) {
+            rsum += -log2f(fmaxf(Pr, 1.52587890625e-05f));
+            if (Pr >= 1.52587890625e-05f) { // clamp_min passes the gradient where P >= 2^-16
+                const float dLdP = -lam_px / (Pr * kLn2);
+                const float e1 = expf(-fabsf(s1) / sig), e2 = expf(-fabsf(s2) / sig);
+                // torch autograd of 0.5 - 0.5 sign(s) expm1(-|s|/sig): d/ds = 0.5 sign(s)^2 e / sig
+                const float Fs1 = 0.5f * sg1 * sg1 * e1 / sig, Fs2 = 0.5f * sg2 * sg2 * e2 / sig;
+                const float Fg1 = -0.5f * sg1 * e1 * fabsf(s1) / (sig * sig), Fg2 = -0.5f * sg2 * e2 * fabsf(s2) / (sig * sig);
+                g_q = dLdP * (Fs1 - Fs2);
+                g_mu = -g_q;
+                const float g_sig = dLdP * (Fg1 - Fg2);
+                g_ls = (l4 >= -4.6f && l4 <= 5.0f) ? g_sig * sig : 0.f;
+            }
+        }
+        // ---- backward through the MLP; weight gradients on the matrix cores
+        float gx[D];
+        {
+#pragma unroll
+            for (int i = 0; i < D; ++i) gx[i] = Wo[i] * g_mu + Wo[D + i] * g_ls;
+            sg[(threadIdx.x & 63) * 3 + 0] = g_mu; // [64][2], pitch 3
+            sg[(threadIdx.x & 63) * 3 + 1] = g_ls;
+#pragma unroll
+            for (int i = 0; i < D; ++i) sa[(threadIdx.x & 63) * (D + 1) + i] = xs[NH][i];
+            wave_lds_sync(); // each wave stages and reads only its own 64 rows
+            mfma_outer<2, D>(sg, sa, acc_o, accb_o);
+            wave_lds_sync();
+        }
+#pragma unroll
+        for (int L = NH - 1; L >= 0; --L) {
+            const cfloat_ptr Wl = P + L * (D * D + D);
+            float gz[D];
+#pragma unroll
+            for (int j = 0; j < D; ++j) {
+                gz[j] = xs[L + 1][j] > 0.f ? gx[j] : 0.f;
+                sg[(threadIdx.x & 63) * (D + 1) + j] = gz[j];
+            }
+#pragma unroll
+            for (int i = 0; i < D; ++i) sa[(threadIdx.x & 63) * (D + 1) + i] = xs[L][i];
+            wave_lds_sync();
+            mfma_outer<D, D>(sg, sa, acc_h[L], accb_h[L]);
+            wave_lds_sync();
+#pragma unroll
+            for (int i = 0; i < D; ++i) {
+                float a = gz[i]; // residual
+#pragma unroll
+                for (int j = 0; j < D; ++j) a = fmaf(Wl[j * D + i], gz[j], a);
+                gx[i] = a;
+            }
+        }
+        // ---- context gradients -> LDS tile, then one global atomic per touched position
+        if (valid) {
+#pragma unroll
+            for (int i = 0; i < D; ++i) {
+                int dy, dx;
+                ctx_off<D>(i, dy, dx);
+                atomicAdd(&s_gy[cy + kAH + dy][cx + kAH + dx], gx[i]);
+            }
+            atomicAdd(&s_gy[cy + kAH][cx + kAH], g_q);
+        }
+        __syncthreads();
+        for (int i = threadIdx.x; i < kALH * kALW; i += kT) {
+            const int r = i / kALW, c = i - r * kALW;
+            const int y = y0 - kAH + r, x = x0 - kAH + c;
+            const float v = s_gy[r][c];
+            if (y >= 0 && y < H && x >= 0 && x < W && v != 0.f) atomicAdd(&gdst[y * W + x], v);
+        }
     }
-    const float rsum = block_sum(rate, s_red);
-    __syncthreads();
-    for (int i = threadIdx.x; i < kALH * kALW; i += kT) {
-        const int r = i / kALW, c = i - r * kALW;
-        const int y = y0 - kAH + r, x = x0 - kAH + c;
-        const float v = s_gy[r][c];
-        if (y >= 0 && y < H && x >= 0 && x < W && v != 0.f) atomicAdd(&gdst[y * W + x], v);
-    }
-    if (threadIdx.x == 0) atomicAdd(&acc4[b * 4 + 1], rsum);
+    // ---- flush this wave's weight / bias gradients and rate
+    float *G = gth + (int64_t)b * gstride;
+    flush_outer<2, D>(acc_o, accb_o, G + NH * (D * D + D), G + NH * (D * D + D) + 2 * D);
+#pragma unroll
+    for (int L = 0; L < NH; ++L) flush_outer<D, D>(acc_h[L], accb_h[L], G + L * (D * D + D), G + L * (D * D + D) + D * D);
+    wave_add(rsum, &acc4[b * 4 + 1]);
 }
 
 // Column sums of per-workgroup partial rows: dst[b][col] += sum_r part[b][r][col].
@@ -470,61 +547,114 @@ __device__ __forceinline__ void qrange(int p, int dd, int n, int &lo, int &hi)
     }
 }
 
-// 3x3 layer backward: g_in (gather) and weight / bias gradients (block reduction + atomics).
-__global__ __launch_bounds__(kT) void t_sp_bwd(const float *__restrict__ gpre, const float *__restrict__ in, Geo g,
-                                               const float *__restrict__ th, int64_t ps, int wo, int bo, int res,
-                                               float *__restrict__ gin, float *__restrict__ gth, int64_t gstride)
+// 3x3 layer backward on 16 x 64 pixel tiles staged in LDS (grid-stride over the tiles).
+//  * X (the layer input) at replicate-clamped coordinates over the tile + 1-pixel ring:
+//    dW[c][i][ky][kx] += G[c][q] X[i][clamp(q + (ky-1, kx-1))], accumulated per thread in
+//    registers over every tile the workgroup visits, reduced once at the end;
+//  * G (the output gradient, times relu'(out) when the layer has a ReLU: the old
+//    t_sp_gpre fused in) over the same ring, zero outside the image: the input gradient of
+//    an interior pixel p is the plain correlation sum_{c,k} W[c][i][k] G[c][p - d_k]; a
+//    pixel on the image border also collects the taps that the replicate padding clamps
+//    onto it (qrange), all within the ring.
+constexpr int kSY = 16, kSX = 64;
+__global__ __launch_bounds__(kT) void t_sp_bwd(const float *__restrict__ gout, const float *__restrict__ outp,
+                                               const float *__restrict__ in, Geo g, const float *__restrict__ th,
+                                               int64_t ps, int wo, int bo, int res, float *__restrict__ gin,
+                                               float *__restrict__ gth, int64_t gstride)
 {
+    constexpr int RH = kSY + 2, RW = kSX + 2;
+    __shared__ float sX[3][RH][RW];
+    __shared__ float sG[3][RH][RW];
     __shared__ float s_red[4][84];
     const int b = blockIdx.y;
-    const int64_t npx = (int64_t)g.H * g.W;
+    const int H = g.H, W = g.W;
+    const int64_t npx = (int64_t)H * W;
     const cfloat_ptr P = (cfloat_ptr)(size_t)(th + (int64_t)b * ps);
-    const float *G = gpre + (int64_t)b * 3 * npx;
-    const float *X = in + (int64_t)b * 3 * npx;
+    const float *Gb = gout + (int64_t)b * 3 * npx;
+    const float *Ob = outp ? outp + (int64_t)b * 3 * npx : nullptr;
+    const float *Xb = in + (int64_t)b * 3 * npx;
+    float *Ib = gin + (int64_t)b * 3 * npx;
+    const int tx = (W + kSX - 1) / kSX, ntile = tx * ((H + kSY - 1) / kSY);
+    const int c = threadIdx.x & 63, rb = (threadIdx.x >> 6) * 4;
     float acc[84];
 #pragma unroll
     for (int e = 0; e < 84; ++e) acc[e] = 0.f;
-    for (int64_t p = (int64_t)blockIdx.x * kT + threadIdx.x; p < npx; p += (int64_t)gridDim.x * kT) {
-        const int py = (int)(p / g.W), px = (int)(p - (int64_t)py * g.W);
-        // weight gradients at output q = p
-        float gp[3];
+    for (int t = blockIdx.x; t < ntile; t += gridDim.x) {
+        const int y0 = (t / tx) * kSY, x0 = (t % tx) * kSX;
+        __syncthreads();
+        for (int i = threadIdx.x; i < RH * RW; i += kT) {
+            const int r = i / RW, q = i - r * RW;
+            const int y = y0 - 1 + r, x = x0 - 1 + q;
+            const int64_t cl = (int64_t)clampi(y, H - 1) * W + clampi(x, W - 1);
+            const bool in_img = y >= 0 && y < H && x >= 0 && x < W;
 #pragma unroll
-        for (int c = 0; c < 3; ++c) gp[c] = G[c * npx + p];
-#pragma unroll
-        for (int k = 0; k < 9; ++k) {
-            const int yy = clampi(py + k / 3 - 1, g.H - 1), xx = clampi(px + k % 3 - 1, g.W - 1);
-#pragma unroll
-            for (int i = 0; i < 3; ++i) {
-                const float xv = X[i * npx + (int64_t)yy * g.W + xx];
-#pragma unroll
-                for (int c = 0; c < 3; ++c) acc[(c * 3 + i) * 9 + k] = fmaf(gp[c], xv, acc[(c * 3 + i) * 9 + k]);
+            for (int ch = 0; ch < 3; ++ch) {
+                sX[ch][r][q] = Xb[ch * npx + cl];
+                float gv = 0.f;
+                if (in_img) {
+                    gv = Gb[ch * npx + cl];
+                    if (Ob && Ob[ch * npx + cl] <= 0.f) gv = 0.f;
+                }
+                sG[ch][r][q] = gv;
             }
         }
+        __syncthreads();
+        const int px = x0 + c;
+#pragma unroll 1
+        for (int pr = 0; pr < 4; ++pr) {
+            const int ry = rb + pr, py = y0 + ry;
+            if (py >= H || px >= W) continue;
+            // weight / bias gradients at output q = (py, px)
+            float gp[3];
 #pragma unroll
-        for (int c = 0; c < 3; ++c) acc[81 + c] += gp[c];
-        // input gradient at p: sum over (q, tap) with clamp(q + tap - 1) == p
-        float gi[3] = {0.f, 0.f, 0.f};
-        for (int ky = 0; ky < 3; ++ky) {
-            int qy0, qy1;
-            qrange(py, ky - 1, g.H, qy0, qy1);
-            for (int qy = qy0; qy <= qy1; ++qy)
-                for (int kx = 0; kx < 3; ++kx) {
-                    int qx0, qx1;
-                    qrange(px, kx - 1, g.W, qx0, qx1);
-                    for (int qx = qx0; qx <= qx1; ++qx) {
-                        const int64_t q = (int64_t)qy * g.W + qx;
+            for (int ch = 0; ch < 3; ++ch) gp[ch] = sG[ch][ry + 1][c + 1];
 #pragma unroll
-                        for (int c = 0; c < 3; ++c) {
-                            const float gq = G[c * npx + q];
+            for (int i = 0; i < 3; ++i)
 #pragma unroll
-                            for (int i = 0; i < 3; ++i) gi[i] = fmaf(P[wo + (c * 3 + i) * 9 + ky * 3 + kx], gq, gi[i]);
-                        }
+                for (int k = 0; k < 9; ++k) {
+                    const float xv = sX[i][ry + k / 3][c + k % 3];
+#pragma unroll
+                    for (int oc = 0; oc < 3; ++oc) acc[(oc * 3 + i) * 9 + k] = fmaf(gp[oc], xv, acc[(oc * 3 + i) * 9 + k]);
+                }
+#pragma unroll
+            for (int oc = 0; oc < 3; ++oc) acc[81 + oc] += gp[oc];
+            // input gradient at p = (py, px)
+            float gi[3] = {0.f, 0.f, 0.f};
+            if (py > 0 && py < H - 1 && px > 0 && px < W - 1) {
+#pragma unroll
+                for (int k = 0; k < 9; ++k) {
+                    const int ky = k / 3, kx = k % 3;
+#pragma unroll
+                    for (int oc = 0; oc < 3; ++oc) {
+                        const float gq = sG[oc][ry + 2 - ky][c + 2 - kx];
+#pragma unroll
+                        for (int i = 0; i < 3; ++i) gi[i] = fmaf(P[wo + (oc * 3 + i) * 9 + k], gq, gi[i]);
                     }
                 }
-        }
-        float *o = gin + (int64_t)b * 3 * npx + p;
+            } else {
+                for (int ky = 0; ky < 3; ++ky) {
+                    int qy0, qy1;
+                    qrange(py, ky - 1, H, qy0, qy1);
+                    for (int qy = qy0; qy <= qy1; ++qy)
+                        for (int kx = 0; kx < 3; ++kx) {
+                            int qx0, qx1;
+                            qrange(px, kx - 1, W, qx0, qx1);
+                            for (int qx = qx0; qx <= qx1; ++qx) {
 #pragma unroll
-        for (int i = 0; i < 3; ++i) o[i * npx] = gi[i] + (res ? gp[i] : 0.f);
+                                for (int oc = 0; oc < 3; ++oc) {
+                                    const float gq = sG[oc][qy - y0 + 1][qx - x0 + 1];
+#pragma unroll
+                                    for (int i = 0; i < 3; ++i)
+                                        gi[i] = fmaf(P[wo + (oc * 3 + i) * 9 + ky * 3 + kx], gq, gi[i]);
+                                }
+                            }
+                        }
+                }
+            }
+            const int64_t pi = (int64_t)py * W + px;
+#pragma unroll
+            for (int i = 0; i < 3; ++i) Ib[i * npx + pi] = gi[i] + (res ? gp[i] : 0.f);
+        }
     }
     // block reduction of the 84 weight / bias gradients
     const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
@@ -543,109 +673,156 @@ __global__ __launch_bounds__(kT) void t_sp_bwd(const float *__restrict__ gpre, c
     }
 }
 
-// 1x1 head backward: g_dense, and the weight gradients as partial rows
-// [W0 (hid x CIN), b0 (hid), W1 (3 x hid), b1 (3)] per workgroup of kHeadT pixels.
-template <int CIN>
+// 1x1 head backward.  Per pixel (lane = pixel, VALU): the hidden layer recomputed, g_h and
+// g_dense.  The weight gradients are sums over pixels -- GEMMs with K = pixels -- and run on
+// the matrix cores (v_mfma_f32_16x16x4_f32, f32 in / f32 accumulate: the same products as
+// an fmaf chain, only the summation order differs):
+//   dW1[k][j] = sum_px gp[px][k] h[px][j]          (M = k < 3, N = j, one MFMA per 16 j)
+//   dW0[j][i] = sum_px gh[px][j] [x[px][i] | 1]    (M = j, N = i <= CIN, column CIN = db0)
+// A wave stages its 64 pixels' rows in LDS (pixel-major, pitch kHP: conflict-free writes)
+// and feeds 4 pixels per MFMA (K = lane >> 4).  Accumulators live in registers across
+// every pixel chunk the workgroup visits (grid-stride) and are flushed once, with one
+// atomic per weight per wave.
+template <int CIN, int NT>
 __global__ __launch_bounds__(kHeadT) void t_head_bwd(const float *__restrict__ dense, const float *__restrict__ gz0, Geo g,
                                                      const float *__restrict__ th, int64_t ps, float *__restrict__ gdense,
-                                                     float *__restrict__ part, int nblk)
+                                                     float *__restrict__ gth, int64_t gstride)
 {
-    extern __shared__ float s_mem[];
-    const int b = blockIdx.y, t = threadIdx.x;
-    const int hid = g.hid;
-    const int64_t npx = (int64_t)g.H * g.W, p = (int64_t)blockIdx.x * kHeadT + t;
-    const bool valid = p < npx;
-    const cfloat_ptr P = (cfloat_ptr)(size_t)(th + (int64_t)b * ps);
-    float xv[CIN], h[64], gp1[3];
-    const float *x = dense + (int64_t)b * CIN * npx + p;
-#pragma unroll
-    for (int i = 0; i < CIN; ++i) xv[i] = valid ? x[i * npx] : 0.f;
-    float o0 = P[g.b1], o1 = P[g.b1 + 1], o2 = P[g.b1 + 2];
-#pragma unroll
-    for (int j = 0; j < 64; ++j) {
+    // dynamic LDS, per wave: [64][hp] h, then g_h (pixel-major, hp = hid | 1: conflict-free
+    // row writes); [64][9] gp, then [x | 1]
+    extern __shared__ float s_dyn[];
+    // hidden unit j: w0[j][0..CIN), b0[j], w1[0..3)[j] -- read back as broadcast ds_read_b128
+    __shared__ __attribute__((aligned(16))) float s_rec[64][12];
+    static_assert(CIN + 4 <= 12, "hidden-unit record");
+    const int b = blockIdx.y, t = threadIdx.x, lane = t & 63, w = t >> 6;
+    const int hid = g.hid, hp = hid | 1; // NT = ceil(hid / 16), a template argument: the
+                                         // accumulator tiles must be compile-time registers
+    const int64_t npx = (int64_t)g.H * g.W;
+    const float *P = th + (int64_t)b * ps;
+    for (int e = t; e < 64 * 12; e += kHeadT) {
+        const int j = e / 12, f = e - j * 12;
+        float v = 0.f;
         if (j < hid) {
-            float a = P[g.b0 + j];
-#pragma unroll
-            for (int i = 0; i < CIN; ++i) a = fmaf(P[g.w0 + j * CIN + i], xv[i], a);
-            if (g.r0) a = fmaxf(a, 0.f);
-            h[j] = a;
-            o0 = fmaf(P[g.w1 + j], a, o0);
-            o1 = fmaf(P[g.w1 + hid + j], a, o1);
-            o2 = fmaf(P[g.w1 + 2 * hid + j], a, o2);
-        } else {
-            h[j] = 0.f;
+            if (f < CIN) v = P[g.w0 + j * CIN + f];
+            else if (f == CIN) v = P[g.b0 + j];
+            else if (f <= CIN + 3) v = P[g.w1 + (f - CIN - 1) * hid + j];
         }
+        s_rec[j][f] = v;
     }
-    {
+    const float bo0 = P[g.b1], bo1 = P[g.b1 + 1], bo2 = P[g.b1 + 2];
+    float *sv = s_dyn + w * 64 * (hp + 9), *sw = sv + 64 * hp;
+    const int ln = lane & 15, lk = lane >> 4;
+    v4f a1[NT], a0[NT];
+#pragma unroll
+    for (int q = 0; q < NT; ++q) a1[q] = a0[q] = v4f{0.f, 0.f, 0.f, 0.f};
+    float db1[3] = {0.f, 0.f, 0.f};
+    __syncthreads(); // s_rec staged
+    const int64_t nchunk = (npx + kHeadT - 1) / kHeadT;
+    for (int64_t ch = blockIdx.x; ch < nchunk; ch += gridDim.x) {
+        const int64_t p = ch * kHeadT + t;
+        const bool valid = p < npx;
+        float xv[CIN], gp1[3];
+        const float *x = dense + (int64_t)b * CIN * npx + p;
+#pragma unroll
+        for (int i = 0; i < CIN; ++i) xv[i] = valid ? x[i * npx] : 0.f;
         const float *G = gz0 + (int64_t)b * 3 * npx + p;
         gp1[0] = valid ? G[0] : 0.f;
         gp1[1] = valid ? G[npx] : 0.f;
         gp1[2] = valid ? G[2 * npx] : 0.f;
+        // ---- hidden layer (kept in this lane's LDS row) and the output pre-activations
+        float o0 = bo0, o1 = bo1, o2 = bo2;
+#pragma unroll 4
+        for (int j = 0; j < hid; ++j) {
+            const float *r = s_rec[j];
+            float a = r[CIN];
+#pragma unroll
+            for (int i = 0; i < CIN; ++i) a = fmaf(r[i], xv[i], a);
+            if (g.r0) a = fmaxf(a, 0.f);
+            sv[lane * hp + j] = a;
+            o0 = fmaf(r[CIN + 1], a, o0);
+            o1 = fmaf(r[CIN + 2], a, o1);
+            o2 = fmaf(r[CIN + 3], a, o2);
+        }
         if (g.r1) {
             if (o0 <= 0.f) gp1[0] = 0.f;
             if (o1 <= 0.f) gp1[1] = 0.f;
             if (o2 <= 0.f) gp1[2] = 0.f;
         }
-    }
-    float *row = part + ((int64_t)b * nblk + blockIdx.x) * g.P_head;
-    const int ph = hid + 1;
-    // phase A: W1 (3 x hid), b1
-    float *s_h = s_mem, *s_gp = s_mem + kHeadT * ph;
 #pragma unroll
-    for (int j = 0; j < 64; ++j)
-        if (j < hid) s_h[t * ph + j] = h[j];
-    s_gp[t * 4 + 0] = gp1[0];
-    s_gp[t * 4 + 1] = gp1[1];
-    s_gp[t * 4 + 2] = gp1[2];
-    __syncthreads();
-    const int wA = g.w1 - g.w0;
-    for (int e = t; e < 3 * hid + 3; e += kHeadT) {
-        float a = 0.f;
-        if (e < 3 * hid) {
-            const int k = e / hid, j = e - k * hid;
-            for (int r = 0; r < kHeadT; ++r) a = fmaf(s_gp[r * 4 + k], s_h[r * ph + j], a);
-        } else {
-            for (int r = 0; r < kHeadT; ++r) a += s_gp[r * 4 + (e - 3 * hid)];
+        for (int k = 0; k < 3; ++k) db1[k] += gp1[k];
+        // ---- dW1 += gp^T h (invalid pixels have gp = 0)
+#pragma unroll
+        for (int k = 0; k < 3; ++k) sw[lane * 4 + k] = gp1[k];
+        wave_lds_sync();
+#pragma unroll 4
+        for (int s = 0; s < 16; ++s) {
+            const int px = 4 * s + lk;
+            const float a = ln < 3 ? sw[px * 4 + ln] : 0.f;
+#pragma unroll
+            for (int q = 0; q < NT; ++q) {
+                const int j = 16 * q + ln;
+                a1[q] = mfma4(a, j < hid ? sv[px * hp + j] : 0.f, a1[q]);
+            }
         }
-        row[wA + e] = a;
+        wave_lds_sync();
+        // ---- g_h (replaces h in this lane's row), g_x
+        float gxv[CIN];
+#pragma unroll
+        for (int i = 0; i < CIN; ++i) gxv[i] = 0.f;
+#pragma unroll 4
+        for (int j = 0; j < hid; ++j) {
+            const float *r = s_rec[j];
+            float gh = r[CIN + 1] * gp1[0] + r[CIN + 2] * gp1[1] + r[CIN + 3] * gp1[2];
+            if (g.r0 && sv[lane * hp + j] <= 0.f) gh = 0.f;
+            sv[lane * hp + j] = gh;
+#pragma unroll
+            for (int i = 0; i < CIN; ++i) gxv[i] = fmaf(r[i], gh, gxv[i]);
+        }
+        if (valid) {
+            float *gd = gdense + (int64_t)b * CIN * npx + p;
+#pragma unroll
+            for (int i = 0; i < CIN; ++i) gd[i * npx] = gxv[i];
+        }
+        // ---- dW0 | db0 += g_h^T [x | 1]
+#pragma unroll
+        for (int i = 0; i < CIN; ++i) sw[lane * 9 + i] = xv[i];
+        sw[lane * 9 + CIN] = 1.f;
+        wave_lds_sync();
+#pragma unroll 4
+        for (int s = 0; s < 16; ++s) {
+            const int px = 4 * s + lk;
+            const float bb = ln <= CIN ? sw[px * 9 + ln] : 0.f;
+#pragma unroll
+            for (int q = 0; q < NT; ++q) {
+                const int j = 16 * q + ln;
+                a0[q] = mfma4(j < hid ? sv[px * hp + j] : 0.f, bb, a0[q]);
+            }
+        }
+        wave_lds_sync();
     }
-    __syncthreads();
-    // g_h, g_x
-    float gxv[CIN];
+    // ---- flush: accumulator register r of lane l holds D[m = 4 (l >> 4) + r][n = l & 15]
+    float *Gp = gth + (int64_t)b * gstride;
 #pragma unroll
-    for (int i = 0; i < CIN; ++i) gxv[i] = 0.f;
+    for (int q = 0; q < NT; ++q) {
 #pragma unroll
-    for (int j = 0; j < 64; ++j) {
-        if (j < hid) {
-            float gh = P[g.w1 + j] * gp1[0] + P[g.w1 + hid + j] * gp1[1] + P[g.w1 + 2 * hid + j] * gp1[2];
-            if (g.r0 && h[j] <= 0.f) gh = 0.f;
-            h[j] = gh;
-#pragma unroll
-            for (int i = 0; i < CIN; ++i) gxv[i] = fmaf(P[g.w0 + j * CIN + i], gh, gxv[i]);
+        for (int r = 0; r < 4; ++r) {
+            const int m = 4 * lk + r;
+            if (m < 3) { // dW1[k = m][j]
+                const int j = 16 * q + ln;
+                if (j < hid) atomicAdd(&Gp[g.w1 + m * hid + j], a1[q][r]);
+            }
+            const int j = 16 * q + m; // dW0[j][i = ln]
+            if (j < hid) {
+                if (ln < CIN) atomicAdd(&Gp[g.w0 + j * CIN + ln], a0[q][r]);
+                else if (ln == CIN) atomicAdd(&Gp[g.b0 + j], a0[q][r]);
+            }
         }
     }
-    if (valid) {
-        float *gd = gdense + (int64_t)b * CIN * npx + p;
 #pragma unroll
-        for (int i = 0; i < CIN; ++i) gd[i * npx] = gxv[i];
-    }
-    // phase B: W0 (hid x CIN), b0
-    float *s_gh = s_mem, *s_x = s_mem + kHeadT * ph;
-#pragma unroll
-    for (int j = 0; j < 64; ++j)
-        if (j < hid) s_gh[t * ph + j] = h[j];
-#pragma unroll
-    for (int i = 0; i < CIN; ++i) s_x[t * (CIN + 1) + i] = xv[i];
-    __syncthreads();
-    for (int e = t; e < hid * CIN + hid; e += kHeadT) {
-        float a = 0.f;
-        if (e < hid * CIN) {
-            const int j = e / CIN, i = e - j * CIN;
-            for (int r = 0; r < kHeadT; ++r) a = fmaf(s_gh[r * ph + j], s_x[r * (CIN + 1) + i], a);
-        } else {
-            for (int r = 0; r < kHeadT; ++r) a += s_gh[r * ph + (e - hid * CIN)];
-        }
-        row[e] = a;
+    for (int k = 0; k < 3; ++k) {
+        float v = db1[k];
+        for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
+        if (lane == 0) atomicAdd(&Gp[g.b1 + k], v);
     }
 }
 
@@ -957,10 +1134,10 @@ size_t align256(size_t v) { return (v + 255) / 256 * 256; }
 struct Plan {
     Geo g;
     ArmTiles at;
-    int B, nblk_arm, nblk_head;
+    int B, nblk_arm;
     // workspace offsets (bytes)
     size_t yq, dq, gq, kf, stacks, stacks_bytes, dense, z[kMaxSp + 1], graw, gbuf[2], gdense, gstack, tmpU, tmpG, G,
-        part_arm, part_head, acc4, total;
+        acc4, total;
     int64_t gstack_off[CCMI_MAX_GRIDS]; // per level k (1..L-2) inside gstack, elements per frame
     int64_t gstack_per, stack_per, tmp_per;
 };
@@ -1052,7 +1229,6 @@ int make_plan(const ccmi_train_args *a, Plan &pl)
     at.start[L] = tiles;
     pl.nblk_arm = tiles;
     const int64_t npx = (int64_t)g.H * g.W;
-    pl.nblk_head = (int)((npx + kHeadT - 1) / kHeadT);
 
     // buffers
     const size_t B = (size_t)pl.B;
@@ -1090,8 +1266,6 @@ int make_plan(const ccmi_train_args *a, Plan &pl)
     pl.tmpU = take(4 * B * tmax);
     pl.tmpG = take(4 * B * tmax);
     pl.G = take(4 * B * ((size_t)g.N + g.P));
-    pl.part_arm = take(4 * B * (size_t)pl.nblk_arm * g.P_arm);
-    pl.part_head = take(4 * B * (size_t)pl.nblk_head * g.P_head);
     pl.acc4 = take(4 * B * 4);
     pl.total = o;
     return CCMI_OK;
@@ -1099,41 +1273,44 @@ int make_plan(const ccmi_train_args *a, Plan &pl)
 
 template <int D>
 int launch_arm_d(int nh, dim3 grid, hipStream_t s, const float *yq, const Geo &g, const ArmTiles &at, const float *th,
-                 int64_t ps, float lam_px, float *gq, float *part, int nblk, float *acc4)
+                 int64_t ps, float lam_px, float *gq, float *gth, int64_t gstride, float *acc4)
 {
     switch (nh) {
-    case 0: hipLaunchKernelGGL((t_arm<D, 0>), grid, dim3(kT), 0, s, yq, g, at, th, ps, lam_px, gq, part, nblk, acc4); break;
-    case 1: hipLaunchKernelGGL((t_arm<D, 1>), grid, dim3(kT), 0, s, yq, g, at, th, ps, lam_px, gq, part, nblk, acc4); break;
-    case 2: hipLaunchKernelGGL((t_arm<D, 2>), grid, dim3(kT), 0, s, yq, g, at, th, ps, lam_px, gq, part, nblk, acc4); break;
-    default: hipLaunchKernelGGL((t_arm<D, 3>), grid, dim3(kT), 0, s, yq, g, at, th, ps, lam_px, gq, part, nblk, acc4); break;
+    case 0: hipLaunchKernelGGL((t_arm<D, 0>), grid, dim3(kT), 0, s, yq, g, at, th, ps, lam_px, gq, gth, gstride, acc4); break;
+    case 1: hipLaunchKernelGGL((t_arm<D, 1>), grid, dim3(kT), 0, s, yq, g, at, th, ps, lam_px, gq, gth, gstride, acc4); break;
+    case 2: hipLaunchKernelGGL((t_arm<D, 2>), grid, dim3(kT), 0, s, yq, g, at, th, ps, lam_px, gq, gth, gstride, acc4); break;
+    default: hipLaunchKernelGGL((t_arm<D, 3>), grid, dim3(kT), 0, s, yq, g, at, th, ps, lam_px, gq, gth, gstride, acc4); break;
     }
     return CCMI_OK;
 }
 
 template <int CIN>
 void launch_head(bool bwd, dim3 grid, hipStream_t s, const float *dense, const float *gz0, const Geo &g, const float *th,
-                 int64_t ps, float *z0_or_gdense, float *part, int nblk)
+                 int64_t ps, float *z0_or_gdense, float *gth, int64_t gstride)
 {
-    if (!bwd) {
-        hipLaunchKernelGGL((t_head_fwd<CIN>), grid, dim3(kT), 0, s, dense, g, th, ps, z0_or_gdense);
-    } else {
-        const size_t lds = sizeof(float) * kHeadT * ((g.hid + 1) + std::max(4, CIN + 1));
-        hipLaunchKernelGGL((t_head_bwd<CIN>), grid, dim3(kHeadT), lds, s, dense, gz0, g, th, ps, z0_or_gdense, part,
-                           nblk);
+    if (!bwd) hipLaunchKernelGGL((t_head_fwd<CIN>), grid, dim3(kT), 0, s, dense, g, th, ps, z0_or_gdense);
+    else {
+        const size_t lds = sizeof(float) * (kHeadT / 64) * 64 * ((g.hid | 1) + 9);
+        switch ((g.hid + 15) / 16) {
+        case 1: hipLaunchKernelGGL((t_head_bwd<CIN, 1>), grid, dim3(kHeadT), lds, s, dense, gz0, g, th, ps, z0_or_gdense, gth, gstride); break;
+        case 2: hipLaunchKernelGGL((t_head_bwd<CIN, 2>), grid, dim3(kHeadT), lds, s, dense, gz0, g, th, ps, z0_or_gdense, gth, gstride); break;
+        case 3: hipLaunchKernelGGL((t_head_bwd<CIN, 3>), grid, dim3(kHeadT), lds, s, dense, gz0, g, th, ps, z0_or_gdense, gth, gstride); break;
+        default: hipLaunchKernelGGL((t_head_bwd<CIN, 4>), grid, dim3(kHeadT), lds, s, dense, gz0, g, th, ps, z0_or_gdense, gth, gstride); break;
+        }
     }
 }
 
 void head_dispatch(int cin, bool bwd, dim3 grid, hipStream_t s, const float *dense, const float *gz0, const Geo &g,
-                   const float *th, int64_t ps, float *o, float *part, int nblk)
+                   const float *th, int64_t ps, float *o, float *gth, int64_t gstride)
 {
     switch (cin) {
-    case 2: launch_head<2>(bwd, grid, s, dense, gz0, g, th, ps, o, part, nblk); break;
-    case 3: launch_head<3>(bwd, grid, s, dense, gz0, g, th, ps, o, part, nblk); break;
-    case 4: launch_head<4>(bwd, grid, s, dense, gz0, g, th, ps, o, part, nblk); break;
-    case 5: launch_head<5>(bwd, grid, s, dense, gz0, g, th, ps, o, part, nblk); break;
-    case 6: launch_head<6>(bwd, grid, s, dense, gz0, g, th, ps, o, part, nblk); break;
-    case 7: launch_head<7>(bwd, grid, s, dense, gz0, g, th, ps, o, part, nblk); break;
-    default: launch_head<8>(bwd, grid, s, dense, gz0, g, th, ps, o, part, nblk); break;
+    case 2: launch_head<2>(bwd, grid, s, dense, gz0, g, th, ps, o, gth, gstride); break;
+    case 3: launch_head<3>(bwd, grid, s, dense, gz0, g, th, ps, o, gth, gstride); break;
+    case 4: launch_head<4>(bwd, grid, s, dense, gz0, g, th, ps, o, gth, gstride); break;
+    case 5: launch_head<5>(bwd, grid, s, dense, gz0, g, th, ps, o, gth, gstride); break;
+    case 6: launch_head<6>(bwd, grid, s, dense, gz0, g, th, ps, o, gth, gstride); break;
+    case 7: launch_head<7>(bwd, grid, s, dense, gz0, g, th, ps, o, gth, gstride); break;
+    default: launch_head<8>(bwd, grid, s, dense, gz0, g, th, ps, o, gth, gstride); break;
     }
 }
 
@@ -1199,17 +1376,15 @@ extern "C" int ccmi_train_step(const ccmi_train_args *a, void *stream)
     hipLaunchKernelGGL(t_quant, grid1(g.N, B), dim3(kT), 0, s, a->latent, a->latent_stride, g.N, a->gain, a->quantizer,
                        a->noise, a->temperature, a->noise_param, (uint64_t)a->seed, a->step, a->noise_in, yq, dq, gq);
     {
-        dim3 grid(pl.nblk_arm, B);
-        float *part = F(pl.part_arm);
+        // persistent over the latent tiles: about one resident wave of workgroups for the batch
+        dim3 grid((unsigned)std::max(1, std::min(pl.nblk_arm, 2048 / B)), B);
         switch (g.d) {
-        case 8: launch_arm_d<8>(g.nh, grid, s, yq, g, pl.at, a->params, a->param_stride, lam_px, gq, part, pl.nblk_arm, acc4); break;
-        case 16: launch_arm_d<16>(g.nh, grid, s, yq, g, pl.at, a->params, a->param_stride, lam_px, gq, part, pl.nblk_arm, acc4); break;
-        case 24: launch_arm_d<24>(g.nh, grid, s, yq, g, pl.at, a->params, a->param_stride, lam_px, gq, part, pl.nblk_arm, acc4); break;
-        default: launch_arm_d<32>(g.nh, grid, s, yq, g, pl.at, a->params, a->param_stride, lam_px, gq, part, pl.nblk_arm, acc4); break;
+        case 8: launch_arm_d<8>(g.nh, grid, s, yq, g, pl.at, a->params, a->param_stride, lam_px, gq, Gth, GS, acc4); break;
+        case 16: launch_arm_d<16>(g.nh, grid, s, yq, g, pl.at, a->params, a->param_stride, lam_px, gq, Gth, GS, acc4); break;
+        case 24: launch_arm_d<24>(g.nh, grid, s, yq, g, pl.at, a->params, a->param_stride, lam_px, gq, Gth, GS, acc4); break;
+        default: launch_arm_d<32>(g.nh, grid, s, yq, g, pl.at, a->params, a->param_stride, lam_px, gq, Gth, GS, acc4); break;
         }
         CCMI_HIP_CHECK(hipGetLastError());
-        hipLaunchKernelGGL(t_colsum, dim3(ccmi_div_up(g.P_arm, 64), ccmi_div_up(pl.nblk_arm, 256), B), dim3(64, 4), 0, s,
-                           part, pl.nblk_arm, g.P_arm, Gth, GS);
     }
     {
         ccmi_ups_args u{};
@@ -1245,20 +1420,18 @@ extern "C" int ccmi_train_step(const ccmi_train_args *a, void *stream)
     // ---- synthesis backward
     float *gcur = graw;
     for (int i = g.n_sp - 1; i >= 0; --i) {
-        if (g.sp_relu[i])
-            hipLaunchKernelGGL(t_sp_gpre, grid1(3 * npx * B, 1), dim3(kT), 0, s, gcur, F(pl.z[i + 1]), 3 * npx * B);
         float *gin = F(pl.gbuf[i & 1]);
-        const int nb = (int)std::min<int64_t>((npx + kT - 1) / kT, 1024);
-        hipLaunchKernelGGL(t_sp_bwd, dim3(nb, B), dim3(kT), 0, s, gcur, F(pl.z[i]), g, a->params, a->param_stride,
-                           g.sp_w[i], g.sp_b[i], g.sp_res[i], gin, Gth, GS);
+        const int ntile = ccmi_div_up(g.W, kSX) * ccmi_div_up(g.H, kSY);
+        const unsigned nb = (unsigned)std::max(1, std::min(ntile, 1024 / B));
+        hipLaunchKernelGGL(t_sp_bwd, dim3(nb, B), dim3(kT), 0, s, gcur, g.sp_relu[i] ? F(pl.z[i + 1]) : nullptr, F(pl.z[i]),
+                           g, a->params, a->param_stride, g.sp_w[i], g.sp_b[i], g.sp_res[i], gin, Gth, GS);
         gcur = gin;
     }
     {
-        float *part = F(pl.part_head);
-        head_dispatch(g.L, true, dim3(pl.nblk_head, B), s, dense, gcur, g, a->params, a->param_stride, gd, part,
-                      pl.nblk_head);
-        hipLaunchKernelGGL(t_colsum, dim3(ccmi_div_up(g.P_head, 64), ccmi_div_up(pl.nblk_head, 256), B), dim3(64, 4), 0,
-                           s, part, pl.nblk_head, g.P_head, Gth + g.syn_off, GS);
+        // grid-stride over pixel chunks: about one resident wave of workgroups for the batch
+        const int64_t nchunk = (npx + kHeadT - 1) / kHeadT;
+        const unsigned nb = (unsigned)std::max<int64_t>(1, std::min<int64_t>(nchunk, 1024 / B));
+        head_dispatch(g.L, true, dim3(nb, B), s, dense, gcur, g, a->params, a->param_stride, gd, Gth, GS);
     }
 
     // ---- upsampling backward, finest level first (step L-2 .. 0)
