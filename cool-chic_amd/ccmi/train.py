@@ -279,10 +279,14 @@ def run_phase(of: Overfitter, ph: Phase, lmbda: float, scale: float = 1.0) -> to
     """train() (enc/training/train.py:86-374) for every frame of the batch at once: Adam
     restarted, cosine learning rate stepped every freq_valid iterations, linear soft-round
     temperature / noise schedules, validation every freq_valid iterations keeping each
-    frame's best parameters (restored at the end of the phase).  Patience-based early
-    stopping is not applied (the batch runs max_itr).  Returns the best validation [B, 4]."""
+    frame's best parameters (restored at the end of the phase).  A validation is a new
+    record when its loss is lower AND it gains more than 0.001 dB or loses less than
+    0.001 bpp (train.py:280-289).  Patience-based early stopping is not applied: the batch
+    runs max_itr and keeps each frame's best record, which can only be at least as good as
+    the record the reference stops at.  Returns the best validation [B, 4]."""
     n = max(1, int(ph.max_itr * scale))
     freq = max(1, int(ph.freq_valid * scale)) if scale < 1 else ph.freq_valid
+    npx = of.arch.sizes[0][0] * of.arch.sizes[0][1]
     of.reset_optimizer()
     best = of.validate(lmbda)
     best_lat, best_prm = of.latents.clone(), of.params.clone()
@@ -294,7 +298,9 @@ def run_phase(of: Overfitter, ph: Phase, lmbda: float, scale: float = 1.0) -> to
         of.step(ph.quantizer_type, ph.quantizer_noise_type, T, nz, lmbda, lr=lr, update=upd)
         if (cnt + 1) % freq == 0 or cnt + 1 == n:
             cur = of.validate(lmbda)
-            better = cur[:, 0] < best[:, 0]
+            d_psnr = 10 * torch.log10(best[:, 1].clamp_min(1e-10) / cur[:, 1].clamp_min(1e-10))
+            d_bpp = (cur[:, 2] - best[:, 2]) / npx
+            better = (cur[:, 0] < best[:, 0]) & ((d_bpp < 1e-3) | (d_psnr > 1e-3))
             if bool(better.any()):
                 best = torch.where(better[:, None], cur, best)
                 best_lat = torch.where(better[:, None], of.latents, best_lat)

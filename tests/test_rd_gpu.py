@@ -1,0 +1,100 @@
+"""Matched rate-distortion: the GPU encoder against the reference encoder on the same images,
+preset, architecture and lambdas (BASELINE configs 1 and 4).
+
+Reference points: tests/golden/rd_reference_*.json, written by tools/gen_golden_rd.py, which
+ran the reference's own warmup() / train() / quantize_model() / test() on CPU here:
+  * kodim15_192x128 -- the image of the reference's sanity check (test/sanity_check.py:13);
+  * kodim01_crop512 -- config 1: results/image/kodak/bitstreams/kodim01-lmbda-00001.cool
+    decoded bit-exactly and cropped to [0, 512) x [0, 512);
+hop decoder (cfg/dec/hop.cfg), lambdas 0.02 / 0.004 / 0.001 / 0.0004, 2 seeds each.
+
+The encoder is stochastic (random initialisation, quantisation noise): neither side can
+reproduce the other's random draws, so the bar is statistical.  Per lambda the GPU mean over
+2 seeds must lie within the reference's own seed-to-seed spread widened by a fixed margin, and
+the BD-rate of the GPU curve against the reference curve (ccmi.rd.bd_rate, the restatement of
+bjontegaard_metric.py:48-90) must stay inside the BD_WORSE / BD_BETTER band.  Records are written to
+gpurun_out/rd_gpu_<preset>.json for the bench / DESIGN.md tables.
+"""
+import json
+import os
+from pathlib import Path
+
+import numpy as np
+import pytest
+import torch
+
+GOLDEN = Path(__file__).resolve().parent / "golden"
+ROOT = Path(__file__).resolve().parents[1]
+HOP = ((48, 1, False, True), (3, 1, False, False), (3, 3, True, True), (3, 3, True, False))
+LAMBDAS = (0.02, 0.004, 0.001, 0.0004)
+PSNR_MARGIN_DB = 0.5   # on top of the reference's own seed-to-seed spread at that lambda
+RATE_MARGIN = 0.15     # relative, on top of the reference's spread
+# BD-rate band (percent, GPU curve against the reference curve, seed means): the GPU encoder
+# may not need more than BD_WORSE % more bits at equal PSNR; a much lower rate would point at
+# a rate-accounting bug, hence the lower bound.  Only on the 512 x 512 crop: the 192 x 128
+# image's 120-iteration curves are too noisy for a cubic fit (the reference's own seed 1
+# against its seed 0 gives -66.6 % there, -0.45 % on the crop).
+BD_WORSE, BD_BETTER = 10.0, 25.0
+
+pytestmark = pytest.mark.gpu
+
+
+def _targets():
+    from ccmi import decode, io
+    img, bd = io.read_png(GOLDEN / "192x128_kodim15.png")
+    assert bd == 8
+    out, = decode.decode_batch([(GOLDEN / "cool" / "kodim01-lmbda-00001.cool").read_bytes()], as_yuv=False)
+    k01, bd = io.parse_ppm(out)
+    assert bd == 8
+    return {"kodim15_192x128": img.float(), "kodim01_crop512": k01[:, :512, :512].float().contiguous()}
+
+
+def _ref(preset_file):
+    d = json.loads((GOLDEN / preset_file).read_text())
+    return d["runs"]
+
+
+def _check(image, ours, ref, bd_band):
+    from ccmi import rd
+    lines = []
+    for lm in LAMBDAS:
+        r = [x for x in ref if x["image"] == image and x["lmbda"] == lm]
+        o = [x for x in ours if x.lmbda == lm]
+        rp, rr = [x["psnr_db"] for x in r], [x["rate_bpp"] for x in r]
+        op, orr = np.mean([x.psnr_db for x in o]), np.mean([x.rate_bpp for x in o])
+        tol_p = PSNR_MARGIN_DB + (max(rp) - min(rp))
+        tol_r = RATE_MARGIN + (max(rr) - min(rr)) / np.mean(rr)
+        lines.append(f"{image} lambda {lm}: PSNR ref {np.mean(rp):.3f} gpu {op:.3f} (tol {tol_p:.2f}), "
+                     f"rate ref {np.mean(rr):.4f} gpu {orr:.4f} (tol {tol_r:.2f})")
+        assert abs(op - np.mean(rp)) <= tol_p, lines[-1]
+        assert abs(orr / np.mean(rr) - 1) <= tol_r, lines[-1]
+    R1, P1, _ = rd.curve([x for x in ref if x["image"] == image])
+    R2, P2, _ = rd.curve(ours)
+    bd = rd.bd_rate(R1, P1, R2, P2)
+    lines.append(f"{image}: BD-rate GPU vs reference {bd:+.2f} %")
+    print("\n" + "\n".join(lines))
+    if bd_band:
+        assert -BD_BETTER <= bd <= BD_WORSE, lines[-1]
+    return bd
+
+
+@pytest.mark.parametrize("image", ["kodim15_192x128", "kodim01_crop512"])
+def test_debug_preset_matches_reference_rd(image, gpu):
+    from ccmi import io, rd, train
+    x = _targets()[image]
+    H, W = x.shape[-2:]
+    arch = train.Arch(H, W, dim_arm=16, n_hidden=2, layers=HOP)
+    tgt = io.to_target(x, "rgb").to(gpu)
+    recs = rd.encode_points(tgt, H, W, LAMBDAS, arch, yuv420=False, seeds=(0, 1), preset="debug", name=image,
+                            write=True)
+    out = ROOT / "gpurun_out"
+    out.mkdir(exist_ok=True)
+    f = out / "rd_gpu_debug.json"
+    prev = json.loads(f.read_text()) if f.exists() else {}
+    prev[image] = [r.as_dict() for r in recs]
+    f.write_text(json.dumps(prev, indent=1))
+    bd = _check(image, recs, _ref("rd_reference_debug.json"), bd_band=image == "kodim01_crop512")
+    # the written .cool streams: what the bitstream really costs next to the estimate
+    for r in recs:
+        assert r.cool_bpp == r.cool_bpp and r.cool_bpp > 0
+    assert np.isfinite(bd)

@@ -28,7 +28,7 @@ per module) for one trained model, to pin ccmi.quantize.quantize_model; and the 
 calibration of oracle/train_oracle.py against the reference's own training iteration
 (BASELINE.md §3.3).
 
-Usage: python tools/gen_golden_rd.py [debug|c3x|quant|calib|all]
+Usage: python tools/gen_golden_rd.py [debug|c3x|quant|calib|bd|all]
 """
 
 from __future__ import annotations
@@ -283,8 +283,33 @@ def gen_calib(out_path: Path):
     out_path.write_text(json.dumps(res, indent=1))
 
 
+def gen_bd(out_path: Path):
+    """Golden vectors for the BD-rate restatement: the reference's own BD_RATE / BD_PSNR
+    (coolchic/utils/bjontegaard_metric.py) on seeded curve pairs, both integration modes."""
+    sys.path.insert(0, str(REF / "coolchic" / "utils"))
+    import bjontegaard_metric as bj
+    g = np.random.default_rng(0)
+    cases = []
+    for k in range(6):
+        n = 4 + k % 3
+        r1 = np.sort(g.uniform(0.05, 2.0, n))
+        p1 = 30 + 6 * np.log(r1) + g.normal(0, 0.1, n)
+        r2 = r1 * g.uniform(0.8, 1.25) * np.exp(g.normal(0, 0.03, n))
+        p2 = 30 + 6 * np.log(r1) + g.normal(0, 0.2, n) + g.uniform(-0.5, 0.5)
+        case = {"R1": r1.tolist(), "PSNR1": p1.tolist(), "R2": r2.tolist(), "PSNR2": p2.tolist()}
+        for pw in (0, 1):
+            case[f"bd_rate_pw{pw}"] = float(bj.BD_RATE(r1, p1, r2, p2, piecewise=pw))
+            case[f"bd_psnr_pw{pw}"] = float(bj.BD_PSNR(r1, p1, r2, p2, piecewise=pw))
+        cases.append(case)
+    out_path.write_text(json.dumps({"source": "coolchic/utils/bjontegaard_metric.py (reference tree)", "cases": cases},
+                                   indent=1))
+    print("bd fixtures:", len(cases))
+
+
 if __name__ == "__main__":
     what = sys.argv[1] if len(sys.argv) > 1 else "all"
+    if what in ("bd", "all"):
+        gen_bd(GOLD / "bd_reference.json")
     if what in ("debug", "all"):
         run_rd("debug", GOLD / "rd_reference_debug.json")
     if what in ("quant", "all"):
