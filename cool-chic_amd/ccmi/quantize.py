@@ -95,6 +95,9 @@ class QuantizedModel:
     expgol: dict = field(default_factory=dict)   # module -> (weight count, bias count)
     nn_bits: dict = field(default_factory=dict)  # module -> Exp-Golomb bits of its weights + biases
     loss: float = 0.0
+    # module -> [(q_w, q_b, loss)] for every candidate tried, in the reference's order; the loss
+    # omits the terms that are the same for every candidate of that module (module docstring)
+    table: dict = field(default_factory=dict)
 
 
 def _full_kernels(arch: Arch, blocks: torch.Tensor, lay: Layout) -> torch.Tensor:
@@ -248,6 +251,7 @@ def quantize_model(arch: Arch, latent: torch.Tensor, params: torch.Tensor, targe
         res.expgol[module] = counts[k]
         res.nn_bits[module] = float(nn_rate[k])
         res.loss = float(loss[k])
+        res.table[module] = [(c[2], c[3], float(v)) for c, v in zip(cands, loss)]
     res.params = cur
     return res
 

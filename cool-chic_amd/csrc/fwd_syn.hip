@@ -19,6 +19,7 @@
 //
 // Any other architecture runs the generic per-layer kernel (one launch per layer,
 // ping-pong through the caller's workspace).
+#include <stdlib.h>
 #include <type_traits>
 
 #include "fwd_common.h"
@@ -75,6 +76,32 @@ __device__ __forceinline__ void store_out(const FusedArgs &A, float *out, int64_
     } else if (!(gy & 1) && !(gx & 1) && (gy >> 1) < (A.H >> 1) && (gx >> 1) < (A.W >> 1)) {
         const int64_t cp = (int64_t)(A.H >> 1) * (A.W >> 1);
         out[plane + (m - 1) * cp + (int64_t)(gy >> 1) * (A.W >> 1) + (gx >> 1)] = q;
+    }
+}
+
+// ---- split-f16 MFMA head (first 1x1 layer) ---------------------------------------------
+// v_mfma_f32_32x32x16_f16 (2.5 PF dense) with every f32 operand split as hi = f16(v),
+// lo = f16(v - hi): W X ~= Wh Xh + Wh Xl + Wl Xh, the dropped Wl Xl and the rounding of the lo
+// parts leave ~2^-22 of sum |w x| (tools/mfma_f16_probe.hip: 4.7e-7 worst on 8-term dots),
+// accumulation in f32.  Operands need |v| < 65504 (f16 range).
+// Lane maps (probe-checked): A[m = l & 31][k = 8 (l >> 5) + j], B[k = 8 (l >> 5) + j][n = l & 31],
+// accumulator register r of lane l = D[m = (r & 3) + 8 (r >> 2) + 4 (l >> 5)][n = l & 31].
+// K = 16 is [Xh | Xl] (half 0 | half 1 of the wave), the input's 8 slots being c_in channels,
+// a constant 1 (the bias column) and zeros.  Hidden tiles of 32 units take two MFMAs
+// (A = [Wh | Wh], then [Wl | 0]); a tile of <= 16 units takes one, its rows 0..15 carrying
+// [Wh | Wh] and rows 16..31 [Wl | 0] of the same units, summed afterwards (registers r, r + 8).
+typedef _Float16 h8 __attribute__((ext_vector_type(8)));
+typedef float f16x __attribute__((ext_vector_type(16)));
+typedef unsigned u4v __attribute__((ext_vector_type(4)));
+
+__device__ __forceinline__ f16x mfma32(h8 a, h8 b, f16x c) { return __builtin_amdgcn_mfma_f32_32x32x16_f16(a, b, c, 0, 0, 0); }
+
+__device__ __forceinline__ void split8(const float (&v)[8], h8 &hi, h8 &lo)
+{
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+        hi[j] = (_Float16)v[j];
+        lo[j] = (_Float16)(v[j] - (float)hi[j]);
     }
 }
 
@@ -188,7 +215,11 @@ __global__ __launch_bounds__(kFThreads) void syn_fused_kernel(FusedArgs A, Level
                 const int jj = rem / kSW, ii = rem - jj * kSW;
                 sv[u] = 0.f;
                 if (i < NSI && jj < nj && ii < ni)
+#if defined(CCMI_DIAG_NOLOAD) // diagnostic build only: phase A without its global loads
+                    sv[u] = 0.001f * (float)(jj + ii);
+#else
                     sv[u] = src[ch * splane + (int64_t)clampi(jbase + jj, U.hs - 1) * U.ws + clampi(ibase + ii, U.ws - 1)];
+#endif
             }
             const float *rs = U.ref_src + (int64_t)b * U.ref_stride;
             constexpr int NTI = kHrRows * kTW, NTU = (NTI + kFThreads - 1) / kFThreads;
@@ -200,7 +231,11 @@ __global__ __launch_bounds__(kFThreads) void syn_fused_kernel(FusedArgs A, Level
                 const int Y = Ya - 3 + yr, X = Xa - 3 + xt;
                 tv[u] = 0.f;
                 if (i < NTI && yr < nr && xt < nt && Y >= 0 && Y < U.hd && X >= 0 && X < U.wd)
+#if defined(CCMI_DIAG_NOLOAD)
+                    tv[u] = 0.001f * (float)(yr + xt);
+#else
                     tv[u] = rs[(int64_t)Y * U.wd + X];
+#endif
             }
 #pragma unroll
             for (int u = 0; u < NSU; ++u) {
@@ -351,7 +386,111 @@ __global__ __launch_bounds__(kFThreads) void syn_fused_kernel(FusedArgs A, Level
         // the raw tiles (region 0) are overwritten by the head output below
         if constexpr (UPS) __syncthreads();
         FSTAMP(2);
-        if (A.n_head == 2) {
+        if (A.n_head == 2 && A.head_mfma) {
+            // ---- split-f16 MFMA first layer, second layer on VALU from the accumulators
+            const int hid = A.hid, lane = threadIdx.x & 63, hh = lane >> 5, m32 = lane & 31;
+            const bool t1_full = hid > 16, t2 = hid > 32, t2_full = hid > 48;
+            __syncthreads(); // s_head staged
+            // A operands of this lane (row m32 of each hidden tile)
+            h8 a1h, a1l, a2h, a2l;
+            {
+                auto wrow = [&](int u, float (&v)[8]) {
+#pragma unroll
+                    for (int j = 0; j < 8; ++j) v[j] = (u < hid && j <= CIN) ? s_head[u][j] : 0.f;
+                };
+                float v[8];
+                h8 hi, lo, z = {};
+                // tile 1: units 0..31 (full) or 0..15 (packed: rows >= 16 hold the lo parts)
+                wrow(t1_full ? m32 : (m32 & 15), v);
+                split8(v, hi, lo);
+                a1h = (t1_full || m32 < 16) ? hi : (hh == 0 ? lo : z);
+                a1l = hh == 0 ? lo : z;
+                wrow(t2_full ? 32 + m32 : 32 + (m32 & 15), v);
+                split8(v, hi, lo);
+                a2h = (t2_full || m32 < 16) ? hi : (hh == 0 ? lo : z);
+                a2l = hh == 0 ? lo : z;
+            }
+            // second-layer weights of the units this lane's accumulator registers hold
+            const float4 *w1v = reinterpret_cast<const float4 *>(&s_head[0][0]);
+            auto wl2 = [&](int u) -> float4 { // w1[0..CMID)[u]
+                const float *r = s_head[u];
+                return float4{r[CIN + 1], CMID > 1 ? r[CIN + 2] : 0.f, CMID > 2 ? r[CIN + 3] : 0.f,
+                              CMID > 3 ? r[CIN + 4] : 0.f};
+            };
+            (void)w1v;
+            const float lo0 = A.relu0 ? 0.f : -INFINITY;
+#pragma unroll
+            for (int p = 0; p < NR; ++p) {
+                // this lane's pixel (column c, row p): [x | 1 | 0] split, then both 32-pixel
+                // operands by one lane-half swap per dword
+                float xv[8];
+#pragma unroll
+                for (int j = 0; j < 8; ++j) xv[j] = j < CIN ? x[p][j] : (j == CIN ? 1.f : 0.f);
+                h8 xh, xl;
+                split8(xv, xh, xl);
+                const u4v uh = __builtin_bit_cast(u4v, xh), ul = __builtin_bit_cast(u4v, xl);
+                u4v b0u, b1u;
+#pragma unroll
+                for (int d = 0; d < 4; ++d) {
+                    const auto r = __builtin_amdgcn_permlane32_swap(uh[d], ul[d], false, false);
+                    b0u[d] = r[0]; // columns 0..31: [Xh | Xl]
+                    b1u[d] = r[1]; // columns 32..63
+                }
+                float po[2][CMID];
+#pragma unroll
+                for (int n = 0; n < 2; ++n) {
+                    const h8 bn = __builtin_bit_cast(h8, n ? b1u : b0u);
+                    f16x acc1 = {}, acc2 = {};
+                    acc1 = mfma32(a1h, bn, acc1);
+                    if (t1_full) acc1 = mfma32(a1l, bn, acc1);
+                    if (t2) {
+                        acc2 = mfma32(a2h, bn, acc2);
+                        if (t2_full) acc2 = mfma32(a2l, bn, acc2);
+                    }
+#pragma unroll
+                    for (int m = 0; m < CMID; ++m) po[n][m] = 0.f;
+                    // tile 1
+#pragma unroll
+                    for (int r = 0; r < 16; ++r) {
+                        const int u0 = (r & 3) + 8 * (r >> 2) + 4 * hh;
+                        float hv;
+                        int u;
+                        if (t1_full) { hv = acc1[r]; u = u0; }
+                        else { if (r >= 8) break; hv = acc1[r] + acc1[r + 8]; u = u0; }
+                        hv = fmaxf(hv, lo0);
+                        const float4 w = wl2(u);
+                        po[n][0] = fmaf(w.x, hv, po[n][0]);
+                        if (CMID > 1) po[n][1] = fmaf(w.y, hv, po[n][1]);
+                        if (CMID > 2) po[n][2] = fmaf(w.z, hv, po[n][2]);
+                        if (CMID > 3) po[n][3] = fmaf(w.w, hv, po[n][3]);
+                    }
+                    if (t2) {
+#pragma unroll
+                        for (int r = 0; r < 16; ++r) {
+                            const int u0 = 32 + (r & 3) + 8 * (r >> 2) + 4 * hh;
+                            float hv;
+                            if (t2_full) hv = acc2[r];
+                            else { if (r >= 8) break; hv = acc2[r] + acc2[r + 8]; }
+                            hv = fmaxf(hv, lo0);
+                            const float4 w = wl2(u0);
+                            po[n][0] = fmaf(w.x, hv, po[n][0]);
+                            if (CMID > 1) po[n][1] = fmaf(w.y, hv, po[n][1]);
+                            if (CMID > 2) po[n][2] = fmaf(w.z, hv, po[n][2]);
+                            if (CMID > 3) po[n][3] = fmaf(w.w, hv, po[n][3]);
+                        }
+                    }
+                }
+                // the two halves of the wave hold complementary units of the same pixels:
+                // one swap brings both partial sums of this lane's own column together
+                const float lo1 = A.relu1 ? 0.f : -INFINITY;
+#pragma unroll
+                for (int m = 0; m < CMID; ++m) {
+                    const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(po[0][m]), __float_as_uint(po[1][m]),
+                                                                     false, false);
+                    o[p][m] = fmaxf(__uint_as_float(r[0]) + __uint_as_float(r[1]) + b1[m], lo1);
+                }
+            }
+        } else if (A.n_head == 2) {
             const int hid = A.hid;
             // fmaxf(acc, lo0) is the optional ReLU without a per-element select
             const f2 lo0 = f2(A.relu0 ? 0.f : -INFINITY);
@@ -628,6 +767,11 @@ bool make_plan(const ccmi_syn_args *a, Plan *P)
         f.w1_off = w_off[1];
         f.b1_off = b_off[1];
         f.relu1 = L[1].relu;
+        // split-f16 MFMA first layer (c_in + bias in one 8-wide K slice, <= 64 hidden units):
+        // parity-green but measured slower than the VALU head in this latency-bound kernel
+        // (DESIGN.md section 5), so opt-in
+        static const bool mfma_head = getenv("CCMI_SYN_MFMA_HEAD") != nullptr;
+        f.head_mfma = mfma_head && a->c_in + 1 <= 8 && hid <= 64 && cmid <= 4;
     }
     f.n_sp = n_sp;
     for (int s = 0; s < n_sp; ++s) {

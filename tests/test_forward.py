@@ -12,7 +12,11 @@ Tolerances (fp32 everywhere; summation order differs from PyTorch's conv/linear)
                p = F(q+.5) - F(q-.5) (two CDF values near 0 or 1, one ulp of 1.0 each, over
                p ln 2) plus first-order propagation of the measured mu / scale differences
                (d rate / d mu <= 1 / (scale ln 2)); and |sum err| <= 1e-5 * sum.
-  decoded 8-bit image: PSNR difference <= 1e-5 dB (north_star bar).
+  decoded 8-bit image: PSNR difference <= 1e-5 dB (north_star bar); every 8-bit value that
+               differs from the reference's is a rounding tie of the reference's float output
+               (|255 x - k - 1/2| within 255 x the float tolerance).
+  realistic-target PSNR (720p, 1080p): the float synthesis output against the reference's
+               output plus N(0, 0.01) noise (a ~40 dB operating point): PSNR within 1e-5 dB.
 """
 
 import numpy as np
@@ -108,9 +112,23 @@ def test_hip_forward_matches_reference_golden(path, gpu, ccmi_lib):
     np.testing.assert_allclose(s[0].cpu().numpy(), z["syn"], rtol=0, atol=_tol(z["syn"]))
     dec = F.post_forward(s, 8, False)[0].cpu().numpy()
     assert np.mean(dec != z["dec"]) < 1e-3
+    _ties_only(dec, z["syn"], _tol(z["syn"]))
     d420 = F.split_420(F.post_forward(s, 8, True)[0], mp.H, mp.W)
     for k in "yuv":
         assert np.mean(d420[k].cpu().numpy() != z[f"dec420_{k}"]) < 1e-3
+
+
+def _ties_only(dec, ref_raw, tol, qmax=255.0):
+    """Every 8-bit value of `dec` that differs from round(ref_raw) is a rounding tie of the
+    reference's float output: |qmax x - k - 1/2| <= qmax * tol (k = floor(qmax x))."""
+    ref = np.clip(np.round(ref_raw * qmax) / qmax, 0, 1)
+    bad = dec != ref
+    if not bad.any():
+        return 0
+    v = ref_raw[bad].astype(np.float64) * qmax
+    dist = np.abs(v - np.floor(v) - 0.5)
+    assert np.all(dist <= qmax * tol), (int(bad.sum()), float(dist.max()), qmax * tol)
+    return int(bad.sum())
 
 
 def _psnr(x, t):
@@ -127,6 +145,29 @@ def test_hip_psnr_within_1e5_db(gpu, ccmi_lib):
     dec = F.post_forward(s, 8, False)[0].cpu().numpy()
     target = np.random.default_rng(0).random(dec.shape)
     assert abs(_psnr(dec, target) - _psnr(z["dec"], target)) <= 1e-5
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("H,W,seed", [(720, 1280, 21), (1080, 1920, 22)])
+def test_fused_psnr_realistic_target(H, W, seed, gpu, ccmi_lib):
+    """north_star bar at a realistic operating point: the fused kernel's float synthesis output
+    and the oracle's, each scored against the oracle's output plus N(0, 0.01) noise (~40 dB),
+    agree within 1e-5 dB; the 8-bit frames differ only on rounding ties."""
+    mp = fo.ModelParams.random(H, W, seed=seed)
+    g = torch.Generator().manual_seed(seed)
+    lat = [0.5 * torch.randn(h, w, generator=g) for h, w in mp.sizes]
+    ref = fo.forward(mp, lat)["syn"].numpy()
+    raw = _fused([mp], [lat], gpu, 0, False)[0].cpu().numpy()
+    target = np.clip(ref + np.random.default_rng(seed).normal(0, 0.01, ref.shape), 0, 1)
+    clip = lambda a: np.clip(a, 0, 1)  # noqa: E731
+    p_ref, p_gpu = _psnr(clip(ref), target), _psnr(clip(raw), target)
+    print(f"\n{H}x{W}: PSNR oracle {p_ref:.6f} dB, HIP {p_gpu:.6f} dB, diff {p_gpu - p_ref:.2e} dB, "
+          f"max |err| {np.abs(raw - ref).max():.2e}")
+    assert 30 < p_ref < 60  # the noise sets ~40 dB; clipping at [0, 1] removes part of it
+    assert abs(p_gpu - p_ref) <= 1e-5
+    dec = _fused([mp], [lat], gpu, 8, False)[0].cpu().numpy()
+    n = _ties_only(dec, ref, _tol(ref))
+    print(f"8-bit values off the oracle's: {n} of {dec.size}, all rounding ties")
 
 
 @pytest.mark.gpu
@@ -209,6 +250,7 @@ def test_fused_decode_matches_reference_golden(path, gpu, ccmi_lib):
     np.testing.assert_allclose(raw[0].cpu().numpy(), z["syn"], rtol=0, atol=_tol(z["syn"]))
     dec = _fused([mp], [_lat(z, mp)], gpu, 8, False)[0].cpu().numpy()
     assert np.mean(dec != z["dec"]) < 1e-3
+    _ties_only(dec, z["syn"], _tol(z["syn"]))
     d420 = F.split_420(_fused([mp], [_lat(z, mp)], gpu, 8, True)[0], mp.H, mp.W)
     for k in "yuv":
         assert np.mean(d420[k].cpu().numpy() != z[f"dec420_{k}"]) < 1e-3
@@ -235,6 +277,7 @@ def test_fused_decode_matches_oracle_random(H, W, seed, layers, gpu, ccmi_lib):
         post = fo.post(ref["syn"], 8)
         dec = _fused([mp], [lat], gpu, 8, False)[0].cpu().numpy()
         assert np.mean(dec != post.numpy()) < 1e-3
+        _ties_only(dec, ref["syn"].numpy(), _tol(ref["syn"].numpy()))
 
 
 @pytest.mark.gpu

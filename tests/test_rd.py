@@ -36,7 +36,7 @@ def test_bd_rate_identities():
 def test_reference_rd_fixtures_are_complete():
     d = json.loads((GOLDEN / "rd_reference_debug.json").read_text())
     keys = {(r["image"], r["lmbda"], r["seed"]) for r in d["runs"]}
-    for img in ("kodim15_192x128", "kodim01_crop512"):
+    for img in ("kodim15_192x128", "kodim01_768x512", "kodim01_crop512"):
         for lm in (0.02, 0.004, 0.001, 0.0004):
             for s in (0, 1):
                 assert (img, lm, s) in keys

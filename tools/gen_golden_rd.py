@@ -13,9 +13,11 @@ Content
   kodim15_192x128 : test/data/192x128_kodim15.png, the image of the reference's own
                     sanity check (test/sanity_check.py:13), committed as
                     tests/golden/192x128_kodim15.png;
-  kodim01_crop512 : SURVEY §8d config 1: results/image/kodak/bitstreams/
-                    kodim01-lmbda-00001.cool decoded bit-exactly (the C oracle, md5 = the
-                    reference decoder) and cropped to rows/cols [0, 512).
+  kodim01_768x512 : results/image/kodak/bitstreams/kodim01-lmbda-00001.cool decoded
+                    bit-exactly (the C oracle, md5 = the reference decoder): Kodak geometry
+                    (BASELINE config 4's content; the reference's 40.5 dB reconstruction
+                    stands in for the original, which is not in the tree);
+  kodim01_crop512 : SURVEY §8d config 1: the same, cropped to rows/cols [0, 512).
 
 Schedules: the `debug` preset (preset_cfg/debug.yaml) at 4 lambdas and 2 seeds (the
 seed-to-seed spread of the reference itself sets the test tolerance), and the c3x preset
@@ -82,7 +84,7 @@ def load_targets() -> dict:
     out = {}
     x, bd = cio.read_png(GOLD / "192x128_kodim15.png")
     assert bd == 8
-    out["kodim15_192x128"] = x.float()
+    out["kodim15_192x128"] = x[0].float()  # [3, 128, 192]
     oracle = ROOT / "oracle" / "_build" / "ccdec_oracle"
     if not oracle.exists():
         subprocess.run(["make", "-s", "-C", str(ROOT / "oracle")], check=True)
@@ -92,7 +94,9 @@ def load_targets() -> dict:
                        stdout=subprocess.DEVNULL)
         k, bd = cio.read_ppm(ppm)
     assert bd == 8
-    out["kodim01_crop512"] = k[:, :512, :512].float().contiguous()
+    k = k[0].float()  # [3, 512, 768]
+    out["kodim01_768x512"] = k.contiguous()                      # Kodak geometry (config 4 content)
+    out["kodim01_crop512"] = k[:, :512, :512].contiguous()
     return out
 
 
@@ -162,6 +166,8 @@ def run_rd(kind: str, out_path: Path):
     seeds = SEEDS if kind == "debug" else [0]
     cfg = preset("debug") if kind == "debug" else preset("c3x", C3X_SCALE)
     for name, x in targets.items():
+        if kind != "debug" and name != "kodim15_192x128":
+            continue  # c3x on CPU: the small image only by default (~17 min per point at Kodak size)
         for lm in LAMBDAS:
             for s in seeds:
                 key = (name, kind if kind == "debug" else f"c3x_x{C3X_SCALE}", lm, s)
@@ -209,27 +215,30 @@ def gen_quant():
         QM.loss_function = rec.orig
     chosen = fe.coolchic_encoder.get_network_quantization_step()
     counts = fe.coolchic_encoder.nn_expgol_cnt
-    table = []
-    for qs, loss in rec.rows:
-        table.append((qs, loss))
-    # the module being searched is the one whose step changes within its block of rows
+    # rows arrive module by module in sorted order (quantizemodel.py:181); a module's block
+    # ends after its last (q_w, q_b) pair in itertools.product order, and candidates with
+    # |q| > 65535 are skipped: split the rows where the searched module's own step pair
+    # (the one that changes from row to row) returns to its first value
     mods = sorted(chosen.keys())
-    rows_by_mod, i = {}, 0
-    n_per = {m: sum(1 for _ in QM.itertools.product(QM.POSSIBLE_Q_STEP[m]["weight"], QM.POSSIBLE_Q_STEP[m]["bias"]))
-             for m in mods}
-    for qs, loss in table:
-        # rows arrive module by module in sorted order; skipped candidates (|q| > 65535) are absent
-        while i < len(mods) and len(rows_by_mod.get(mods[i], [])) >= n_per[mods[i]]:
-            i += 1
-        m = mods[i]
-        cur = qs[m]
-        rows_by_mod.setdefault(m, []).append((float(cur["weight"]), float(cur["bias"]), loss))
+    rows_by_mod, cur = {m: [] for m in mods}, 0
+    for qs, loss in rec.rows:
+        while True:
+            m = mods[cur]
+            q = (float(qs[m]["weight"]), float(qs[m]["bias"]))
+            prev = rows_by_mod[m][-1][:2] if rows_by_mod[m] else None
+            last = (float(QM.POSSIBLE_Q_STEP[m]["weight"][-1]), float(QM.POSSIBLE_Q_STEP[m]["bias"][-1]))
+            if prev is not None and prev == last:
+                cur += 1  # the previous module's block is complete
+                continue
+            rows_by_mod[m].append((q[0], q[1], loss))
+            break
     for m in mods:
-        arr = np.array(rows_by_mod.get(m, []), dtype=np.float64).reshape(-1, 3)
+        arr = np.array(rows_by_mod[m], dtype=np.float64).reshape(-1, 3)
         z[f"table/{m}"] = arr
         z[f"chosen/{m}"] = np.array([chosen[m]["weight"], chosen[m]["bias"]], dtype=np.float64)
         z[f"expgol/{m}"] = np.array([counts[m]["weight"], counts[m]["bias"]], dtype=np.int64)
-    z["meta"] = repr({"H": int(x.shape[1]), "W": int(x.shape[2]), "lmbda": 1e-3, "arch": "hop",
+    z["meta"] = repr({"H": int(x.shape[1]), "W": int(x.shape[2]), "lmbda": 1e-3, "arch": "hop", "dim_arm": 16,
+                      "n_hidden_arm": 2, "n_grids": 7, "layers": "|".join(HOP["layers"]), "encoder_gain": 16,
                       "frame_data_type": "rgb", "bitdepth": 8})
     np.savez_compressed(GOLD / "quantize_ref_kodim15_hop.npz", **z)
     print("quantize fixture:", {m: z[f"chosen/{m}"].tolist() for m in mods})

@@ -11,7 +11,8 @@ For each case, tests/golden/train_<name>.npz holds
            ``g/<name>``: the gradient of every parameter after loss.backward(),
            ``s1/<name>`` / ``s2/<name>``: the parameters after one and two optimisation
            steps exactly as enc/training/train.py:238-262 runs them
-           (clip_grad_norm_(1e-1) then torch.optim.Adam(lr)).
+           (clip_grad_norm_(1e-1) then torch.optim.Adam(lr)); ``g1/<name>``: the gradient
+           at the step-1 parameters (before the second step's clipping).
 The quantisation noise is zero (gaussian of std 0 / "none"; the reference draws it from torch's RNG, which a
 GPU kernel cannot reproduce); noise paths are checked against the CPU oracle with a
 shared noise tensor instead.
@@ -39,6 +40,9 @@ CASES = [
     ("mop_ste_29x37", 29, 37, 16, 2, G.MOP, 6, "ste", 1e-4, 1e-2, True),
     ("arm8_sra_20x31", 20, 31, 8, 1, ["8-1-linear-relu", "3-1-linear-none", "3-3-residual-none"], 5,
      "softround_alone", 0.2, 4e-3, False),
+    # a realistic size: every pyramid level has interior pixels, the 3x3 layers' adjoint and
+    # the workgroup-level reductions see many tiles
+    ("hop_sr_128x192", 128, 192, 16, 2, G.HOP, 7, "softround", 0.3, 1e-3, True),
 ]
 
 
@@ -57,7 +61,10 @@ def forward_loss(enc, target, qtype, temp, lmbda, yuv420):
 
 
 def main():
+    only = sys.argv[1:]  # case names to (re)generate; default: the ones without a file yet
     for name, h, w, d, nh, layers, ng, qtype, temp, lmbda, yuv420 in CASES:
+        if (only and name not in only) or (not only and (ROOT / "tests" / "golden" / f"train_{name}.npz").exists()):
+            continue
         enc = G.build(h, w, d, nh, layers, ng, seed=zlib.crc32(name.encode()) % 1000)
         with torch.no_grad():  # keep most of the output inside [0, 1] so the clamp passes gradients
             n_syn = len(layers)
@@ -99,6 +106,9 @@ def main():
                 p.grad = None
             out, _ = forward_loss(enc, target, qtype, temp, lmbda, yuv420)
             out.loss.backward()
+            if s == 2:  # the gradient at the parameters after one step (before clipping)
+                for k, v in named:
+                    z[f"g1/{k}"] = (v.grad if v.grad is not None else torch.zeros_like(v)).numpy().copy()
             clip_grad_norm_(params, 1e-1, norm_type=2.0, error_if_nonfinite=False)
             opt.step()
             for k, v in named:
