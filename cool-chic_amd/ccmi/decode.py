@@ -5,7 +5,38 @@ from __future__ import annotations
 import ctypes as C
 from typing import Sequence
 
-from . import CcmiError, check, lib
+from . import MAX_GRIDS, MAX_SYN_LAYERS, CcmiError, SynLayer, check, lib
+
+
+class UpsI32Args(C.Structure):
+    _fields_ = [("latent", C.c_void_p), ("n_grids", C.c_int), ("h", C.c_int * MAX_GRIDS), ("w", C.c_int * MAX_GRIDS),
+                ("kernels", C.c_void_p), ("ups_k", C.c_int), ("n_ups", C.c_int), ("pre_k", C.c_int), ("n_pre", C.c_int),
+                ("out", C.c_void_p), ("workspace", C.c_void_p), ("workspace_bytes", C.c_size_t)]
+
+
+class SynI32Args(C.Structure):
+    _fields_ = [("in_", C.c_void_p), ("c_in", C.c_int), ("h", C.c_int), ("w", C.c_int), ("n_layers", C.c_int),
+                ("layers", SynLayer * MAX_SYN_LAYERS), ("params", C.c_void_p), ("out", C.c_void_p),
+                ("workspace", C.c_void_p), ("workspace_bytes", C.c_size_t)]
+
+
+def _bind():
+    L = lib()
+    if not getattr(L, "_ccmi_dec_bound", False):
+        L.ccmi_decode_weights_i32.argtypes = [C.c_void_p, C.c_size_t, C.c_void_p, C.c_size_t, C.c_void_p, C.c_size_t,
+                                              C.c_void_p, C.c_size_t, C.c_void_p]
+        L.ccmi_ups_workspace_bytes_i32.argtypes = [C.c_int, C.c_void_p, C.c_void_p]
+        L.ccmi_ups_workspace_bytes_i32.restype = C.c_size_t
+        L.ccmi_ups_forward_i32.argtypes = [C.POINTER(UpsI32Args), C.c_void_p]
+        L.ccmi_syn_workspace_bytes_i32.argtypes = [C.POINTER(SynI32Args)]
+        L.ccmi_syn_workspace_bytes_i32.restype = C.c_size_t
+        L.ccmi_syn_forward_i32.argtypes = [C.POINTER(SynI32Args), C.c_void_p]
+        L.ccmi_decode_batch_workspace_bytes.argtypes = [C.c_void_p, C.c_void_p, C.c_int, C.c_int, C.c_int, C.c_int,
+                                                        C.c_void_p]
+        L.ccmi_decode_batch_ws.argtypes = [C.c_void_p, C.c_void_p, C.c_int, C.c_void_p, C.c_void_p, C.c_void_p, C.c_int,
+                                           C.c_int, C.c_int, C.c_void_p, C.c_size_t, C.c_void_p]
+        L._ccmi_dec_bound = True
+    return L
 
 
 def decode_file(inp: str, out: str = "", output_bitdepth: int = 0, output_chroma_format: int = 0,
@@ -24,9 +55,11 @@ def output_size(stream: bytes, output_bitdepth: int = 0, output_chroma_format: i
 
 
 def decode_batch(streams: Sequence[bytes], output_bitdepth: int = 0, output_chroma_format: int = 0,
-                 as_yuv: bool = True, stream_handle: int | None = None) -> list[bytes]:
+                 as_yuv: bool = True, stream_handle: int | None = None, workspace=None) -> list[bytes]:
     """Decode independent intra .cool streams in one batched launch sequence; returns the
-    bytes the reference decoder would write for each (YUV planes, or PPM)."""
+    bytes the reference decoder would write for each (YUV planes, or PPM).  workspace: an
+    optional caller-owned device buffer (a uint8 torch tensor of at least
+    decode_batch_workspace_bytes(...) bytes): ccmi_decode_batch_ws, no allocation inside."""
     n = len(streams)
     bufs = [C.create_string_buffer(s, len(s)) for s in streams]
     sizes = [output_size(s, output_bitdepth, output_chroma_format, as_yuv) for s in streams]
@@ -39,9 +72,83 @@ def decode_batch(streams: Sequence[bytes], output_bitdepth: int = 0, output_chro
     if stream_handle is None:
         import torch
         stream_handle = torch.cuda.current_stream().cuda_stream if torch.cuda.is_available() else None
-    check(lib().ccmi_decode_batch(sp, ln, n, op, cap, got, output_bitdepth, output_chroma_format, int(as_yuv),
-                                  stream_handle))
+    if workspace is None:
+        check(lib().ccmi_decode_batch(sp, ln, n, op, cap, got, output_bitdepth, output_chroma_format, int(as_yuv),
+                                      stream_handle))
+    else:
+        check(_bind().ccmi_decode_batch_ws(sp, ln, n, op, cap, got, output_bitdepth, output_chroma_format,
+                                           int(as_yuv), workspace.data_ptr(), workspace.numel(), stream_handle))
     return [o.raw[: got[i]] for i, o in enumerate(outs)]
+
+
+def decode_batch_workspace_bytes(streams: Sequence[bytes], output_bitdepth: int = 0, output_chroma_format: int = 0,
+                                 as_yuv: bool = True) -> int:
+    n = len(streams)
+    bufs = [C.create_string_buffer(s, len(s)) for s in streams]
+    sp = (C.c_void_p * n)(*[C.cast(b, C.c_void_p) for b in bufs])
+    ln = (C.c_size_t * n)(*[len(s) for s in streams])
+    out = C.c_size_t(0)
+    check(_bind().ccmi_decode_batch_workspace_bytes(sp, ln, n, output_bitdepth, output_chroma_format, int(as_yuv),
+                                                    C.byref(out)))
+    return out.value
+
+
+def weights_i32(stream: bytes):
+    """(arm, ups, syn) fixed-point network integers of a stream's intra frame, as the
+    decoder uses them (ccmi_decode_weights_i32; cc-frame-decoder.cpp:201-353)."""
+    import numpy as np
+    L = _bind()
+    buf = C.create_string_buffer(stream, len(stream))
+    cnt = (C.c_size_t * 3)()
+    check(L.ccmi_decode_weights_i32(C.cast(buf, C.c_void_p), len(stream), None, 0, None, 0, None, 0, cnt))
+    arr = [np.zeros(max(int(c), 1), dtype=np.int32) for c in cnt]
+    check(L.ccmi_decode_weights_i32(C.cast(buf, C.c_void_p), len(stream), arr[0].ctypes.data, arr[0].size,
+                                    arr[1].ctypes.data, arr[1].size, arr[2].ctypes.data, arr[2].size, cnt))
+    return tuple(a[: int(c)] for a, c in zip(arr, cnt))
+
+
+def ups_forward_i32(latent, sizes, kernels, ups_k: int, n_ups: int, pre_k: int, n_pre: int):
+    """Integer upsampling on the GPU (ccmi_ups_forward_i32): latent int32 [N] (value << 8,
+    grids flat in order), kernels int32 (weights_i32()[1]) -> int32 [L, H, W]."""
+    import torch
+    from . import require_cuda
+    require_cuda(latent, kernels)
+    L = _bind()
+    n = len(sizes)
+    h = (C.c_int * MAX_GRIDS)(*[s[0] for s in sizes])
+    w = (C.c_int * MAX_GRIDS)(*[s[1] for s in sizes])
+    if latent.dtype != torch.int32 or latent.numel() < sum(a * b for a, b in sizes):
+        raise ValueError("latent: int32 with sum(h * w) elements expected")
+    out = torch.empty(n, sizes[0][0], sizes[0][1], dtype=torch.int32, device=latent.device)
+    nws = L.ccmi_ups_workspace_bytes_i32(n, h, w)
+    ws = torch.empty(max(nws, 4), dtype=torch.uint8, device=latent.device)
+    a = UpsI32Args(latent=latent.data_ptr(), n_grids=n, h=h, w=w, kernels=kernels.contiguous().data_ptr(), ups_k=ups_k,
+                   n_ups=n_ups, pre_k=pre_k, n_pre=n_pre, out=out.data_ptr(), workspace=ws.data_ptr(), workspace_bytes=nws)
+    check(L.ccmi_ups_forward_i32(C.byref(a), torch.cuda.current_stream(latent.device).cuda_stream))
+    return out
+
+
+def syn_forward_i32(x, layers, params):
+    """Integer synthesis of one branch on the GPU (ccmi_syn_forward_i32): x int32 [C, H, W]
+    at precision 12, layers [(n_out, ks, residual, relu)], params int32 -> int32 [n_out, H, W]."""
+    import torch
+    from . import require_cuda
+    require_cuda(x, params)
+    L = _bind()
+    c, hh, ww = x.shape
+    arr = (SynLayer * MAX_SYN_LAYERS)()
+    for i, (n_out, ks, res, relu) in enumerate(layers):
+        arr[i] = SynLayer(int(n_out), int(ks), int(res), int(relu))
+    out = torch.empty(layers[-1][0], hh, ww, dtype=torch.int32, device=x.device)
+    a = SynI32Args(in_=x.contiguous().data_ptr(), c_in=c, h=hh, w=ww, n_layers=len(layers), layers=arr,
+                   params=params.contiguous().data_ptr(), out=out.data_ptr(), workspace=None, workspace_bytes=0)
+    nws = L.ccmi_syn_workspace_bytes_i32(C.byref(a))
+    ws = None
+    if nws:
+        ws = torch.empty(nws, dtype=torch.uint8, device=x.device)
+        a.workspace, a.workspace_bytes = ws.data_ptr(), nws
+    check(L.ccmi_syn_forward_i32(C.byref(a), torch.cuda.current_stream(x.device).cuda_stream))
+    return out
 
 
 def decode_latents(stream: bytes, stream_handle: int | None = None) -> list:
@@ -74,4 +181,5 @@ def last_timing() -> dict:
     return dict(zip(("upload", "arm_cabac", "ups_syn_out", "download"), list(ms)))
 
 
-__all__ = ["last_timing", "decode_latents", "decode_file", "decode_batch", "output_size", "CcmiError"]
+__all__ = ["last_timing", "decode_latents", "decode_file", "decode_batch", "decode_batch_workspace_bytes", "output_size",
+           "weights_i32", "ups_forward_i32", "syn_forward_i32", "CcmiError"]

@@ -283,9 +283,11 @@ struct EventSet {
     }
 };
 
+// ws / ws_bytes: caller-owned device workspace (NULL: one hipMalloc per call); need: when
+// not NULL, only the workspace size is computed (streams parsed, nothing launched).
 int decode_many(const uint8_t *const *streams, const size_t *lens, int n, uint8_t *const *outs, const size_t *caps,
                 size_t *sizes, int out_bitdepth, int out_chroma, int as_yuv, hipStream_t s,
-                int32_t *const *lat_out = nullptr)
+                int32_t *const *lat_out = nullptr, void *ws = nullptr, size_t ws_bytes = 0, size_t *need = nullptr)
 {
     if (n < 1) return ccmi_set_error(CCMI_ERR_ARG, "decode: no streams");
     std::vector<FrameHost> fr(n);
@@ -373,12 +375,22 @@ int decode_many(const uint8_t *const *streams, const size_t *lens, int n, uint8_
         memcpy(&host[p.syn_off], f.syn.data(), f.syn.size() * 4);
     }
 
-    uint8_t *dev = nullptr;
-    CCMI_HIP_CHECK(hipMalloc(&dev, tot));
+    if (need) {
+        *need = tot;
+        return CCMI_OK;
+    }
+    uint8_t *dev = static_cast<uint8_t *>(ws);
+    if (dev) {
+        if (ws_bytes < tot) return ccmi_set_error(CCMI_ERR_ARG, "decode: workspace of %zu bytes, need %zu", ws_bytes, tot);
+        if (reinterpret_cast<uintptr_t>(dev) % 256)
+            return ccmi_set_error(CCMI_ERR_ARG, "decode: workspace must be 256-byte aligned");
+    } else {
+        CCMI_HIP_CHECK(hipMalloc(&dev, tot));
+    }
     struct Free {
         uint8_t *p;
         ~Free() { if (p) (void)hipFree(p); }
-    } guard{dev};
+    } guard{ws ? nullptr : dev};
     EventSet ev;
     ev.rec(0, s);
     CCMI_HIP_CHECK(hipMemcpyAsync(dev, host.data(), cst, hipMemcpyHostToDevice, s));
@@ -607,6 +619,24 @@ extern "C" int ccmi_decode_batch(const uint8_t *const *streams, const size_t *le
     if (!streams || !lens || !out || !out_caps) return ccmi_set_error(CCMI_ERR_ARG, "decode_batch: null argument");
     return decode_many(streams, lens, n, out, out_caps, out_sizes, out_bitdepth, out_chroma, as_yuv,
                        static_cast<hipStream_t>(stream));
+}
+
+extern "C" int ccmi_decode_batch_workspace_bytes(const uint8_t *const *streams, const size_t *lens, int n,
+                                                 int out_bitdepth, int out_chroma, int as_yuv, size_t *bytes)
+{
+    if (!streams || !lens || !bytes) return ccmi_set_error(CCMI_ERR_ARG, "decode_batch_workspace_bytes: null argument");
+    return decode_many(streams, lens, n, nullptr, nullptr, nullptr, out_bitdepth, out_chroma, as_yuv, nullptr, nullptr,
+                       nullptr, 0, bytes);
+}
+
+extern "C" int ccmi_decode_batch_ws(const uint8_t *const *streams, const size_t *lens, int n, uint8_t *const *out,
+                                    const size_t *out_caps, size_t *out_sizes, int out_bitdepth, int out_chroma,
+                                    int as_yuv, void *workspace, size_t workspace_bytes, void *stream)
+{
+    if (!streams || !lens || !out || !out_caps || !workspace)
+        return ccmi_set_error(CCMI_ERR_ARG, "decode_batch_ws: null argument");
+    return decode_many(streams, lens, n, out, out_caps, out_sizes, out_bitdepth, out_chroma, as_yuv,
+                       static_cast<hipStream_t>(stream), nullptr, workspace, workspace_bytes);
 }
 
 extern "C" int ccmi_decode_latents(const uint8_t *stream, size_t len, int32_t *out, size_t cap, void *hstream)

@@ -460,9 +460,9 @@ __global__ __launch_bounds__(kFThreads) void syn_fused_kernel(FusedArgs A, Level
                         hv = fmaxf(hv, lo0);
                         const float4 w = wl2(u);
                         po[n][0] = fmaf(w.x, hv, po[n][0]);
-                        if (CMID > 1) po[n][1] = fmaf(w.y, hv, po[n][1]);
-                        if (CMID > 2) po[n][2] = fmaf(w.z, hv, po[n][2]);
-                        if (CMID > 3) po[n][3] = fmaf(w.w, hv, po[n][3]);
+                        if constexpr (CMID > 1) po[n][1] = fmaf(w.y, hv, po[n][1]);
+                        if constexpr (CMID > 2) po[n][2] = fmaf(w.z, hv, po[n][2]);
+                        if constexpr (CMID > 3) po[n][3] = fmaf(w.w, hv, po[n][3]);
                     }
                     if (t2) {
 #pragma unroll
@@ -474,9 +474,9 @@ __global__ __launch_bounds__(kFThreads) void syn_fused_kernel(FusedArgs A, Level
                             hv = fmaxf(hv, lo0);
                             const float4 w = wl2(u0);
                             po[n][0] = fmaf(w.x, hv, po[n][0]);
-                            if (CMID > 1) po[n][1] = fmaf(w.y, hv, po[n][1]);
-                            if (CMID > 2) po[n][2] = fmaf(w.z, hv, po[n][2]);
-                            if (CMID > 3) po[n][3] = fmaf(w.w, hv, po[n][3]);
+                            if constexpr (CMID > 1) po[n][1] = fmaf(w.y, hv, po[n][1]);
+                            if constexpr (CMID > 2) po[n][2] = fmaf(w.z, hv, po[n][2]);
+                            if constexpr (CMID > 3) po[n][3] = fmaf(w.w, hv, po[n][3]);
                         }
                     }
                 }

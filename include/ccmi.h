@@ -214,6 +214,60 @@ int ccmi_decode_latents(const uint8_t *stream, size_t len, int32_t *out, size_t 
 int ccmi_row_reduce_f32(const float *a, int64_t a_stride, const float *t, int64_t t_stride, int64_t len, int batch,
                         int mode, double *out, void *stream);
 
+/* ccmi_decode_batch with a caller-owned device workspace (no allocation inside):
+ * ccmi_decode_batch_workspace_bytes() parses the streams and returns the size the same
+ * arguments need; the workspace must be 256-byte aligned. */
+int ccmi_decode_batch_workspace_bytes(const uint8_t *const *streams, const size_t *lens, int n,
+                                      int out_bitdepth, int out_chroma, int as_yuv, size_t *bytes);
+int ccmi_decode_batch_ws(const uint8_t *const *streams, const size_t *lens, int n,
+                         uint8_t *const *out, const size_t *out_caps, size_t *out_sizes,
+                         int out_bitdepth, int out_chroma, int as_yuv, void *workspace,
+                         size_t workspace_bytes, void *stream);
+
+/* Network weights of a stream's intra frame as the decoder's fixed-point integers
+ * (cc-frame-decoder.cpp:201-353, read_arm / read_ups / read_syn):
+ *   arm: per hidden layer W[d][d] (out, in) then b[d]; then W_out[2][d], b_out[2]
+ *        (ARM_PRECISION 8; the reference stores W transposed for its loop, :240-246);
+ *   ups: n_ups full kernels of ups_k taps, then n_pre of pre_k taps (UPS_PRECISION 12,
+ *        half kernels mirrored, decode_upsweights_qi :188-199);
+ *   syn: per branch, per layer W[n_out][n_in][k][k] then b[n_out] (SYN precision 12).
+ * counts[3] receives the three lengths; NULL buffers only query them. Host buffers. */
+int ccmi_decode_weights_i32(const uint8_t *stream, size_t len, int32_t *arm, size_t arm_cap,
+                            int32_t *ups, size_t ups_cap, int32_t *syn, size_t syn_cap, size_t *counts);
+
+/* Integer upsampling (run_ups, cc-frame-decoder.cpp:572-679; ups_refine_cpu.hpp:11-79,
+ * ups_upsample_cpu.hpp:12-91): latent grids (value << 8, flat in grid order) -> the
+ * [n_grids][h0][w0] synthesis input at precision 12.  Device pointers. */
+typedef struct ccmi_ups_i32_args {
+    const int32_t *latent;  /* sum_l h[l] w[l] int32, grid l after grids 0..l-1 */
+    int n_grids;
+    int h[CCMI_MAX_GRIDS_PUBLIC];
+    int w[CCMI_MAX_GRIDS_PUBLIC];
+    const int32_t *kernels; /* the ups array of ccmi_decode_weights_i32 */
+    int ups_k, n_ups, pre_k, n_pre;
+    int32_t *out;           /* n_grids * h[0] * w[0] int32 */
+    void *workspace;        /* ccmi_ups_workspace_bytes_i32() */
+    size_t workspace_bytes;
+} ccmi_ups_i32_args;
+size_t ccmi_ups_workspace_bytes_i32(int n_grids, const int *h, const int *w);
+int ccmi_ups_forward_i32(const ccmi_ups_i32_args *args, void *stream);
+
+/* Integer synthesis of one branch (run_syn_branch, cc-frame-decoder.cpp:773-1042;
+ * synfused_cpu.hpp:17-109, synlb_cpu.hpp:22-124, syn_cpu.hpp:21-112): [c_in][h][w] at
+ * precision 12 -> [n_out][h][w].  Device pointers. */
+typedef struct ccmi_syn_i32_args {
+    const int32_t *in;
+    int c_in, h, w;
+    int n_layers;
+    ccmi_syn_layer layers[CCMI_MAX_SYN_LAYERS];
+    const int32_t *params;  /* one branch of the syn array of ccmi_decode_weights_i32 */
+    int32_t *out;
+    void *workspace;        /* ccmi_syn_workspace_bytes_i32(); 0 bytes for fused architectures */
+    size_t workspace_bytes;
+} ccmi_syn_i32_args;
+size_t ccmi_syn_workspace_bytes_i32(const ccmi_syn_i32_args *args);
+int ccmi_syn_forward_i32(const ccmi_syn_i32_args *args, void *stream);
+
 /* Byte size of the decoded output of one stream (header parse only). */
 int ccmi_decode_output_size(const uint8_t *stream, size_t len, int out_bitdepth,
                             int out_chroma, int as_yuv, size_t *size);

@@ -10,9 +10,14 @@ import pytest
 GOLDEN = Path(__file__).resolve().parent / "golden"
 MD5 = json.loads((GOLDEN / "ref_md5.json").read_text())
 FILES = sorted((GOLDEN / "cool").glob("*.cool"))
+# CLIC20-pro-valid (BASELINE config 5 content): 5 geometries from 384 x 512 to 1725 x 1145
+# (portrait) at lambda 0.02, and one 1360 x 2048 stream at lambda 1e-4 (~1.1 bpp)
+CLIC = sorted((GOLDEN / "cool" / "clic").glob("*.cool"))
 
 
 def _key(f):
+    if f.parent.name == "clic":
+        return "clic20-pro-valid/" + f.name
     return ("kodak/" if f.name.startswith("kodim") else "jvet/") + f.name
 
 
@@ -27,6 +32,70 @@ def test_hip_decode_file_bit_exact(f, gpu, ccmi_lib, tmp_path):
     data = out.read_bytes()
     assert len(data) == e["bytes"]
     assert hashlib.md5(data).hexdigest() == e["md5"]
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("f", CLIC, ids=[f.stem[:40] for f in CLIC])
+def test_hip_decode_clic_bit_exact(f, gpu, ccmi_lib, tmp_path):
+    test_hip_decode_file_bit_exact(f, gpu, ccmi_lib, tmp_path)
+
+
+@pytest.mark.gpu
+def test_hip_decode_batch_caller_workspace(gpu, ccmi_lib):
+    """ccmi_decode_batch_ws: the caller sizes and owns the device workspace; same bytes."""
+    import torch
+    from ccmi import decode
+    for fs, yuv in (([f for f in FILES if f.name[:2] in ("E-", "D-")][:8], True), (CLIC, False)):  # CLIC: rgb -> PPM
+        data = [f.read_bytes() for f in fs]
+        nb = decode.decode_batch_workspace_bytes(data, as_yuv=yuv)
+        ws = torch.empty(nb, dtype=torch.uint8, device=gpu)
+        outs = decode.decode_batch(data, as_yuv=yuv, workspace=ws)
+        for f, o in zip(fs, outs):
+            assert hashlib.md5(o).hexdigest() == MD5[_key(f)]["md5"], f.name
+        with pytest.raises(decode.CcmiError):  # too small
+            decode.decode_batch(data, as_yuv=yuv, workspace=ws[: nb // 2])
+
+
+def _oracle_stages(oracle_c, data):
+    import ctypes as C
+    import numpy as np
+    from test_encode import _Frame
+    fr = _Frame()
+    buf = C.create_string_buffer(data, len(data))
+    assert oracle_c.cco_decode_frame_mem(buf, len(data), C.byref(fr)) == 0
+    try:
+        sizes = [(fr.lh[l], fr.lw[l]) for l in range(fr.n_layers)]
+        lat = np.concatenate([np.ctypeslib.as_array(fr.lat[l], shape=(h * w,)).copy() for l, (h, w) in enumerate(sizes)])
+        n = fr.n_layers * fr.h * fr.w
+        syn_in = np.ctypeslib.as_array(fr.syn_in, shape=(n,)).copy().reshape(fr.n_layers, fr.h, fr.w)
+        syn_out = np.ctypeslib.as_array(fr.syn_out, shape=(fr.n_out * fr.h * fr.w,)).copy().reshape(fr.n_out, fr.h, fr.w)
+        return sizes, lat, syn_in, syn_out
+    finally:
+        oracle_c.cco_frame_free(C.byref(fr))
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("name", ["D-BQSquare-lmbda-0001", "kodim01-lmbda-00001", "E-Johnny-lmbda-00004",
+                                  "clic/todd-quackenbush-222-lmbda-002"])
+def test_integer_stage_entry_points_match_oracle(name, gpu, ccmi_lib, oracle_c):
+    """ccmi_decode_weights_i32 -> ccmi_ups_forward_i32 -> ccmi_syn_forward_i32 on the
+    decoded latents reproduce the oracle's synthesis input and output planes bit for bit."""
+    import numpy as np
+    import torch
+    from ccmi import decode, encode
+    f = [g for g in FILES + CLIC if (g.parent.name + "/" + g.stem if g.parent.name == "clic" else g.stem).startswith(name)][0]
+    data = f.read_bytes()
+    sizes, lat, syn_in, syn_out = _oracle_stages(oracle_c, data)
+    arm, ups, syn = decode.weights_i32(data)
+    d = encode.parse(data).desc
+    got_in = decode.ups_forward_i32(torch.from_numpy(lat).to(gpu), sizes, torch.from_numpy(ups).to(gpu), d.ups_k,
+                                    d.n_ups, d.pre_k, d.n_pre)
+    assert np.array_equal(got_in.cpu().numpy(), syn_in)
+    layers = [(int(d.syn_out[i]), int(d.syn_ks[i]), int(d.syn_type[i]) // 16 == 1, int(d.syn_type[i]) % 16 == 1)
+              for i in range(d.n_syn_layers)]
+    if d.n_branches == 1:
+        got_out = decode.syn_forward_i32(torch.from_numpy(syn_in).to(gpu), layers, torch.from_numpy(syn).to(gpu))
+        assert np.array_equal(got_out.cpu().numpy(), syn_out)
 
 
 @pytest.mark.gpu

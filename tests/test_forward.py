@@ -259,6 +259,7 @@ def test_fused_decode_matches_reference_golden(path, gpu, ccmi_lib):
 @pytest.mark.gpu
 @pytest.mark.parametrize("H,W,seed,layers", [
     (720, 1280, 1, None), (1080, 1920, 11, None), (37, 53, 2, None), (1, 1, 3, None), (2, 130, 4, None), (129, 3, 5, None),
+    (1365, 2048, 12, None), (1725, 1145, 13, None),  # CLIC20-pro-valid geometries (config 5 content)
     (45, 70, 6, "3-1-linear-none|3-3-residual-relu"),
     (45, 70, 7, "16-1-linear-relu|3-1-linear-none"),
     (64, 96, 8, "16-1-linear-relu|4-1-linear-none|4-3-residual-relu|4-3-residual-none|4-3-linear-none"),
