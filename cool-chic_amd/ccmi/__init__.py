@@ -30,6 +30,7 @@ EXPORTED = [
     "ccmi_ups_workspace_bytes_i32", "ccmi_ups_forward_i32", "ccmi_syn_workspace_bytes_i32", "ccmi_syn_forward_i32",
     "ccmi_cool_parse", "ccmi_code_wb", "ccmi_decode_wb", "ccmi_code_latent_layer", "ccmi_arm_forward_i32",
     "ccmi_encode_frame", "ccmi_row_reduce_f32", "ccmi_train_param_count", "ccmi_train_workspace_bytes", "ccmi_train_step",
+    "ccmi_quantize_f32",
 ]
 
 

@@ -39,6 +39,8 @@ class TrainArgs(C.Structure):
         ("beta2", C.c_float), ("eps", C.c_float), ("clip", C.c_float), ("step", C.c_int), ("seed", C.c_uint64),
         ("noise_in", C.c_void_p), ("grad_out", C.c_void_p), ("loss_out", C.c_void_p), ("update", C.c_int),
         ("workspace", C.c_void_p), ("workspace_bytes", C.c_size_t),
+        ("forward_only", C.c_int), ("raw_out", C.c_void_p), ("rate_out", C.c_void_p), ("grad_raw", C.c_void_p),
+        ("grad_rate", C.c_void_p),
     ]
 
 

@@ -103,12 +103,40 @@ class CoolChicEncoder(nn.Module):
                 soft_round_temperature: Optional[Tensor] = torch.tensor(0.3),
                 noise_parameter: Optional[Tensor] = torch.tensor(1.0), AC_MAX_VAL: int = -1,
                 flag_additional_outputs: bool = False) -> Tuple[Tensor, Tensor, Dict[str, Any]]:
-        """Eval forward (coolchic.py:291-479): returns raw synthesis output [B, C, H, W],
-        rate [B, N] in bits and the optional per-grid detail dictionary."""
-        if self.training:
-            raise NotImplementedError("training-mode forward (noisy / soft quantisers, autograd) is not "
-                                      "implemented on the HIP path yet; call .eval() for decoding")
-        return forward_batch([self], AC_MAX_VAL=AC_MAX_VAL, flag_additional_outputs=flag_additional_outputs)
+        """coolchic.py:291-479: returns raw synthesis output [B, C, H, W], rate [B, N] in bits
+        and the optional per-grid detail dictionary.  Eval mode: hard-rounded latents, no
+        autograd (forward_batch).  Train mode: the reference's quantizer and noise
+        (quantizer_type / quantizer_noise_type / soft_round_temperature / noise_parameter),
+        differentiable w.r.t. every parameter; forward and backward both run in libccmi
+        (ccmi.autograd.TrainForward), the noise drawn with the reference's torch calls."""
+        if not self.training:
+            return forward_batch([self], AC_MAX_VAL=AC_MAX_VAL, flag_additional_outputs=flag_additional_outputs)
+        if AC_MAX_VAL != -1 or flag_additional_outputs:
+            raise NotImplementedError("AC_MAX_VAL / additional outputs are eval-mode (bitstream) features")
+        from ccmi import train as _T
+        from ccmi.autograd import TrainForward
+        from coolchic.enc.component.core.quantizer import draw_noise
+        flat = self.flat_latent()
+        if flat.device.type != "cuda":
+            raise ValueError("CoolChicEncoder.forward runs on the GPU: move the module with .to('cuda')")
+        # drawn whenever the reference draws it (quantizer.py:188-197), so the torch RNG stream
+        # advances as in the reference; only "none" / "softround" add it (:200-213)
+        noise = draw_noise(flat.detach() * self.encoder_gains, quantizer_noise_type, noise_parameter)
+        p = self.param
+        layers = tuple(self.synthesis.layer_desc)
+        arch = _T.Arch(p.img_size[0], p.img_size[1], dim_arm=p.dim_arm, n_hidden=p.n_hidden_layers_arm, layers=layers,
+                       n_grids=p.latent_n_grids, ups_k=p.ups_k_size, pre_k=p.ups_preconcat_k_size,
+                       gain=float(self.encoder_gains))
+        lin = [m for m in self.arm.mlp if hasattr(m, "weight")]
+        convs = [m for m in self.synthesis.layers if hasattr(m, "weight")]
+        params = _T.pack_params([(m.weight, m.bias) for m in lin],
+                                [m.parametrizations.weight.original for m in self.upsampling.conv_transpose2ds],
+                                [m.parametrizations.weight.original for m in self.upsampling.conv2ds],
+                                [(m.weight, m.bias) for m in convs])
+        t = float(soft_round_temperature) if soft_round_temperature is not None else 0.3
+        raw, rate = TrainForward.apply(flat, params[None].expand(flat.shape[0], -1),
+                                       {"arch": arch, "quantizer": quantizer_type, "temperature": t, "noise": noise})
+        return raw, rate, {}
 
     # ---------------------------------------------------------------- parameters
     def get_param(self) -> "OrderedDict[str, Tensor]":

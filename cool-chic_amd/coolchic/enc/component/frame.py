@@ -1,4 +1,4 @@
-"""FrameEncoder (reference: coolchic/enc/component/frame.py), intra frames, eval forward.
+"""FrameEncoder (reference: coolchic/enc/component/frame.py), intra frames.
 
 forward() = CoolChicEncoder.forward + the eval post-processing of frame.py:175-183
 (rounding to the output bitdepth, optional 444 -> 420 nearest, clamp), the latter in
@@ -45,7 +45,13 @@ class FrameEncoder(nn.Module):
 
     def post_process(self, raw: Tensor):
         if self.training:
-            raise NotImplementedError("training-mode frame forward")
+            # frame.py:175-183 in train mode: no rounding; 444 -> 420 nearest (even rows /
+            # columns, yuv.py:275-299); clamp to [0, 1] -- differentiable torch ops
+            if self.frame_data_type == "yuv420":  # F.interpolate(scale 0.5, nearest): floor(H / 2) rows
+                h2, w2 = 2 * (raw.shape[-2] // 2), 2 * (raw.shape[-1] // 2)
+                return {"y": raw[:, 0:1].clamp(0.0, 1.0), "u": raw[:, 1:2, 0:h2:2, 0:w2:2].clamp(0.0, 1.0),
+                        "v": raw[:, 2:3, 0:h2:2, 0:w2:2].clamp(0.0, 1.0)}
+            return raw.clamp(0.0, 1.0)
         H, W = raw.shape[-2:]
         if self.frame_data_type == "yuv420":
             out = _F.post_forward(raw, self.bitdepth, True)

@@ -142,8 +142,8 @@ __global__ void t_quant(const float *__restrict__ lat, int64_t ls, int N, float 
     default: y = rintf(x); d = 0.f; break; // hardround: torch.round has a zero gradient
     }
     yq[wi] = y;
-    dq[wi] = gain * d;
-    gq[wi] = 0.f;
+    if (dq) dq[wi] = gain * d;
+    if (gq) gq[wi] = 0.f;
 }
 
 // ------------------------------------------------------------------ ARM forward + backward
@@ -238,7 +238,8 @@ __device__ __forceinline__ void wave_add(float v, float *dst)
 template <int D, int NH>
 __global__ __launch_bounds__(kT) void t_arm(const float *__restrict__ yq, Geo g, ArmTiles at, const float *__restrict__ th,
                                             int64_t ps, float lam_px, float *__restrict__ gq,
-                                            float *__restrict__ gth, int64_t gstride, float *__restrict__ acc4)
+                                            float *__restrict__ gth, int64_t gstride, float *__restrict__ acc4,
+                                            const float *__restrict__ grad_rate, float *__restrict__ rate_out)
 {
     constexpr int NT = (D + 15) / 16, MT = (D + 15) / 16;
     __shared__ float s_y[kALH][kALW];
@@ -323,9 +324,13 @@ __global__ __launch_bounds__(kT) void t_arm(const float *__restrict__ yq, Geo g,
         const float Pr = F1 - F2;
         float g_q = 0.f, g_mu = 0.f, g_ls = 0.f;
         if (valid) {
-            rsum += -log2f(fmaxf(Pr, 1.52587890625e-05f));
+            const float rbits = -log2f(fmaxf(Pr, 1.52587890625e-05f));
+            rsum += rbits;
+            const int64_t li = (int64_t)b * g.N + g.off[l] + (int64_t)(y0 + cy) * W + (x0 + cx);
+            if (rate_out) rate_out[li] = rbits;
+            const float lam = grad_rate ? grad_rate[li] : lam_px;
             if (Pr >= 1.52587890625e-05f) { // clamp_min passes the gradient where P >= 2^-16
-                const float dLdP = -lam_px / (Pr * kLn2);
+                const float dLdP = -lam / (Pr * kLn2);
                 const float e1 = expf(-fabsf(s1) / sig), e2 = expf(-fabsf(s2) / sig);
                 // torch autograd of 0.5 - 0.5 sign(s) expm1(-|s|/sig): d/ds = 0.5 sign(s)^2 e / sig
                 const float Fs1 = 0.5f * sg1 * sg1 * e1 / sig, Fs2 = 0.5f * sg2 * sg2 * e2 / sig;
@@ -1273,13 +1278,14 @@ int make_plan(const ccmi_train_args *a, Plan &pl)
 
 template <int D>
 int launch_arm_d(int nh, dim3 grid, hipStream_t s, const float *yq, const Geo &g, const ArmTiles &at, const float *th,
-                 int64_t ps, float lam_px, float *gq, float *gth, int64_t gstride, float *acc4)
+                 int64_t ps, float lam_px, float *gq, float *gth, int64_t gstride, float *acc4, const float *grate,
+                 float *rate_out)
 {
     switch (nh) {
-    case 0: hipLaunchKernelGGL((t_arm<D, 0>), grid, dim3(kT), 0, s, yq, g, at, th, ps, lam_px, gq, gth, gstride, acc4); break;
-    case 1: hipLaunchKernelGGL((t_arm<D, 1>), grid, dim3(kT), 0, s, yq, g, at, th, ps, lam_px, gq, gth, gstride, acc4); break;
-    case 2: hipLaunchKernelGGL((t_arm<D, 2>), grid, dim3(kT), 0, s, yq, g, at, th, ps, lam_px, gq, gth, gstride, acc4); break;
-    default: hipLaunchKernelGGL((t_arm<D, 3>), grid, dim3(kT), 0, s, yq, g, at, th, ps, lam_px, gq, gth, gstride, acc4); break;
+    case 0: hipLaunchKernelGGL((t_arm<D, 0>), grid, dim3(kT), 0, s, yq, g, at, th, ps, lam_px, gq, gth, gstride, acc4, grate, rate_out); break;
+    case 1: hipLaunchKernelGGL((t_arm<D, 1>), grid, dim3(kT), 0, s, yq, g, at, th, ps, lam_px, gq, gth, gstride, acc4, grate, rate_out); break;
+    case 2: hipLaunchKernelGGL((t_arm<D, 2>), grid, dim3(kT), 0, s, yq, g, at, th, ps, lam_px, gq, gth, gstride, acc4, grate, rate_out); break;
+    default: hipLaunchKernelGGL((t_arm<D, 3>), grid, dim3(kT), 0, s, yq, g, at, th, ps, lam_px, gq, gth, gstride, acc4, grate, rate_out); break;
     }
     return CCMI_OK;
 }
@@ -1320,6 +1326,23 @@ dim3 grid1(int64_t n, int B) { return dim3((unsigned)((n + kT - 1) / kT), (unsig
 unsigned red_blocks(int64_t n) { return (unsigned)std::max<int64_t>(1, std::min<int64_t>((n + kT - 1) / kT, 64)); }
 
 } // namespace
+
+extern "C" int ccmi_quantize_f32(const float *x, int64_t n, int quantizer, float temperature, const float *noise,
+                                 float *y, float *dy, void *stream)
+{
+    if (!x || !y || n < 0) return ccmi_set_error(CCMI_ERR_ARG, "quantize: null argument");
+    if (n > INT32_MAX) return ccmi_set_error(CCMI_ERR_ARG, "quantize: n > 2^31");
+    if (quantizer < CCMI_Q_NONE || quantizer > CCMI_Q_TRUE_STE) return ccmi_set_error(CCMI_ERR_ARG, "quantize: type %d", quantizer);
+    if ((quantizer == CCMI_Q_SOFTROUND || quantizer == CCMI_Q_SOFTROUND_ALONE || quantizer == CCMI_Q_STE) &&
+        !(temperature > 0.f))
+        return ccmi_set_error(CCMI_ERR_ARG, "quantize: soft-round temperature must be > 0");
+    if (n == 0) return CCMI_OK;
+    // noise comes as a tensor (or none): the counter-based generator is not used here
+    hipLaunchKernelGGL(t_quant, grid1(n, 1), dim3(kT), 0, static_cast<hipStream_t>(stream), x, (int64_t)n, (int)n, 1.f,
+                       quantizer, (int)CCMI_NOISE_NONE, temperature, 1.f, (uint64_t)0, 0, noise, y, dy, (float *)nullptr);
+    CCMI_HIP_CHECK(hipGetLastError());
+    return CCMI_OK;
+}
 
 extern "C" size_t ccmi_train_param_count(const ccmi_train_args *a)
 {
@@ -1379,10 +1402,10 @@ extern "C" int ccmi_train_step(const ccmi_train_args *a, void *stream)
         // persistent over the latent tiles: about one resident wave of workgroups for the batch
         dim3 grid((unsigned)std::max(1, std::min(pl.nblk_arm, 2048 / B)), B);
         switch (g.d) {
-        case 8: launch_arm_d<8>(g.nh, grid, s, yq, g, pl.at, a->params, a->param_stride, lam_px, gq, Gth, GS, acc4); break;
-        case 16: launch_arm_d<16>(g.nh, grid, s, yq, g, pl.at, a->params, a->param_stride, lam_px, gq, Gth, GS, acc4); break;
-        case 24: launch_arm_d<24>(g.nh, grid, s, yq, g, pl.at, a->params, a->param_stride, lam_px, gq, Gth, GS, acc4); break;
-        default: launch_arm_d<32>(g.nh, grid, s, yq, g, pl.at, a->params, a->param_stride, lam_px, gq, Gth, GS, acc4); break;
+        case 8: launch_arm_d<8>(g.nh, grid, s, yq, g, pl.at, a->params, a->param_stride, lam_px, gq, Gth, GS, acc4, a->grad_rate, a->rate_out); break;
+        case 16: launch_arm_d<16>(g.nh, grid, s, yq, g, pl.at, a->params, a->param_stride, lam_px, gq, Gth, GS, acc4, a->grad_rate, a->rate_out); break;
+        case 24: launch_arm_d<24>(g.nh, grid, s, yq, g, pl.at, a->params, a->param_stride, lam_px, gq, Gth, GS, acc4, a->grad_rate, a->rate_out); break;
+        default: launch_arm_d<32>(g.nh, grid, s, yq, g, pl.at, a->params, a->param_stride, lam_px, gq, Gth, GS, acc4, a->grad_rate, a->rate_out); break;
         }
         CCMI_HIP_CHECK(hipGetLastError());
     }
@@ -1414,8 +1437,21 @@ extern "C" int ccmi_train_step(const ccmi_train_args *a, void *stream)
     for (int i = 0; i < g.n_sp; ++i)
         hipLaunchKernelGGL(t_sp_fwd, grid1(npx, B), dim3(kT), 0, s, F(pl.z[i]), g, a->params, a->param_stride, g.sp_w[i],
                            g.sp_b[i], g.sp_res[i], g.sp_relu[i], F(pl.z[i + 1]));
-    hipLaunchKernelGGL(t_loss, grid1(npx, B), dim3(kT), 0, s, F(pl.z[g.n_sp]), g, a->target, a->target_stride, a->yuv420,
-                       graw, acc4);
+    if (a->raw_out)
+        CCMI_HIP_CHECK(hipMemcpyAsync(a->raw_out, F(pl.z[g.n_sp]), sizeof(float) * 3 * npx * B, hipMemcpyDeviceToDevice, s));
+    if (a->forward_only) {
+        if (a->loss_out) {
+            const float total = a->yuv420 ? (float)(npx + 2 * (int64_t)(g.H / 2) * (g.W / 2)) : (float)(3 * npx);
+            hipLaunchKernelGGL(t_finish, dim3(1), dim3(std::max(64, B)), 0, s, acc4, 1.f / total, lam_px, a->loss_out, B);
+        }
+        CCMI_HIP_CHECK(hipGetLastError());
+        return CCMI_OK;
+    }
+    if (a->grad_raw) // the caller's d loss / d raw output (autograd); no built-in MSE term
+        CCMI_HIP_CHECK(hipMemcpyAsync(graw, a->grad_raw, sizeof(float) * 3 * npx * B, hipMemcpyDeviceToDevice, s));
+    else
+        hipLaunchKernelGGL(t_loss, grid1(npx, B), dim3(kT), 0, s, F(pl.z[g.n_sp]), g, a->target, a->target_stride,
+                           a->yuv420, graw, acc4);
 
     // ---- synthesis backward
     float *gcur = graw;

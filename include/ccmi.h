@@ -400,10 +400,25 @@ typedef struct ccmi_train_args {
                                latents only (optimized_module ["latent"]; the norm still covers all) */
     void *workspace;        /* ccmi_train_workspace_bytes() */
     size_t workspace_bytes;
+    /* autograd use (torch.autograd.Function around the train-mode forward): */
+    int forward_only;       /* 1: run the training forward only and write raw_out / rate_out */
+    float *raw_out;         /* optional [batch][3][H][W]: raw synthesis output of the forward */
+    float *rate_out;        /* optional [batch][N]: per-latent rate (bits) of the forward */
+    const float *grad_raw;  /* optional [batch][3][H][W]: d loss / d raw output, used instead of
+                               the built-in MSE term (whose value then reads 0 in loss_out) */
+    const float *grad_rate; /* optional [batch][N]: d loss / d rate per latent, used instead of
+                               the built-in lmbda / (H W) */
 } ccmi_train_args;
 size_t ccmi_train_param_count(const ccmi_train_args *args);
 size_t ccmi_train_workspace_bytes(const ccmi_train_args *args);
 int ccmi_train_step(const ccmi_train_args *args, void *stream);
+
+/* quantize (quantizer.py:116-232) of n values x (already multiplied by the encoder gain):
+ * y = Q(x) and dy = dQ/dx as the reference's autograd sees it (softround derivative for
+ * "ste", 1 for "true_ste" and "none", 0 for "hardround"); noise: optional [n] additive
+ * noise (the reference draws it with torch.rand_like / randn_like).  Device pointers. */
+int ccmi_quantize_f32(const float *x, int64_t n, int quantizer, float temperature, const float *noise, float *y,
+                      float *dy, void *stream);
 
 #ifdef __cplusplus
 }

@@ -1,0 +1,103 @@
+"""The reference's optimisation loop (enc/training/train.py:238-262) driving the HIP training
+kernels through the mirror modules: FrameEncoder.forward in train mode (ccmi.autograd:
+torch.autograd.Functions whose forward and backward run in libccmi), the mirror loss_function,
+loss.backward(), clip_grad_norm_, torch.optim.Adam -- checked against the reference's own
+gradients and parameters after two steps (tests/golden/train_*.npz, small cases; the 128 x 192
+golden is the kernel-level test's, see test_train_gpu.py)."""
+import ast
+from pathlib import Path
+
+import numpy as np
+import pytest
+import torch
+
+GOLDEN = Path(__file__).resolve().parent / "golden"
+FILES = [f for f in sorted(GOLDEN.glob("train_*.npz")) if "g1/latent_grids.0.data" not in np.load(f).files]
+pytestmark = pytest.mark.gpu
+
+
+def _build(z, gpu):
+    from coolchic.enc.component.coolchic import CoolChicEncoderParameter
+    from coolchic.enc.component.frame import FrameEncoder
+    meta = ast.literal_eval(str(z["meta"]))
+    p = CoolChicEncoderParameter(layers_synthesis=meta["layers"].split("|"), n_ft_per_res=[1] * meta["n_grids"],
+                                 dim_arm=meta["dim_arm"], n_hidden_layers_arm=meta["n_hidden_arm"])
+    p.set_image_size((meta["H"], meta["W"]))
+    fe = FrameEncoder(p, frame_data_type="yuv420" if meta["yuv420"] else "rgb")
+    sd = {k[2:]: torch.from_numpy(z[k]) for k in z.files if k.startswith("p/")}
+    missing, unexpected = fe.coolchic_encoder.load_state_dict(sd, strict=False)
+    assert not unexpected, unexpected
+    assert all("upsampling" in k and k.endswith("bias") for k in missing), missing  # unused reference biases
+    fe = fe.to(gpu)
+    fe.set_to_train() if hasattr(fe, "set_to_train") else fe.train()
+    if meta["yuv420"]:
+        tgt = {c: torch.from_numpy(z[f"t420_{c}"])[None, None].to(gpu) for c in "yuv"}
+    else:
+        tgt = torch.from_numpy(z["t444"])[None].to(gpu)
+    return fe, tgt, meta
+
+
+def _close(got, ref, name, rtol=2e-3):
+    np.testing.assert_allclose(got, ref, rtol=rtol, atol=1e-7 + 2e-4 * np.abs(ref).max(), err_msg=name)
+
+
+@pytest.mark.parametrize("f", FILES, ids=lambda f: f.stem)
+def test_reference_loop_through_mirror_modules(f, gpu):
+    from coolchic.enc.training.loss import loss_function
+    from torch.nn.utils import clip_grad_norm_
+    z = np.load(f)
+    fe, target, meta = _build(z, gpu)
+    qtype = meta["quantizer_type"]
+    names = [n for n, _ in fe.coolchic_encoder.named_parameters()]
+    params = list(fe.parameters())
+    optimizer = torch.optim.Adam(fe.parameters(), lr=meta["lr"])
+    for s in (1, 2):
+        # ---- train.py:238-262, verbatim in shape
+        for param in params:
+            param.grad = None
+        out_forward = fe.forward(quantizer_noise_type="gaussian" if qtype == "softround" else "none",
+                                 quantizer_type=qtype, soft_round_temperature=torch.tensor(meta["temperature"]),
+                                 noise_parameter=torch.tensor(0.0))
+        out = loss_function(out_forward.decoded_image, out_forward.rate, target, lmbda=meta["lmbda"],
+                            rate_mlp_bit=0.0, compute_logs=True)
+        out.loss.backward()
+        if s == 1:
+            assert abs(out.loss.item() - float(z["loss"])) <= 1e-5 * abs(float(z["loss"]))
+            for n, p in fe.coolchic_encoder.named_parameters():
+                if f"g/{n}" not in z.files:
+                    continue
+                if p.grad is None:  # the upsampling biases: in the reference's state, unused by its forward
+                    assert not np.any(z[f"g/{n}"]), n
+                    continue
+                _close(p.grad.cpu().numpy(), z[f"g/{n}"], "grad " + n)
+        clip_grad_norm_(params, 1e-1, norm_type=2.0, error_if_nonfinite=False)
+        optimizer.step()
+        for n, p in fe.coolchic_encoder.named_parameters():
+            if f"s{s}/{n}" in z.files:
+                got, ref = p.detach().cpu().numpy(), z[f"s{s}/{n}"]
+                bad = np.abs(got - ref) > 1e-5 * np.abs(ref) + 2e-3 * meta["lr"]
+                assert bad.mean() <= 0.02, f"step {s} {n}: {int(bad.sum())} of {bad.size} off"
+                assert np.all(np.abs(got - ref) <= 2 * meta["lr"] + 1e-6), n
+    assert names
+
+
+def test_mirror_quantizer_matches_reference_formulas(gpu):
+    """core/quantizer.py on the GPU (ccmi_quantize_f32) against the reference's formulas
+    (quantizer.py:16-232, restated in oracle/train_oracle.py), values and derivatives."""
+    import train_oracle as to
+    from coolchic.enc.component.core.quantizer import quantize
+    g = torch.Generator().manual_seed(0)
+    x = (torch.randn(4096, generator=g) * 3).to(gpu)
+    for qtype in ("softround_alone", "softround", "ste", "true_ste", "hardround", "none"):
+        torch.manual_seed(5)
+        xg = x.clone().requires_grad_(True)
+        y = quantize(xg, "kumaraswamy", qtype, torch.tensor(0.3), torch.tensor(2.0))
+        y.sum().backward()
+        torch.manual_seed(5)  # the same noise, drawn the reference's way
+        from coolchic.enc.component.core.quantizer import draw_noise
+        nz = draw_noise(x, "kumaraswamy", torch.tensor(2.0))
+        xc = x.detach().cpu().clone().requires_grad_(True)
+        yc = to.quantize(xc, qtype, 0.3, nz.cpu())
+        yc.sum().backward()
+        np.testing.assert_allclose(y.detach().cpu().numpy(), yc.detach().numpy(), rtol=1e-5, atol=1e-5, err_msg=qtype)
+        np.testing.assert_allclose(xg.grad.cpu().numpy(), xc.grad.numpy(), rtol=1e-4, atol=1e-5, err_msg=qtype)
