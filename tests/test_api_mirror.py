@@ -38,12 +38,16 @@ def test_reference_state_dict_loads_strictly(path):
     assert mine == ref_keys
 
 
-def test_training_forward_is_refused_loudly():
+def test_forward_on_cpu_tensors_is_refused_loudly():
+    """No CPU path: a module left on the CPU raises in train and in eval mode."""
     z = np.load(GOLDEN[0])
     enc, _ = _build(z)
     enc.train()
-    with pytest.raises(NotImplementedError):
+    with pytest.raises((ValueError, RuntimeError)):
         enc.forward()
+    enc.eval()
+    with pytest.raises((ValueError, RuntimeError)):
+        enc.forward(quantizer_noise_type="none", quantizer_type="hardround")
 
 
 @pytest.mark.gpu
