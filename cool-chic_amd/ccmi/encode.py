@@ -215,6 +215,8 @@ def encode_frame(frame: CoolFrame, latent, search_counts: bool = False) -> bytes
         if search_counts:
             d.expgol_count[k] = -1
     n = sum(h * w for h, w in frame.grid_sizes)
+    if latent.numel() < n:
+        raise ValueError(f"encode_frame: {latent.numel()} latents given, the frame's grids hold {n}")
     s = torch.cuda.current_stream(latent.device).cuda_stream
     out = _grow(lambda buf, cap, ln: L.ccmi_encode_frame(C.byref(d), latent.data_ptr(), buf, cap, ln, s),
                 4 * n + (1 << 16))

@@ -74,34 +74,48 @@ class Record:
         return asdict(self)
 
 
+def encode_batch(targets: torch.Tensor, H: int, W: int, lmbda: float, arch, *, names=None, seeds=None,
+                 yuv420: bool = False, preset: str = "debug", scale: float = 1.0, write: bool = False) -> list[Record]:
+    """Overfit B frames of one geometry together (targets [B, n] flat ccmi.train targets on
+    the GPU, one independent decoder per frame), then measure each as the reference's test()
+    does (quantised model, hard-rounded latents): one Record per frame.  `seconds` is the
+    batch's wall time divided by B."""
+    from . import encode, quantize, train
+    warm, phases = (train.DEBUG_WARMUP, train.DEBUG_PHASES) if preset == "debug" else (train.C3X_WARMUP, train.C3X_PHASES)
+    B = targets.shape[0]
+    names = list(names) if names is not None else [""] * B
+    seeds = list(seeds) if seeds is not None else list(range(B))
+    npx = H * W
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    of, _ = train.overfit(arch, targets, lmbda=float(lmbda), yuv420=yuv420, scale=scale, seed=int(seeds[0]),
+                          warmup=warm, phases=phases)
+    torch.cuda.synchronize()
+    dt = time.perf_counter() - t0
+    its = sum(max(1, int(p.max_itr * scale)) for _, p in warm) + sum(max(1, int(p.max_itr * scale)) for p in phases)
+    out = []
+    for b in range(B):
+        mse, rate_lat = quantize.evaluate(arch, of.latents[b], of.params[b], of.targets[b], yuv420=yuv420, bitdepth=8)
+        qm = of.quantized[b] if of.quantized else None
+        nn_bits = sum(qm.nn_bits.values()) if qm else 0.0
+        rec = Record(image=names[b], lmbda=float(lmbda), seed=int(seeds[b]), psnr_db=-10 * math.log10(mse + 1e-10),
+                     rate_bpp=(rate_lat + nn_bits) / npx, rate_latent_bpp=rate_lat / npx, rate_nn_bpp=nn_bits / npx,
+                     iterations=its, seconds=dt / B)
+        if write and qm is not None:
+            rec.cool_bpp = 8 * len(encode.write_cool(arch, of.latents[b], qm, yuv420=yuv420)) / npx
+        out.append(rec)
+    return out
+
+
 def encode_points(target: torch.Tensor, H: int, W: int, lambdas, arch, *, yuv420: bool = False, seeds=(0,),
                   preset: str = "debug", scale: float = 1.0, name: str = "", write: bool = False) -> list[Record]:
     """Encode one image (flat ccmi.train target on the GPU) at every lambda; the seeds of one
     lambda train together as one batch (independent initialisations and noise streams)."""
-    from . import encode, quantize, train
-    warm, phases = (train.DEBUG_WARMUP, train.DEBUG_PHASES) if preset == "debug" else (train.C3X_WARMUP, train.C3X_PHASES)
     out = []
-    npx = H * W
     for lm in lambdas:
-        B = len(seeds)
-        tg = target.reshape(1, -1).repeat(B, 1).contiguous()
-        torch.cuda.synchronize()
-        t0 = time.perf_counter()
-        of, _ = train.overfit(arch, tg, lmbda=float(lm), yuv420=yuv420, scale=scale, seed=int(seeds[0]),
-                              warmup=warm, phases=phases)
-        torch.cuda.synchronize()
-        dt = time.perf_counter() - t0
-        its = sum(max(1, int(p.max_itr * scale)) for _, p in warm) + sum(max(1, int(p.max_itr * scale)) for p in phases)
-        for b, s in enumerate(seeds):
-            mse, rate_lat = quantize.evaluate(arch, of.latents[b], of.params[b], of.targets[b], yuv420=yuv420, bitdepth=8)
-            qm = of.quantized[b] if of.quantized else None
-            nn_bits = sum(qm.nn_bits.values()) if qm else 0.0
-            rec = Record(image=name, lmbda=float(lm), seed=int(s), psnr_db=-10 * math.log10(mse + 1e-10),
-                         rate_bpp=(rate_lat + nn_bits) / npx, rate_latent_bpp=rate_lat / npx, rate_nn_bpp=nn_bits / npx,
-                         iterations=its, seconds=dt / B)
-            if write and qm is not None:
-                rec.cool_bpp = 8 * len(encode.write_cool(arch, of.latents[b], qm, yuv420=yuv420)) / npx
-            out.append(rec)
+        tg = target.reshape(1, -1).repeat(len(seeds), 1).contiguous()
+        out += encode_batch(tg, H, W, lm, arch, names=[name] * len(seeds), seeds=seeds, yuv420=yuv420,
+                            preset=preset, scale=scale, write=write)
     return out
 
 
@@ -116,4 +130,4 @@ def curve(records, key="rate_bpp"):
             [float(np.mean([r["psnr_db"] for r in by[l]])) for l in lms], lms)
 
 
-__all__ = ["bd_rate", "bd_psnr", "Record", "encode_points", "curve"]
+__all__ = ["bd_rate", "bd_psnr", "Record", "encode_batch", "encode_points", "curve"]

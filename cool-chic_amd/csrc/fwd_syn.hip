@@ -127,7 +127,10 @@ constexpr int kSW = kRW / 2 + 1 + FT::NS - 1 + 3; // raw source tile pitch (37 u
 constexpr int kTW = kRW + 7 - 1 + 2;              // raw latent tile pitch (70 used, 72 read)
 constexpr int kPairs = kRW / 2 + 1;               // even/odd column pairs under <= kRW columns
 
-template <int CIN, int CMID, bool UPS>
+// MH: split-f16 MFMA first head layer (a separate instantiation: compiled into the default
+// kernel as a runtime branch, its registers pushed the VALU variant from 108 to 133 VGPRs,
+// i.e. from 4 to 3 waves per SIMD, and decode_fused from 0.97 to 1.40 ms per 32 frames)
+template <int CIN, int CMID, bool UPS, bool MH = false>
 __global__ __launch_bounds__(kFThreads) void syn_fused_kernel(FusedArgs A, LevelArgs U)
 {
     constexpr int NR = kRowsPerThread;
@@ -386,7 +389,7 @@ __global__ __launch_bounds__(kFThreads) void syn_fused_kernel(FusedArgs A, Level
         // the raw tiles (region 0) are overwritten by the head output below
         if constexpr (UPS) __syncthreads();
         FSTAMP(2);
-        if (A.n_head == 2 && A.head_mfma) {
+        if constexpr (MH) {
             // ---- split-f16 MFMA first layer, second layer on VALU from the accumulators
             const int hid = A.hid, lane = threadIdx.x & 63, hh = lane >> 5, m32 = lane & 31;
             const bool t1_full = hid > 16, t2 = hid > 32, t2_full = hid > 48;
@@ -714,6 +717,15 @@ void launch_fused(dim3 grid, hipStream_t s, const FusedArgs &fa, const LevelArgs
     }
 }
 
+// opt-in MFMA-head variant: the 7-grid decoders with upsampling fused (the common case) only
+template <int CMID>
+bool launch_fused_mfma_head(dim3 grid, hipStream_t s, const FusedArgs &fa, const LevelArgs &u)
+{
+    if (fa.cin != 7 || !fa.head_mfma) return false;
+    hipLaunchKernelGGL((syn_fused_kernel<7, CMID, true, true>), grid, dim3(kFThreads), 0, s, fa, u);
+    return true;
+}
+
 } // namespace
 
 namespace ccmi_fwd {
@@ -899,8 +911,11 @@ extern "C" int ccmi_decode_forward_f32(const ccmi_decode_args *a, void *stream)
     const int halo = P.fa.n_sp;
     P.fa.tiles_x = ccmi_div_up(y.w, kRW - 2 * halo);
     dim3 grid(P.fa.tiles_x * ccmi_div_up(y.h, kRH - 2 * halo), y.batch);
-    if (P.cmid == 3) launch_fused<3, true>(grid, s, P.fa, last);
-    else launch_fused<4, true>(grid, s, P.fa, last);
+    if (P.cmid == 3) {
+        if (!launch_fused_mfma_head<3>(grid, s, P.fa, last)) launch_fused<3, true>(grid, s, P.fa, last);
+    } else if (!launch_fused_mfma_head<4>(grid, s, P.fa, last)) {
+        launch_fused<4, true>(grid, s, P.fa, last);
+    }
     CCMI_HIP_CHECK(hipGetLastError());
     return CCMI_OK;
 }

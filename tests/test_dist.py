@@ -56,3 +56,73 @@ def test_shard_validates_rank():
     with pytest.raises(ValueError):
         cd.shard([1, 2], 2, 2)
     assert cd.shard(list(range(5)), 1, 2) == [1, 3]
+
+
+def test_bench_inputs_come_from_the_product_side():
+    """bench.py's timed legs build their frames with ccmi.synthetic (no oracle import); the
+    CPU baseline converts the same tensors, which equal the oracle's own random init."""
+    from pathlib import Path
+
+    import torch
+
+    import forward_oracle as fo
+    from ccmi import synthetic as S
+    a = S.random_frame(64, 96, seed=3)
+    b = fo.ModelParams.random(64, 96, seed=3)
+    for (w1, b1), (w2, b2) in zip(a.arm + a.syn, b.arm + b.syn):
+        assert torch.equal(w1, w2) and torch.equal(b1, b2)
+    for x, y in zip(a.ups_full() + a.pre_full(), b.ups_full() + b.pre_full()):
+        assert torch.equal(x, y)
+    src = (Path(__file__).resolve().parents[1] / "bench.py").read_text()
+    head = src[:src.index("def _oracle(")]
+    assert "forward_oracle" not in head and "sys.path.insert(0, str(ROOT / \"oracle\"))" not in head
+
+
+def test_bench_reference_comparison_and_proxies():
+    import importlib.util
+    from pathlib import Path
+    root = Path(__file__).resolve().parents[1]
+    spec = importlib.util.spec_from_file_location("bench_mod", root / "bench.py")
+    bench = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(bench)
+    px = bench.kodak_proxies()
+    assert [n for n, _ in px] == [f"kodim{i:02d}" for i in range(1, 25)]
+    rows = {(r["seq_name"], r["lmbda"]): r for r in bench.kodak_reference_rows()}
+    lms = [0.02, 0.004, 0.001, 0.0004]
+    # the reference's own points, fed back as "ours": deltas 0, BD-rate 0
+    recs = [{"image": n, "lmbda": lm, "psnr_db": rows[(n, lm)]["psnr_db"], "rate_bpp": rows[(n, lm)]["rate_bpp"]}
+            for n in ("kodim01", "kodim07") for lm in lms]
+    c = bench.compare_with_reference(recs, lms)
+    assert c["bd_rate_images"] == 2 and abs(c["bd_rate_vs_reference_pct_mean"]) < 1e-6
+    for v in c["per_lambda"].values():
+        assert v["psnr_db_mean"] == v["reference_psnr_db_mean"] and v["images"] == 2
+
+
+@pytest.mark.gpu
+def test_bench_two_ranks_gloo_on_one_gpu(tmp_path):
+    """bench.py's multi-rank path end to end: torch.distributed.run with 2 ranks on the one
+    card (CCMI_BENCH_BACKEND=gloo), tiny legs; the line reports the whole job of both ranks."""
+    import json
+    import subprocess
+    import sys
+    from pathlib import Path
+
+    import torch
+    assert torch.cuda.device_count() >= 1   # counts without initialising HIP in this process
+    root = Path(__file__).resolve().parents[1]
+    env = dict(os.environ, CCMI_BENCH_BACKEND="gloo", OMP_NUM_THREADS="2")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2",
+           "--master-addr=127.0.0.1", f"--master-port={_free_port()}", str(root / "bench.py"), "--gpus", "2",
+           "--steps", "2", "--warmup", "1", "--batch", "2", "--hd-steps", "0", "--decode-reps", "1",
+           "--hd-decode-reps", "1", "--encode-images", "3", "--encode-scale", "0.002", "--no-cpu-baseline"]
+    p = subprocess.run(cmd, cwd=root, env=env, capture_output=True, text=True, timeout=110)
+    assert p.returncode == 0, p.stderr[-3000:]
+    line = [x for x in p.stdout.splitlines() if x.startswith("{")]
+    assert len(line) == 1, p.stdout[-2000:]
+    r = json.loads(line[0])
+    assert r["n_gpus"] == 2 and r["per_gpu"] * 2 == pytest.approx(r["value"], rel=1e-3)
+    assert r["bitexact_decode"]["frames"] == 15 and r["bitexact_decode"]["bit_exact_vs_reference_md5"]
+    assert r["bitexact_decode_1080p"]["frames"] == 5
+    assert r["bitexact_encode"]["identical_to_shipped_streams"] and r["bitexact_encode"]["frames"] == 30
+    e = r["encoder_overfit"]
+    assert sorted(x["image"] for x in e["records"]) == ["kodim01", "kodim02", "kodim03"]

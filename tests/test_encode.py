@@ -170,6 +170,8 @@ def test_gpu_encode_frame_reproduces_shipped_stream(f, enc, oracle_c, gpu):
     x = torch.from_numpy(np.concatenate(lat).astype(np.int32)).to(gpu)
     out = enc.encode_frame(fr, x)
     assert out == data
+    with pytest.raises(ValueError):   # short latent buffer: refused before any device read
+        enc.encode_frame(enc.parse(data), x[:-1].clone())
 
 
 @pytest.mark.gpu

@@ -1,0 +1,69 @@
+"""Register / scratch budgets of the hot kernels, read from the gfx950 code-object metadata
+of the built libccmi.so (no GPU needed).  A budget line here is a performance contract:
+crossing a VGPR step halves or thirds the waves a SIMD can hold (512 VGPRs per lane slot:
+<= 128 -> 4 waves, <= 168 -> 3, <= 256 -> 2), which the bench only shows at round end.
+Round 2 lost 30 % of the headline this way (an opt-in MFMA head compiled into the default
+fused kernel took it from 108 to 133 VGPRs)."""
+import re
+import shutil
+import subprocess
+from pathlib import Path
+
+import pytest
+
+ROOT = Path(__file__).resolve().parents[1]
+LIB = ROOT / "cool-chic_amd" / "lib" / "libccmi.so"
+LLVM = Path("/opt/rocm/lib/llvm/bin")
+
+# demangled-name prefix -> (max VGPRs, scratch bytes allowed)
+BUDGET = {
+    "syn_fused_kernel<7, 3, true, false>": (128, 0),   # path A headline (hop, 7 grids)
+    "syn_fused_kernel<7, 4, true, false>": (128, 0),
+    "arm_fwd_kernel<16>": (128, 0),                      # path A ARM + rate
+    "ups_level_fixed<8, 7>": (64, 0),                    # upsampling pyramid
+    "dec_arm_kernel<16, 2>": (128, 0),                   # path B ARM + CABAC
+    "dec_arm_spec_kernel<16, 2>": (128, 0),
+    "dec_ups_level_batch": (64, 0),
+    "t_arm<16, 2>": (168, 0),                            # training step (3 waves / SIMD)
+    "t_head_bwd<7, 3>": (128, 0),
+    "t_sp_bwd": (168, 0),
+}
+
+
+def _metadata(tmp_path):
+    objdump, readelf = LLVM / "llvm-objdump", LLVM / "llvm-readelf"
+    if not (LIB.exists() and objdump.exists() and readelf.exists()):
+        pytest.skip("libccmi.so or the ROCm llvm tools are absent")
+    lib = tmp_path / "libccmi.so"
+    shutil.copy(LIB, lib)
+    subprocess.run([str(objdump), "--offloading", str(lib)], cwd=tmp_path, check=True, capture_output=True)
+    text = "".join(subprocess.run([str(readelf), "--notes", str(f)], capture_output=True, text=True).stdout
+                   for f in sorted(tmp_path.glob("libccmi.so.*gfx950")))
+    out, name = {}, None
+    for line in text.splitlines():
+        m = re.match(r"\s+\.name:\s+(\S+)", line)
+        if m:
+            name = m.group(1)
+            out[name] = {}
+            continue
+        m = re.match(r"\s+\.(vgpr_count|vgpr_spill_count|private_segment_fixed_size):\s+(\d+)", line)
+        if m and name:
+            out[name][m.group(1)] = int(m.group(2))
+    names = list(out)
+    dem = subprocess.run(["c++filt"], input="\n".join(names), capture_output=True, text=True).stdout.splitlines()
+    return {d: out[n] for n, d in zip(names, dem)}
+
+
+def test_hot_kernel_register_budgets(tmp_path):
+    meta = _metadata(tmp_path)
+    assert len(meta) > 50
+    lines = []
+    for key, (vmax, scratch) in BUDGET.items():
+        hits = [(d, v) for d, v in meta.items() if key in d]
+        assert hits, f"kernel {key} not found in libccmi.so"
+        for d, v in hits:
+            lines.append(f"{d[:100]}: {v}")
+            assert v.get("vgpr_count", 0) <= vmax, lines[-1]
+            assert v.get("vgpr_spill_count", 0) == 0, lines[-1]
+            assert v.get("private_segment_fixed_size", 0) <= scratch, lines[-1]
+    print("\n".join(lines))

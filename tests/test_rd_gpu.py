@@ -104,3 +104,49 @@ def test_debug_preset_matches_reference_rd(image, gpu):
     for r in recs:
         assert r.cool_bpp == r.cool_bpp and r.cool_bpp > 0
     assert np.isfinite(bd)
+
+
+# c3x preset (preset_cfg/c3x.yaml) with every phase / warm-up / patience scaled by 0.1, as
+# tools/gen_golden_rd.py ran it (C3X_SCALE): one reference seed per lambda, so the tolerance is
+# the fixed margin widened by the debug preset's largest seed spread on the same image.
+C3X_SCALE = 0.1
+
+
+@pytest.mark.parametrize("image", ["kodim15_192x128", "kodim01_768x512"])
+def test_c3x_preset_matches_reference_rd(image, gpu):
+    from ccmi import io, rd, train
+    d = json.loads((GOLDEN / "rd_reference_c3x.json").read_text())
+    ref = [r for r in d["runs"] if r["image"] == image]
+    assert {r["lmbda"] for r in ref} == set(LAMBDAS)
+    spread_p = max(max(x["psnr_db"] for x in g) - min(x["psnr_db"] for x in g)
+                   for g in ([r for r in _ref("rd_reference_debug.json") if r["image"] == image and r["lmbda"] == lm]
+                             for lm in LAMBDAS))
+    x = _targets()[image]
+    H, W = x.shape[-2:]
+    arch = train.Arch(H, W, dim_arm=16, n_hidden=2, layers=HOP)
+    tgt = io.to_target(x, "rgb").to(gpu)
+    recs = rd.encode_points(tgt, H, W, LAMBDAS, arch, yuv420=False, seeds=(0, 1), preset="c3x", scale=C3X_SCALE,
+                            name=image)
+    out = ROOT / "gpurun_out"
+    out.mkdir(exist_ok=True)
+    f = out / "rd_gpu_c3x.json"
+    prev = json.loads(f.read_text()) if f.exists() else {}
+    prev[image] = [r.as_dict() for r in recs]
+    f.write_text(json.dumps(prev, indent=1))
+    lines = []
+    for lm in LAMBDAS:
+        r = [x for x in ref if x["lmbda"] == lm][0]
+        o = [x for x in recs if x.lmbda == lm]
+        op, orr = np.mean([x.psnr_db for x in o]), np.mean([x.rate_bpp for x in o])
+        tol_p = PSNR_MARGIN_DB + spread_p
+        lines.append(f"{image} c3x lambda {lm}: PSNR ref {r['psnr_db']:.3f} gpu {op:.3f} (tol {tol_p:.2f}), "
+                     f"rate ref {r['rate_bpp']:.4f} gpu {orr:.4f}, iterations ref {r['iterations']} gpu {o[0].iterations}")
+        assert abs(op - r["psnr_db"]) <= tol_p, lines[-1]
+        assert abs(orr / r["rate_bpp"] - 1) <= 2 * RATE_MARGIN, lines[-1]
+    R1, P1, _ = rd.curve(ref)
+    R2, P2, _ = rd.curve(recs)
+    bd = rd.bd_rate(R1, P1, R2, P2)
+    lines.append(f"{image} c3x: BD-rate GPU vs reference {bd:+.2f} %")
+    print("\n" + "\n".join(lines))
+    if image != "kodim15_192x128":
+        assert -BD_BETTER <= bd <= BD_WORSE, lines[-1]
