@@ -92,7 +92,10 @@ def encode_batch(targets: torch.Tensor, H: int, W: int, lmbda: float, arch, *, n
                           warmup=warm, phases=phases)
     torch.cuda.synchronize()
     dt = time.perf_counter() - t0
-    its = sum(max(1, int(p.max_itr * scale)) for _, p in warm) + sum(max(1, int(p.max_itr * scale)) for p in phases)
+    # counted as the reference's results columns count them: every warm-up candidate's
+    # iterations (3 x 10 + 2 x 10 for debug), then the phases
+    its = sum(n * max(1, int(p.max_itr * scale)) for n, p in warm) + \
+        sum(max(1, int(p.max_itr * scale)) for p in phases)
     out = []
     for b in range(B):
         mse, rate_lat = quantize.evaluate(arch, of.latents[b], of.params[b], of.targets[b], yuv420=yuv420, bitdepth=8)
