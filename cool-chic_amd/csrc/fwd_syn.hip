@@ -131,7 +131,7 @@ constexpr int kPairs = kRW / 2 + 1;               // even/odd column pairs under
 // kernel as a runtime branch, its registers pushed the VALU variant from 108 to 133 VGPRs,
 // i.e. from 4 to 3 waves per SIMD, and decode_fused from 0.97 to 1.40 ms per 32 frames)
 template <int CIN, int CMID, bool UPS, bool MH = false>
-__global__ __launch_bounds__(kFThreads) void syn_fused_kernel(FusedArgs A, LevelArgs U)
+__global__ __launch_bounds__(kFThreads) __attribute__((amdgpu_waves_per_eu(4))) void syn_fused_kernel(FusedArgs A, LevelArgs U)
 {
     constexpr int NR = kRowsPerThread;
     // region 0: raw input tiles (UPS, phase A-B), then the head output / 3x3 buffer 0
@@ -173,21 +173,26 @@ __global__ __launch_bounds__(kFThreads) void syn_fused_kernel(FusedArgs A, Level
     const int cxg = clampi(gx, A.W - 1);
 
     __shared__ float s_lut8[256];
-    const float *lut8 = nullptr;
-    if (A.qmax == 255.f) {
-        s_lut8[threadIdx.x & 255] = (float)(threadIdx.x & 255) / 255.f;
-        lut8 = s_lut8;
+    const float *lut8 = A.qmax == 255.f ? s_lut8 : nullptr;
+    // per-frame tables in LDS (8-bit output quotients, head weight records); with fused
+    // upsampling this runs while the raw tile loads are in flight, and the phase-A
+    // barrier publishes it
+    auto stage_tables = [&]() {
+        if (lut8) s_lut8[threadIdx.x & 255] = (float)(threadIdx.x & 255) / 255.f;
+        if (A.n_head == 2)
+            for (int i = threadIdx.x; i < A.hid * 16; i += kFThreads) {
+                const int j = i >> 4, f = i & 15;
+                float v = 0.f;
+                if (f < CIN) v = prm[A.w0_off + j * CIN + f];
+                else if (f == CIN) v = prm[A.b0_off + j];
+                else if (f <= CIN + CMID) v = prm[A.w1_off + (f - CIN - 1) * A.hid + j];
+                s_head[j][f] = v;
+            }
+    };
+    if constexpr (!UPS) {
+        stage_tables();
         __syncthreads();
     }
-    if (A.n_head == 2)
-        for (int i = threadIdx.x; i < A.hid * 16; i += kFThreads) {
-            const int j = i >> 4, f = i & 15;
-            float v = 0.f;
-            if (f < CIN) v = prm[A.w0_off + j * CIN + f];
-            else if (f == CIN) v = prm[A.b0_off + j];
-            else if (f <= CIN + CMID) v = prm[A.w1_off + (f - CIN - 1) * A.hid + j];
-            s_head[j][f] = v;
-        }
 
     // window's clamped image rectangle [Ya, Yb] x [Xa, Xb] (fused upsampling only)
     const int Ya = clampi(oy, A.H - 1), Yb = clampi(oy + kRH - 1, A.H - 1);
@@ -240,6 +245,7 @@ __global__ __launch_bounds__(kFThreads) void syn_fused_kernel(FusedArgs A, Level
                     tv[u] = rs[(int64_t)Y * U.wd + X];
 #endif
             }
+            stage_tables();
 #pragma unroll
             for (int u = 0; u < NSU; ++u) {
                 const int i = threadIdx.x + u * kFThreads;
@@ -258,25 +264,35 @@ __global__ __launch_bounds__(kFThreads) void syn_fused_kernel(FusedArgs A, Level
         // which share NS source samples (compile-time taps per parity).
         {
             const int xe0 = Xa & ~1; // first even column of the pairs
-#pragma unroll 2
-            for (int i = threadIdx.x; i < C * kHsRows * kPairs; i += kFThreads) {
-                const int ch = i / (kHsRows * kPairs), rem = i - ch * (kHsRows * kPairs);
-                const int jj = rem / kPairs, k = rem - jj * kPairs;
-                if (jj >= nj) continue;
-                const int xe = xe0 + 2 * k - Xa; // window-relative column of the even output
-                if (xe > nX - 1) continue;
-                const float *sr = s_st + (ch * kHsRows + jj) * kSW + k;
-                float e = 0.f, o = 0.f;
+            // one item = 4 consecutive pairs of a source row: NS + 3 samples read once, the
+            // (even, odd) outputs of a pair accumulated as one packed FMA per sample
+            constexpr int kG = (kPairs + 3) / 4;
+            f2 wp[FT::NS];
 #pragma unroll
-                for (int m = 0; m < FT::NS; ++m) {
-                    const float v = sr[m];
-                    const int te = FT::tap(0, FT::D0 + m), to = FT::tap(1, FT::D0 + m);
-                    if (te >= 0) e = fmaf(wu[te], v, e);
-                    if (to >= 0) o = fmaf(wu[to], v, o);
-                }
+            for (int m = 0; m < FT::NS; ++m) {
+                const int te = FT::tap(0, FT::D0 + m), to = FT::tap(1, FT::D0 + m);
+                wp[m] = f2{te >= 0 ? wu[te] : 0.f, to >= 0 ? wu[to] : 0.f};
+            }
+            static_assert(4 * kG + FT::NS - 1 <= kSW, "group reads stay inside the source row");
+#pragma unroll 2
+            for (int i = threadIdx.x; i < C * kHsRows * kG; i += kFThreads) {
+                const int ch = i / (kHsRows * kG), rem = i - ch * (kHsRows * kG);
+                const int jj = rem / kG, g = rem - jj * kG;
+                if (jj >= nj) continue;
+                const float *sr = s_st + (ch * kHsRows + jj) * kSW + 4 * g;
+                float v[FT::NS + 3];
+#pragma unroll
+                for (int m = 0; m < FT::NS + 3; ++m) v[m] = sr[m];
                 float *hr = s_hs + (ch * kHsRows + jj) * kRW;
-                if (xe >= 0) hr[xe] = e;
-                if (xe + 1 < nX) hr[xe + 1] = o;
+#pragma unroll
+                for (int q = 0; q < 4; ++q) {
+                    f2 eo = f2(0.f);
+#pragma unroll
+                    for (int m = 0; m < FT::NS; ++m) eo = __builtin_elementwise_fma(wp[m], f2(v[q + m]), eo);
+                    const int xe = xe0 + 2 * (4 * g + q) - Xa; // window-relative column of the even output
+                    if (xe >= 0 && xe <= nX - 1) hr[xe] = eo.x;
+                    if (xe + 1 >= 0 && xe + 1 < nX) hr[xe + 1] = eo.y;
+                }
             }
         }
         // refine: one item = 4 consecutive columns of a row (sliding 7-tap window)
