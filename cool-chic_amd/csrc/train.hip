@@ -195,7 +195,9 @@ __device__ __forceinline__ void mfma_outer(const float *s_g, const float *s_a, v
             const float av = 16 * mt + ln < R ? s_g[r * (R + 1) + 16 * mt + ln] : 0.f;
 #pragma unroll
             for (int nt = 0; nt < NT; ++nt) acc[mt][nt] = mfma4(av, bv[nt], acc[mt][nt]);
+#if !defined(CCMI_DIAG_ARM_NOBIAS) // diagnostic builds only (tools/arm_diag.sh): wrong results
             accb[mt] = mfma4(av, 1.f, accb[mt]);
+#endif
         }
     }
 }
@@ -236,16 +238,17 @@ __device__ __forceinline__ void wave_add(float v, float *dst)
 }
 
 template <int D, int NH>
-__global__ __launch_bounds__(kT) void t_arm(const float *__restrict__ yq, Geo g, ArmTiles at, const float *__restrict__ th,
+__global__ __launch_bounds__(kT) __attribute__((amdgpu_waves_per_eu(3))) void t_arm(const float *__restrict__ yq, Geo g, ArmTiles at, const float *__restrict__ th,
                                             int64_t ps, float lam_px, float *__restrict__ gq,
                                             float *__restrict__ gth, int64_t gstride, float *__restrict__ acc4,
                                             const float *__restrict__ grad_rate, float *__restrict__ rate_out)
 {
     constexpr int NT = (D + 15) / 16, MT = (D + 15) / 16;
     __shared__ float s_y[kALH][kALW];
-    __shared__ float s_gy[kALH][kALW];
-    __shared__ float s_g[kT * (D + 1)];
-    __shared__ float s_a[kT * (D + 1)];
+    // MFMA staging rows (per wave: gradients s_g, activations s_a), one array so the
+    // context-gradient planes can span both once the MFMA stage is over
+    __shared__ float s_ga[2 * kT * (D + 1)];
+    float *const s_g = s_ga, *const s_a = s_ga + kT * (D + 1);
 
     const int b = blockIdx.y;
     const int w = threadIdx.x >> 6;
@@ -269,23 +272,47 @@ __global__ __launch_bounds__(kT) void t_arm(const float *__restrict__ yq, Geo g,
         }
     float rsum = 0.f;
 
-    for (int t = blockIdx.x; t < at.start[at.n]; t += gridDim.x) {
-        int l = 0;
+    // the latent tile (+ causal halo) of the NEXT tile is loaded into registers while this
+    // one is processed, so a tile starts without waiting on HBM
+    constexpr int kSU = (kALH * kALW + kT - 1) / kT;
+    float pre[kSU];
+    auto tile_geo = [&](int t, int &l, int &y0, int &x0) {
+        l = 0;
 #pragma unroll
         for (int k = 1; k < CCMI_MAX_GRIDS; ++k)
             if (k < at.n && t >= at.start[k]) l = k;
         const int lt = t - at.start[l];
+        y0 = (lt / at.tiles_x[l]) * kATY;
+        x0 = (lt % at.tiles_x[l]) * kATX;
+    };
+    auto load_tile = [&](int t) {
+        int l, y0, x0;
+        tile_geo(t, l, y0, x0);
         const int H = g.h[l], W = g.w[l];
-        const int y0 = (lt / at.tiles_x[l]) * kATY, x0 = (lt % at.tiles_x[l]) * kATX;
         const float *src = yq + (int64_t)b * g.N + g.off[l];
-        float *gdst = gq + (int64_t)b * g.N + g.off[l];
-        __syncthreads(); // previous tile's LDS readers are done
-        for (int i = threadIdx.x; i < kALH * kALW; i += kT) {
+#pragma unroll
+        for (int u = 0; u < kSU; ++u) {
+            const int i = threadIdx.x + u * kT;
             const int r = i / kALW, c = i - r * kALW;
             const int y = y0 - kAH + r, x = x0 - kAH + c;
-            s_y[r][c] = (y >= 0 && y < H && x >= 0 && x < W) ? src[y * W + x] : 0.f;
-            s_gy[r][c] = 0.f;
+            pre[u] = (i < kALH * kALW && y >= 0 && y < H && x >= 0 && x < W) ? src[y * W + x] : 0.f;
         }
+    };
+    const int n_tiles = at.start[at.n];
+    if ((int)blockIdx.x < n_tiles) load_tile(blockIdx.x);
+
+    for (int t = blockIdx.x; t < n_tiles; t += gridDim.x) {
+        int l, y0, x0;
+        tile_geo(t, l, y0, x0);
+        const int H = g.h[l], W = g.w[l];
+        float *gdst = gq + (int64_t)b * g.N + g.off[l];
+        __syncthreads(); // previous tile's LDS readers are done
+#pragma unroll
+        for (int u = 0; u < kSU; ++u) {
+            const int i = threadIdx.x + u * kT;
+            if (i < kALH * kALW) (&s_y[0][0])[i] = pre[u];
+        }
+        if (t + (int)gridDim.x < n_tiles) load_tile(t + gridDim.x);
         __syncthreads();
         const bool valid = (y0 + cy) < H && (x0 + cx) < W;
 
@@ -351,7 +378,9 @@ __global__ __launch_bounds__(kT) void t_arm(const float *__restrict__ yq, Geo g,
 #pragma unroll
             for (int i = 0; i < D; ++i) sa[(threadIdx.x & 63) * (D + 1) + i] = xs[NH][i];
             wave_lds_sync(); // each wave stages and reads only its own 64 rows
+#if !defined(CCMI_DIAG_ARM_NOOUTER)
             mfma_outer<2, D>(sg, sa, acc_o, accb_o);
+#endif
             wave_lds_sync();
         }
 #pragma unroll
@@ -366,7 +395,9 @@ __global__ __launch_bounds__(kT) void t_arm(const float *__restrict__ yq, Geo g,
 #pragma unroll
             for (int i = 0; i < D; ++i) sa[(threadIdx.x & 63) * (D + 1) + i] = xs[L][i];
             wave_lds_sync();
+#if !defined(CCMI_DIAG_ARM_NOOUTER)
             mfma_outer<D, D>(sg, sa, acc_h[L], accb_h[L]);
+#endif
             wave_lds_sync();
 #pragma unroll
             for (int i = 0; i < D; ++i) {
@@ -376,21 +407,36 @@ __global__ __launch_bounds__(kT) void t_arm(const float *__restrict__ yq, Geo g,
                 gx[i] = a;
             }
         }
-        // ---- context gradients -> LDS tile, then one global atomic per touched position
-        if (valid) {
+        // ---- context gradients: each latent's D + 1 gradients (contexts, then its own value)
+        // go to LDS rows (this wave's own rows of s_g, free after its MFMA stage); every
+        // position of the tile + causal halo then GATHERS what the latents whose context holds
+        // it send, and adds the sum to HBM with one atomic.  (Scattering with LDS float atomics
+        // instead runs at about half a lane per clock on gfx950: 35 % of this kernel; a
+        // row-per-wave gather over zero-padded planes measured slower than this form.)
+        {
+            float *row = sg + (threadIdx.x & 63) * (D + 1);
 #pragma unroll
-            for (int i = 0; i < D; ++i) {
-                int dy, dx;
-                ctx_off<D>(i, dy, dx);
-                atomicAdd(&s_gy[cy + kAH + dy][cx + kAH + dx], gx[i]);
-            }
-            atomicAdd(&s_gy[cy + kAH][cx + kAH], g_q);
+            for (int i = 0; i < D; ++i) row[i] = valid ? gx[i] : 0.f;
+            row[D] = valid ? g_q : 0.f;
         }
         __syncthreads();
-        for (int i = threadIdx.x; i < kALH * kALW; i += kT) {
-            const int r = i / kALW, c = i - r * kALW;
+        // halo row 0 receives nothing (context rows reach 3 rows up)
+#pragma unroll 1
+        for (int i = threadIdx.x; i < (kALH - 1) * kALW; i += kT) {
+            const int r = 1 + i / kALW, c = i - (r - 1) * kALW;
             const int y = y0 - kAH + r, x = x0 - kAH + c;
-            const float v = s_gy[r][c];
+            float v = 0.f;
+            {   // own value: the latent at (r - kAH, c - kAH)
+                const int ly = r - kAH, lx = c - kAH;
+                if (ly >= 0 && lx >= 0 && lx < kATX) v = s_g[(ly * kATX + lx) * (D + 1) + D];
+            }
+#pragma unroll
+            for (int k = 0; k < D; ++k) {
+                int dy, dx;
+                ctx_off<D>(k, dy, dx);
+                const int ly = r - kAH - dy, lx = c - kAH - dx;
+                if (ly >= 0 && ly < kATY && lx >= 0 && lx < kATX) v += s_g[(ly * kATX + lx) * (D + 1) + k];
+            }
             if (y >= 0 && y < H && x >= 0 && x < W && v != 0.f) atomicAdd(&gdst[y * W + x], v);
         }
     }
