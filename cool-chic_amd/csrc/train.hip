@@ -739,15 +739,19 @@ __global__ __launch_bounds__(kHeadT) void t_head_bwd(const float *__restrict__ d
                                                      const float *__restrict__ th, int64_t ps, float *__restrict__ gdense,
                                                      float *__restrict__ gth, int64_t gstride)
 {
-    // dynamic LDS, per wave: [64][hp] h, then g_h (pixel-major, hp = hid | 1: conflict-free
-    // row writes); [64][9] gp, then [x | 1]
+    // dynamic LDS, per wave: [64][hp] h, then g_h (pixel-major, hp = 16 NT + 1: conflict-free
+    // row writes, columns [hid, 16 NT) zero); [64][kXP] gp | 0, then x | 1 | 0.  The zero
+    // columns let every lane read its MFMA operand unconditionally (no exec-mask branches
+    // between the LDS reads and the MFMAs).
     extern __shared__ float s_dyn[];
+    constexpr int kXP = CIN + 2 > 4 ? CIN + 2 : 4;
     // hidden unit j: w0[j][0..CIN), b0[j], w1[0..3)[j] -- read back as broadcast ds_read_b128
     __shared__ __attribute__((aligned(16))) float s_rec[64][12];
     static_assert(CIN + 4 <= 12, "hidden-unit record");
     const int b = blockIdx.y, t = threadIdx.x, lane = t & 63, w = t >> 6;
-    const int hid = g.hid, hp = hid | 1; // NT = ceil(hid / 16), a template argument: the
-                                         // accumulator tiles must be compile-time registers
+    const int hid = g.hid; // NT = ceil(hid / 16), a template argument: the accumulator tiles
+                           // must be compile-time registers
+    constexpr int hp = 16 * NT + 1;
     const int64_t npx = (int64_t)g.H * g.W;
     const float *P = th + (int64_t)b * ps;
     for (int e = t; e < 64 * 12; e += kHeadT) {
@@ -761,8 +765,10 @@ __global__ __launch_bounds__(kHeadT) void t_head_bwd(const float *__restrict__ d
         s_rec[j][f] = v;
     }
     const float bo0 = P[g.b1], bo1 = P[g.b1 + 1], bo2 = P[g.b1 + 2];
-    float *sv = s_dyn + w * 64 * (hp + 9), *sw = sv + 64 * hp;
+    float *sv = s_dyn + w * 64 * (hp + kXP), *sw = sv + 64 * hp;
     const int ln = lane & 15, lk = lane >> 4;
+    for (int j = hid; j < 16 * NT; ++j) sv[lane * hp + j] = 0.f; // pad columns of this lane's row
+    const int ia = ln < 3 ? ln : 3, ib = ln <= CIN ? ln : CIN + 1; // operand columns (pads read 0)
     v4f a1[NT], a0[NT];
 #pragma unroll
     for (int q = 0; q < NT; ++q) a1[q] = a0[q] = v4f{0.f, 0.f, 0.f, 0.f};
@@ -804,16 +810,14 @@ __global__ __launch_bounds__(kHeadT) void t_head_bwd(const float *__restrict__ d
         // ---- dW1 += gp^T h (invalid pixels have gp = 0)
 #pragma unroll
         for (int k = 0; k < 3; ++k) sw[lane * 4 + k] = gp1[k];
+        sw[lane * 4 + 3] = 0.f;
         wave_lds_sync();
-#pragma unroll 4
+#pragma unroll
         for (int s = 0; s < 16; ++s) {
             const int px = 4 * s + lk;
-            const float a = ln < 3 ? sw[px * 4 + ln] : 0.f;
+            const float a = sw[px * 4 + ia];
 #pragma unroll
-            for (int q = 0; q < NT; ++q) {
-                const int j = 16 * q + ln;
-                a1[q] = mfma4(a, j < hid ? sv[px * hp + j] : 0.f, a1[q]);
-            }
+            for (int q = 0; q < NT; ++q) a1[q] = mfma4(a, sv[px * hp + 16 * q + ln], a1[q]);
         }
         wave_lds_sync();
         // ---- g_h (replaces h in this lane's row), g_x
@@ -836,18 +840,16 @@ __global__ __launch_bounds__(kHeadT) void t_head_bwd(const float *__restrict__ d
         }
         // ---- dW0 | db0 += g_h^T [x | 1]
 #pragma unroll
-        for (int i = 0; i < CIN; ++i) sw[lane * 9 + i] = xv[i];
-        sw[lane * 9 + CIN] = 1.f;
+        for (int i = 0; i < CIN; ++i) sw[lane * kXP + i] = xv[i];
+        sw[lane * kXP + CIN] = 1.f;
+        sw[lane * kXP + CIN + 1] = 0.f;
         wave_lds_sync();
-#pragma unroll 4
+#pragma unroll
         for (int s = 0; s < 16; ++s) {
             const int px = 4 * s + lk;
-            const float bb = ln <= CIN ? sw[px * 9 + ln] : 0.f;
+            const float bb = sw[px * kXP + ib];
 #pragma unroll
-            for (int q = 0; q < NT; ++q) {
-                const int j = 16 * q + ln;
-                a0[q] = mfma4(j < hid ? sv[px * hp + j] : 0.f, bb, a0[q]);
-            }
+            for (int q = 0; q < NT; ++q) a0[q] = mfma4(sv[px * hp + 16 * q + ln], bb, a0[q]);
         }
         wave_lds_sync();
     }
@@ -1342,7 +1344,8 @@ void launch_head(bool bwd, dim3 grid, hipStream_t s, const float *dense, const f
 {
     if (!bwd) hipLaunchKernelGGL((t_head_fwd<CIN>), grid, dim3(kT), 0, s, dense, g, th, ps, z0_or_gdense);
     else {
-        const size_t lds = sizeof(float) * (kHeadT / 64) * 64 * ((g.hid | 1) + 9);
+        constexpr int kXP = CIN + 2 > 4 ? CIN + 2 : 4; // t_head_bwd's per-wave LDS rows
+        const size_t lds = sizeof(float) * (kHeadT / 64) * 64 * (16 * ((g.hid + 15) / 16) + 1 + kXP);
         switch ((g.hid + 15) / 16) {
         case 1: hipLaunchKernelGGL((t_head_bwd<CIN, 1>), grid, dim3(kHeadT), lds, s, dense, gz0, g, th, ps, z0_or_gdense, gth, gstride); break;
         case 2: hipLaunchKernelGGL((t_head_bwd<CIN, 2>), grid, dim3(kHeadT), lds, s, dense, gz0, g, th, ps, z0_or_gdense, gth, gstride); break;
