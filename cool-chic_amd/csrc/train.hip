@@ -26,6 +26,8 @@
 //   t_head_bwd    1x1 head backward; weight gradients reduced through LDS
 //   t_ref_* / t_up_*        upsampling backward, one pyramid level at a time
 //   t_latgrad, t_sumsq, t_adam   dL/dy, global grad norm, clipped Adam update
+#include <stdlib.h>
+
 #include "fwd_common.h"
 
 using ccmi_fwd::cfloat_ptr;
@@ -175,28 +177,36 @@ typedef float v4f __attribute__((ext_vector_type(4)));
 __device__ __forceinline__ v4f mfma4(float a, float b, v4f c) { return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0); }
 
 // One layer's weight gradient over a wave's 64 rows, on the matrix cores:
-// acc[mt][nt] += G^T A, G = [64][R] (pitch R + 1), A = [64][D] (pitch D + 1): a GEMM
+// acc[mt][nt] += G^T A, G = [64][R] (pitch R + 1, column R zero), A = [64][D] (pitch D + 1,
+// column D zero): a GEMM
 // whose K is the latent index, 4 latents per MFMA.
 // With B = 1 the same A operand also accumulates the bias gradient sum_k A[m][k] (accb).
-template <int R, int D>
+template <int R, int D, bool BIAS = true>
 __device__ __forceinline__ void mfma_outer(const float *s_g, const float *s_a, v4f (&acc)[(R + 15) / 16][(D + 15) / 16],
                                            v4f (&accb)[(R + 15) / 16])
 {
     constexpr int MT = (R + 15) / 16, NT = (D + 15) / 16;
     const int lane = threadIdx.x & 63, ln = lane & 15, lk = lane >> 4;
+    // operand columns past R / D read the rows' zero pad column (R, D): no exec-mask branch
+    // between the LDS reads and the MFMAs
+    int ca[MT], cb[NT];
+#pragma unroll
+    for (int mt = 0; mt < MT; ++mt) ca[mt] = 16 * mt + ln < R ? 16 * mt + ln : R;
+#pragma unroll
+    for (int nt = 0; nt < NT; ++nt) cb[nt] = 16 * nt + ln < D ? 16 * nt + ln : D;
 #pragma unroll 4
     for (int s = 0; s < 16; ++s) {
         const int r = 4 * s + lk;
         float bv[NT];
 #pragma unroll
-        for (int nt = 0; nt < NT; ++nt) bv[nt] = 16 * nt + ln < D ? s_a[r * (D + 1) + 16 * nt + ln] : 0.f;
+        for (int nt = 0; nt < NT; ++nt) bv[nt] = s_a[r * (D + 1) + cb[nt]];
 #pragma unroll
         for (int mt = 0; mt < MT; ++mt) {
-            const float av = 16 * mt + ln < R ? s_g[r * (R + 1) + 16 * mt + ln] : 0.f;
+            const float av = s_g[r * (R + 1) + ca[mt]];
 #pragma unroll
             for (int nt = 0; nt < NT; ++nt) acc[mt][nt] = mfma4(av, bv[nt], acc[mt][nt]);
 #if !defined(CCMI_DIAG_ARM_NOBIAS) // diagnostic builds only (tools/arm_diag.sh): wrong results
-            accb[mt] = mfma4(av, 1.f, accb[mt]);
+            if constexpr (BIAS) accb[mt] = mfma4(av, 1.f, accb[mt]);
 #endif
         }
     }
@@ -235,6 +245,42 @@ __device__ __forceinline__ void wave_add(float v, float *dst)
 {
     for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
     if ((threadIdx.x & 63) == 0) atomicAdd(dst, v);
+}
+
+// weights of the ARM MLP: wave-uniform scalar loads (the diagnostic build replaces them by
+// constants to bound their cost -- wrong results, tools/arm_diag.sh)
+#if defined(CCMI_DIAG_ARM_NOWLOAD)
+#define ARMW(ptr, idx) (0.001f * (float)((idx) & 7))
+#else
+#define ARMW(ptr, idx) ((ptr)[idx])
+#endif
+// Laplace rate of one latent and its gradients (coolchic.py:419-424, arm.py:262-266):
+// scale = exp(clamp(ls - 4, -4.6, 5)); P = F(q + 1/2) - F(q - 1/2); bits = -log2(max(P, 2^-16)).
+// Returns (through refs) the rate in bits (valid latents) and dL/dq, dL/dmu, dL/dls for the
+// per-latent rate weight lam (0 when P < 2^-16: clamp_min blocks the gradient).
+__device__ __forceinline__ void arm_rate(float q, float mu, float ls, bool valid, float lam, float &rbits, float &g_q,
+                                         float &g_mu, float &g_ls)
+{
+    const float l4 = ls - 4.f, sig = expf(fminf(fmaxf(l4, -4.6f), 5.0f));
+    const float s1 = q + 0.5f - mu, s2 = q - 0.5f - mu;
+    const float sg1 = s1 > 0.f ? 1.f : (s1 < 0.f ? -1.f : 0.f), sg2 = s2 > 0.f ? 1.f : (s2 < 0.f ? -1.f : 0.f);
+    const float F1 = 0.5f - 0.5f * sg1 * expm1f(-fabsf(s1) / sig), F2 = 0.5f - 0.5f * sg2 * expm1f(-fabsf(s2) / sig);
+    const float Pr = F1 - F2;
+    g_q = 0.f, g_mu = 0.f, g_ls = 0.f, rbits = 0.f;
+    if (valid) {
+        rbits = -log2f(fmaxf(Pr, 1.52587890625e-05f));
+        if (Pr >= 1.52587890625e-05f) { // clamp_min passes the gradient where P >= 2^-16
+            const float dLdP = -lam / (Pr * kLn2);
+            const float e1 = expf(-fabsf(s1) / sig), e2 = expf(-fabsf(s2) / sig);
+            // torch autograd of 0.5 - 0.5 sign(s) expm1(-|s|/sig): d/ds = 0.5 sign(s)^2 e / sig
+            const float Fs1 = 0.5f * sg1 * sg1 * e1 / sig, Fs2 = 0.5f * sg2 * sg2 * e2 / sig;
+            const float Fg1 = -0.5f * sg1 * e1 * fabsf(s1) / (sig * sig), Fg2 = -0.5f * sg2 * e2 * fabsf(s2) / (sig * sig);
+            g_q = dLdP * (Fs1 - Fs2);
+            g_mu = -g_q;
+            const float g_sig = dLdP * (Fg1 - Fg2);
+            g_ls = (l4 >= -4.6f && l4 <= 5.0f) ? g_sig * sig : 0.f;
+        }
+    }
 }
 
 template <int D, int NH>
@@ -328,55 +374,42 @@ __global__ __launch_bounds__(kT) __attribute__((amdgpu_waves_per_eu(3))) void t_
             const cfloat_ptr Wl = P + L * (D * D + D);
 #pragma unroll
             for (int j = 0; j < D; ++j) {
-                float z = Wl[D * D + j];
+                float z = ARMW(Wl, D * D + j);
 #pragma unroll
-                for (int i = 0; i < D; ++i) z = fmaf(Wl[j * D + i], xs[L][i], z);
+                for (int i = 0; i < D; ++i) z = fmaf(ARMW(Wl, j * D + i), xs[L][i], z);
                 z += xs[L][j];
                 xs[L + 1][j] = fmaxf(z, 0.f);
             }
         }
         const cfloat_ptr Wo = P + NH * (D * D + D);
-        float mu = Wo[2 * D], ls = Wo[2 * D + 1];
+        float mu = ARMW(Wo, 2 * D), ls = ARMW(Wo, 2 * D + 1);
 #pragma unroll
         for (int i = 0; i < D; ++i) {
-            mu = fmaf(Wo[i], xs[NH][i], mu);
-            ls = fmaf(Wo[D + i], xs[NH][i], ls);
+            mu = fmaf(ARMW(Wo, i), xs[NH][i], mu);
+            ls = fmaf(ARMW(Wo, D + i), xs[NH][i], ls);
         }
-        // scale = exp(clamp(ls - 4, -4.6, 5)) (arm.py:262-266); rate (coolchic.py:419-424)
-        const float l4 = ls - 4.f, sig = expf(fminf(fmaxf(l4, -4.6f), 5.0f));
         const float q = s_y[cy + kAH][cx + kAH];
-        const float s1 = q + 0.5f - mu, s2 = q - 0.5f - mu;
-        const float sg1 = s1 > 0.f ? 1.f : (s1 < 0.f ? -1.f : 0.f), sg2 = s2 > 0.f ? 1.f : (s2 < 0.f ? -1.f : 0.f);
-        const float F1 = 0.5f - 0.5f * sg1 * expm1f(-fabsf(s1) / sig), F2 = 0.5f - 0.5f * sg2 * expm1f(-fabsf(s2) / sig);
-        const float Pr = F1 - F2;
-        float g_q = 0.f, g_mu = 0.f, g_ls = 0.f;
-        if (valid) {
-            const float rbits = -log2f(fmaxf(Pr, 1.52587890625e-05f));
-            rsum += rbits;
+        float g_q, g_mu, g_ls, rbits;
+        {
             const int64_t li = (int64_t)b * g.N + g.off[l] + (int64_t)(y0 + cy) * W + (x0 + cx);
-            if (rate_out) rate_out[li] = rbits;
-            const float lam = grad_rate ? grad_rate[li] : lam_px;
-            if (Pr >= 1.52587890625e-05f) { // clamp_min passes the gradient where P >= 2^-16
-                const float dLdP = -lam / (Pr * kLn2);
-                const float e1 = expf(-fabsf(s1) / sig), e2 = expf(-fabsf(s2) / sig);
-                // torch autograd of 0.5 - 0.5 sign(s) expm1(-|s|/sig): d/ds = 0.5 sign(s)^2 e / sig
-                const float Fs1 = 0.5f * sg1 * sg1 * e1 / sig, Fs2 = 0.5f * sg2 * sg2 * e2 / sig;
-                const float Fg1 = -0.5f * sg1 * e1 * fabsf(s1) / (sig * sig), Fg2 = -0.5f * sg2 * e2 * fabsf(s2) / (sig * sig);
-                g_q = dLdP * (Fs1 - Fs2);
-                g_mu = -g_q;
-                const float g_sig = dLdP * (Fg1 - Fg2);
-                g_ls = (l4 >= -4.6f && l4 <= 5.0f) ? g_sig * sig : 0.f;
+            const float lam = valid && grad_rate ? grad_rate[li] : lam_px;
+            arm_rate(q, mu, ls, valid, lam, rbits, g_q, g_mu, g_ls);
+            if (valid) {
+                rsum += rbits;
+                if (rate_out) rate_out[li] = rbits;
             }
         }
         // ---- backward through the MLP; weight gradients on the matrix cores
         float gx[D];
         {
 #pragma unroll
-            for (int i = 0; i < D; ++i) gx[i] = Wo[i] * g_mu + Wo[D + i] * g_ls;
-            sg[(threadIdx.x & 63) * 3 + 0] = g_mu; // [64][2], pitch 3
+            for (int i = 0; i < D; ++i) gx[i] = ARMW(Wo, i) * g_mu + ARMW(Wo, D + i) * g_ls;
+            sg[(threadIdx.x & 63) * 3 + 0] = g_mu; // [64][2], pitch 3, column 2 zero
             sg[(threadIdx.x & 63) * 3 + 1] = g_ls;
+            sg[(threadIdx.x & 63) * 3 + 2] = 0.f;
 #pragma unroll
             for (int i = 0; i < D; ++i) sa[(threadIdx.x & 63) * (D + 1) + i] = xs[NH][i];
+            sa[(threadIdx.x & 63) * (D + 1) + D] = 0.f;
             wave_lds_sync(); // each wave stages and reads only its own 64 rows
 #if !defined(CCMI_DIAG_ARM_NOOUTER)
             mfma_outer<2, D>(sg, sa, acc_o, accb_o);
@@ -392,8 +425,10 @@ __global__ __launch_bounds__(kT) __attribute__((amdgpu_waves_per_eu(3))) void t_
                 gz[j] = xs[L + 1][j] > 0.f ? gx[j] : 0.f;
                 sg[(threadIdx.x & 63) * (D + 1) + j] = gz[j];
             }
+            sg[(threadIdx.x & 63) * (D + 1) + D] = 0.f;
 #pragma unroll
             for (int i = 0; i < D; ++i) sa[(threadIdx.x & 63) * (D + 1) + i] = xs[L][i];
+            sa[(threadIdx.x & 63) * (D + 1) + D] = 0.f;
             wave_lds_sync();
 #if !defined(CCMI_DIAG_ARM_NOOUTER)
             mfma_outer<D, D>(sg, sa, acc_h[L], accb_h[L]);
@@ -403,7 +438,7 @@ __global__ __launch_bounds__(kT) __attribute__((amdgpu_waves_per_eu(3))) void t_
             for (int i = 0; i < D; ++i) {
                 float a = gz[i]; // residual
 #pragma unroll
-                for (int j = 0; j < D; ++j) a = fmaf(Wl[j * D + i], gz[j], a);
+                for (int j = 0; j < D; ++j) a = fmaf(ARMW(Wl, j * D + i), gz[j], a);
                 gx[i] = a;
             }
         }
@@ -445,6 +480,269 @@ __global__ __launch_bounds__(kT) __attribute__((amdgpu_waves_per_eu(3))) void t_
     flush_outer<2, D>(acc_o, accb_o, G + NH * (D * D + D), G + NH * (D * D + D) + 2 * D);
 #pragma unroll
     for (int L = 0; L < NH; ++L) flush_outer<D, D>(acc_h[L], accb_h[L], G + L * (D * D + D), G + L * (D * D + D) + D * D);
+    wave_add(rsum, &acc4[b * 4 + 1]);
+}
+
+// ARM forward + rate + backward for dim_arm = 16 with the MLP on the matrix cores.
+// A wave owns one 64-latent row of the 4 x 64 tile, as 4 groups of 16 latents.  Each
+// 16 x 16 layer is Z^T = W X^T on v_mfma_f32_16x16x4_f32 (A = W, B = X^T, K = the layer's
+// inputs), with the K order permuted so that input k = 4 (lane >> 4) + s: the accumulator
+// register r of lane l then holds unit 4 (l >> 4) + r of latent l & 15 -- exactly the B
+// operand of the next layer, so activations never leave the registers, and residual, bias
+// and ReLU are elementwise on the accumulators.  The weights (W for the forward, W^T for
+// the input gradients) are 8 VGPRs per layer per lane, loaded ONCE per workgroup (one
+// frame): no per-tile weight loads at all (their scalar-load waits were 37 % of the
+// VALU kernel, tools/arm_diag.sh NOWLOAD).  The 2-wide output layer and the rate are VALU
+// (an M = 2 MFMA would be 8x padding); the rate runs one latent per lane (lane = tile
+// column: group g's values sit in the lanes with lane >> 4 == g).  Weight gradients of the
+// hidden layers: LDS-staged rows on the matrix cores (mfma_outer, K = latents); biases and
+// the output layer's weight gradients: per-lane partial sums over every tile the workgroup
+// visits, reduced once at the end.
+template <int NH>
+__global__ __launch_bounds__(kT) __attribute__((amdgpu_waves_per_eu(3))) void t_arm16(
+    const float *__restrict__ yq, Geo g, ArmTiles at, const float *__restrict__ th, int64_t ps, float lam_px,
+    float *__restrict__ gq, float *__restrict__ gth, int64_t gstride, float *__restrict__ acc4,
+    const float *__restrict__ grad_rate, float *__restrict__ rate_out)
+{
+    constexpr int D = 16, LS = D * D + D, NL = NH > 0 ? NH : 1;
+    __shared__ float s_y[kALH][kALW];
+    __shared__ float s_ga[2 * kT * (D + 1)];
+    float *const s_g = s_ga, *const s_a = s_ga + kT * (D + 1);
+    const int b = blockIdx.y, w = threadIdx.x >> 6, lane = threadIdx.x & 63, ln = lane & 15, lk = lane >> 4;
+    const int cy = w, cx = lane; // per-latent phase: this lane's latent in the tile
+    const cfloat_ptr P = (cfloat_ptr)(size_t)(th + (int64_t)b * ps);
+    float *sg = s_g + 64 * w * (D + 1), *sa = s_a + 64 * w * (D + 1);
+
+    float WA[NL][4], WT[NL][4], BI[NL][4];
+#pragma unroll
+    for (int L = 0; L < NH; ++L)
+#pragma unroll
+        for (int s = 0; s < 4; ++s) {
+            WA[L][s] = P[L * LS + ln * D + 4 * lk + s];   // A = W[j = ln][i = 4 lk + s]
+            WT[L][s] = P[L * LS + (4 * lk + s) * D + ln]; // A = W^T[i = ln][j = 4 lk + s]
+            BI[L][s] = P[L * LS + D * D + 4 * lk + s];    // bias of unit 4 lk + s
+        }
+    const cfloat_ptr Wo = P + NH * LS;
+    float WO0[4], WO1[4];
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+        WO0[r] = Wo[4 * lk + r];
+        WO1[r] = Wo[D + 4 * lk + r];
+    }
+    const float bo0 = Wo[2 * D], bo1 = Wo[2 * D + 1];
+    // s_y offsets of the context inputs k = 4 lk + s
+    int coff[4];
+#pragma unroll
+    for (int s = 0; s < 4; ++s) {
+        int o[4];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            int dy, dx;
+            ctx_off<D>(4 * q + s, dy, dx);
+            o[q] = dy * kALW + dx;
+        }
+        coff[s] = lk == 0 ? o[0] : lk == 1 ? o[1] : lk == 2 ? o[2] : o[3];
+    }
+
+    const v4f z4 = {0.f, 0.f, 0.f, 0.f};
+    v4f acc_h[NL][1][1], accb_dummy[1];
+    float accb[NL][4], accwo0[4], accwo1[4];
+#pragma unroll
+    for (int L = 0; L < NL; ++L) {
+        acc_h[L][0][0] = z4;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) accb[L][r] = 0.f;
+    }
+#pragma unroll
+    for (int r = 0; r < 4; ++r) accwo0[r] = accwo1[r] = 0.f;
+    float accbo0 = 0.f, accbo1 = 0.f, rsum = 0.f;
+
+    constexpr int kSU = (kALH * kALW + kT - 1) / kT;
+    float pre[kSU];
+    auto tile_geo = [&](int t, int &l, int &y0, int &x0) {
+        l = 0;
+#pragma unroll
+        for (int k = 1; k < CCMI_MAX_GRIDS; ++k)
+            if (k < at.n && t >= at.start[k]) l = k;
+        const int lt = t - at.start[l];
+        y0 = (lt / at.tiles_x[l]) * kATY;
+        x0 = (lt % at.tiles_x[l]) * kATX;
+    };
+    auto load_tile = [&](int t) {
+        int l, y0, x0;
+        tile_geo(t, l, y0, x0);
+        const int H = g.h[l], W = g.w[l];
+        const float *src = yq + (int64_t)b * g.N + g.off[l];
+#pragma unroll
+        for (int u = 0; u < kSU; ++u) {
+            const int i = threadIdx.x + u * kT;
+            const int r = i / kALW, c = i - r * kALW;
+            const int y = y0 - kAH + r, x = x0 - kAH + c;
+            pre[u] = (i < kALH * kALW && y >= 0 && y < H && x >= 0 && x < W) ? src[y * W + x] : 0.f;
+        }
+    };
+    const int n_tiles = at.start[at.n];
+    if ((int)blockIdx.x < n_tiles) load_tile(blockIdx.x);
+
+    for (int t = blockIdx.x; t < n_tiles; t += gridDim.x) {
+        int l, y0, x0;
+        tile_geo(t, l, y0, x0);
+        const int H = g.h[l], W = g.w[l];
+        float *gdst = gq + (int64_t)b * g.N + g.off[l];
+        __syncthreads(); // previous tile's LDS readers are done
+#pragma unroll
+        for (int u = 0; u < kSU; ++u) {
+            const int i = threadIdx.x + u * kT;
+            if (i < kALH * kALW) (&s_y[0][0])[i] = pre[u];
+        }
+        if (t + (int)gridDim.x < n_tiles) load_tile(t + gridDim.x);
+        __syncthreads();
+        const bool valid = (y0 + cy) < H && (x0 + cx) < W;
+
+        // ---- forward: X[L][g][r] = input / activation unit 4 lk + r of latent 16 g + ln
+        const float *yrow = &s_y[cy + kAH][kAH + ln];
+        float X[NH + 1][4][4];
+#pragma unroll
+        for (int gg = 0; gg < 4; ++gg)
+#pragma unroll
+            for (int s = 0; s < 4; ++s) X[0][gg][s] = yrow[16 * gg + coff[s]];
+#pragma unroll
+        for (int L = 0; L < NH; ++L)
+#pragma unroll
+            for (int gg = 0; gg < 4; ++gg) {
+                v4f acc = {BI[L][0], BI[L][1], BI[L][2], BI[L][3]};
+#pragma unroll
+                for (int s = 0; s < 4; ++s) acc = mfma4(WA[L][s], X[L][gg][s], acc);
+#pragma unroll
+                for (int r = 0; r < 4; ++r) X[L + 1][gg][r] = fmaxf(acc[r] + X[L][gg][r], 0.f);
+            }
+        // output layer: partial dot products over this lane's 4 units, summed over the 4
+        // lanes of the latent; group g's (mu, ls) kept by the lanes with lk == g
+        float mu = 0.f, ls = 0.f;
+#pragma unroll
+        for (int gg = 0; gg < 4; ++gg) {
+            float pm = 0.f, pl = 0.f;
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                pm = fmaf(WO0[r], X[NH][gg][r], pm);
+                pl = fmaf(WO1[r], X[NH][gg][r], pl);
+            }
+            pm += __shfl_xor(pm, 16);
+            pl += __shfl_xor(pl, 16);
+            pm += __shfl_xor(pm, 32);
+            pl += __shfl_xor(pl, 32);
+            if (gg == lk) {
+                mu = pm + bo0;
+                ls = pl + bo1;
+            }
+        }
+        // ---- rate, one latent per lane
+        const float q = s_y[cy + kAH][cx + kAH];
+        float g_q, g_mu, g_ls, rbits;
+        {
+            const int64_t li = (int64_t)b * g.N + g.off[l] + (int64_t)(y0 + cy) * W + (x0 + cx);
+            const float lam = valid && grad_rate ? grad_rate[li] : lam_px;
+            arm_rate(q, mu, ls, valid, lam, rbits, g_q, g_mu, g_ls);
+            if (valid) {
+                rsum += rbits;
+                if (rate_out) rate_out[li] = rbits;
+            }
+        }
+        accbo0 += g_mu;
+        accbo1 += g_ls;
+        // ---- backward: output layer (VALU), its weight gradients as per-lane partial sums
+        float G[4][4];
+#pragma unroll
+        for (int gg = 0; gg < 4; ++gg) {
+            const float gm = __shfl(g_mu, 16 * gg + ln), gl = __shfl(g_ls, 16 * gg + ln);
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                G[gg][r] = WO0[r] * gm + WO1[r] * gl;
+                accwo0[r] = fmaf(gm, X[NH][gg][r], accwo0[r]);
+                accwo1[r] = fmaf(gl, X[NH][gg][r], accwo1[r]);
+            }
+        }
+        // hidden layers
+#pragma unroll
+        for (int L = NH - 1; L >= 0; --L) {
+            float gz[4][4];
+#pragma unroll
+            for (int gg = 0; gg < 4; ++gg)
+#pragma unroll
+                for (int r = 0; r < 4; ++r) {
+                    gz[gg][r] = X[L + 1][gg][r] > 0.f ? G[gg][r] : 0.f;
+                    sg[(16 * gg + ln) * (D + 1) + 4 * lk + r] = gz[gg][r];
+                    // layer 0's input is the context, re-read from the tile (not kept live)
+                    sa[(16 * gg + ln) * (D + 1) + 4 * lk + r] = L == 0 ? yrow[16 * gg + coff[r]] : X[L][gg][r];
+                }
+#pragma unroll
+            for (int r = 0; r < 4; ++r) accb[L][r] += (gz[0][r] + gz[1][r]) + (gz[2][r] + gz[3][r]);
+            wave_lds_sync(); // each wave stages and reads only its own 64 rows
+            mfma_outer<D, D, false>(sg, sa, acc_h[L], accb_dummy);
+            wave_lds_sync();
+            // input gradient: W^T gz + gz (residual), K permuted like the forward
+#pragma unroll
+            for (int gg = 0; gg < 4; ++gg) {
+                v4f acc = {gz[gg][0], gz[gg][1], gz[gg][2], gz[gg][3]};
+#pragma unroll
+                for (int s = 0; s < 4; ++s) acc = mfma4(WT[L][s], gz[gg][s], acc);
+#pragma unroll
+                for (int r = 0; r < 4; ++r) G[gg][r] = acc[r];
+            }
+        }
+        // ---- context gradients (input k = 4 lk + r of latent 16 g + ln) and the latent's own
+        // gradient to this wave's rows of s_g, then the gather of t_arm
+#pragma unroll
+        for (int gg = 0; gg < 4; ++gg)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) sg[(16 * gg + ln) * (D + 1) + 4 * lk + r] = G[gg][r];
+        sg[lane * (D + 1) + D] = g_q;
+        __syncthreads();
+#pragma unroll 1
+        for (int i = threadIdx.x; i < (kALH - 1) * kALW; i += kT) {
+            const int r = 1 + i / kALW, c = i - (r - 1) * kALW;
+            const int y = y0 - kAH + r, x = x0 - kAH + c;
+            float v = 0.f;
+            {
+                const int ly = r - kAH, lx = c - kAH;
+                if (ly >= 0 && lx >= 0 && lx < kATX) v = s_g[(ly * kATX + lx) * (D + 1) + D];
+            }
+#pragma unroll
+            for (int k = 0; k < D; ++k) {
+                int dy, dx;
+                ctx_off<D>(k, dy, dx);
+                const int ly = r - kAH - dy, lx = c - kAH - dx;
+                if (ly >= 0 && ly < kATY && lx >= 0 && lx < kATX) v += s_g[(ly * kATX + lx) * (D + 1) + k];
+            }
+            if (y >= 0 && y < H && x >= 0 && x < W && v != 0.f) atomicAdd(&gdst[y * W + x], v);
+        }
+    }
+    // ---- flush
+    float *Gp = gth + (int64_t)b * gstride;
+#pragma unroll
+    for (int L = 0; L < NH; ++L) {
+#pragma unroll
+        for (int r = 0; r < 4; ++r) { // dW_L[m = 4 lk + r][n = ln]
+            atomicAdd(&Gp[L * LS + (4 * lk + r) * D + ln], acc_h[L][0][0][r]);
+            float v = accb[L][r];
+            for (int o = 1; o < 16; o <<= 1) v += __shfl_xor(v, o);
+            if (ln == 0) atomicAdd(&Gp[L * LS + D * D + 4 * lk + r], v);
+        }
+    }
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+        float v0 = accwo0[r], v1 = accwo1[r];
+        for (int o = 1; o < 16; o <<= 1) {
+            v0 += __shfl_xor(v0, o);
+            v1 += __shfl_xor(v1, o);
+        }
+        if (ln == 0) {
+            atomicAdd(&Gp[NH * LS + 4 * lk + r], v0);
+            atomicAdd(&Gp[NH * LS + D + 4 * lk + r], v1);
+        }
+    }
+    wave_add(accbo0, &Gp[NH * LS + 2 * D]);
+    wave_add(accbo1, &Gp[NH * LS + 2 * D + 1]);
     wave_add(rsum, &acc4[b * 4 + 1]);
 }
 
@@ -1329,6 +1627,19 @@ int launch_arm_d(int nh, dim3 grid, hipStream_t s, const float *yq, const Geo &g
                  int64_t ps, float lam_px, float *gq, float *gth, int64_t gstride, float *acc4, const float *grate,
                  float *rate_out)
 {
+    if constexpr (D == 16) {
+        // the matrix-core ARM (t_arm16); CCMI_ARM_VALU=1 keeps the VALU kernel (A/B runs)
+        static const bool valu = getenv("CCMI_ARM_VALU") != nullptr;
+        if (!valu) {
+            switch (nh) {
+            case 0: hipLaunchKernelGGL((t_arm16<0>), grid, dim3(kT), 0, s, yq, g, at, th, ps, lam_px, gq, gth, gstride, acc4, grate, rate_out); break;
+            case 1: hipLaunchKernelGGL((t_arm16<1>), grid, dim3(kT), 0, s, yq, g, at, th, ps, lam_px, gq, gth, gstride, acc4, grate, rate_out); break;
+            case 2: hipLaunchKernelGGL((t_arm16<2>), grid, dim3(kT), 0, s, yq, g, at, th, ps, lam_px, gq, gth, gstride, acc4, grate, rate_out); break;
+            default: hipLaunchKernelGGL((t_arm16<3>), grid, dim3(kT), 0, s, yq, g, at, th, ps, lam_px, gq, gth, gstride, acc4, grate, rate_out); break;
+            }
+            return CCMI_OK;
+        }
+    }
     switch (nh) {
     case 0: hipLaunchKernelGGL((t_arm<D, 0>), grid, dim3(kT), 0, s, yq, g, at, th, ps, lam_px, gq, gth, gstride, acc4, grate, rate_out); break;
     case 1: hipLaunchKernelGGL((t_arm<D, 1>), grid, dim3(kT), 0, s, yq, g, at, th, ps, lam_px, gq, gth, gstride, acc4, grate, rate_out); break;
