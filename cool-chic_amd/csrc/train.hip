@@ -499,7 +499,10 @@ __global__ __launch_bounds__(kT) __attribute__((amdgpu_waves_per_eu(3))) void t_
 // the output layer's weight gradients: per-lane partial sums over every tile the workgroup
 // visits, reduced once at the end.
 template <int NH>
-__global__ __launch_bounds__(kT) __attribute__((amdgpu_waves_per_eu(3))) void t_arm16(
+#ifndef CCMI_ARM16_WAVES
+#define CCMI_ARM16_WAVES 3
+#endif
+__global__ __launch_bounds__(kT) __attribute__((amdgpu_waves_per_eu(CCMI_ARM16_WAVES))) void t_arm16(
     const float *__restrict__ yq, Geo g, ArmTiles at, const float *__restrict__ th, int64_t ps, float lam_px,
     float *__restrict__ gq, float *__restrict__ gth, int64_t gstride, float *__restrict__ acc4,
     const float *__restrict__ grad_rate, float *__restrict__ rate_out)
@@ -768,23 +771,40 @@ template <int CIN>
 __global__ __launch_bounds__(kT) void t_head_fwd(const float *__restrict__ dense, Geo g, const float *__restrict__ th,
                                                  int64_t ps, float *__restrict__ z0)
 {
-    const int b = blockIdx.y;
+    // hidden unit j as one LDS record w0[j][0..CIN), b0[j], w1[0..3)[j] (broadcast reads, as
+    // t_head_bwd; scalar loads of the weights in the unit loop stalled on their waits)
+    __shared__ __attribute__((aligned(16))) float s_rec[64][12];
+    static_assert(CIN + 4 <= 12, "hidden-unit record");
+    const int b = blockIdx.y, hid = g.hid;
+    const cfloat_ptr P = (cfloat_ptr)(size_t)(th + (int64_t)b * ps);
+    for (int e = threadIdx.x; e < 64 * 12; e += kT) {
+        const int j = e / 12, f = e - j * 12;
+        float v = 0.f;
+        if (j < hid) {
+            if (f < CIN) v = P[g.w0 + j * CIN + f];
+            else if (f == CIN) v = P[g.b0 + j];
+            else if (f <= CIN + 3) v = P[g.w1 + (f - CIN - 1) * hid + j];
+        }
+        s_rec[j][f] = v;
+    }
+    __syncthreads();
     const int64_t npx = (int64_t)g.H * g.W, p = (int64_t)blockIdx.x * kT + threadIdx.x;
     if (p >= npx) return;
-    const cfloat_ptr P = (cfloat_ptr)(size_t)(th + (int64_t)b * ps);
     const float *x = dense + (int64_t)b * CIN * npx + p;
     float xv[CIN];
 #pragma unroll
     for (int i = 0; i < CIN; ++i) xv[i] = x[i * npx];
     float o0 = P[g.b1], o1 = P[g.b1 + 1], o2 = P[g.b1 + 2];
-    for (int j = 0; j < g.hid; ++j) {
-        float h = P[g.b0 + j];
+#pragma unroll 4
+    for (int j = 0; j < hid; ++j) {
+        const float *r = s_rec[j];
+        float h = r[CIN];
 #pragma unroll
-        for (int i = 0; i < CIN; ++i) h = fmaf(P[g.w0 + j * CIN + i], xv[i], h);
+        for (int i = 0; i < CIN; ++i) h = fmaf(r[i], xv[i], h);
         if (g.r0) h = fmaxf(h, 0.f);
-        o0 = fmaf(P[g.w1 + j], h, o0);
-        o1 = fmaf(P[g.w1 + g.hid + j], h, o1);
-        o2 = fmaf(P[g.w1 + 2 * g.hid + j], h, o2);
+        o0 = fmaf(r[CIN + 1], h, o0);
+        o1 = fmaf(r[CIN + 2], h, o1);
+        o2 = fmaf(r[CIN + 3], h, o2);
     }
     if (g.r1) {
         o0 = fmaxf(o0, 0.f);
@@ -836,12 +856,15 @@ __global__ __launch_bounds__(kT) void t_loss(const float *__restrict__ raw, Geo 
 {
     __shared__ float s_red[8];
     const int b = blockIdx.y;
-    const int64_t npx = (int64_t)g.H * g.W, p = (int64_t)blockIdx.x * kT + threadIdx.x;
+    const int64_t npx = (int64_t)g.H * g.W;
     const int h2 = g.H / 2, w2 = g.W / 2;
     const float total = yuv420 ? (float)(npx + 2 * (int64_t)h2 * w2) : (float)(3 * npx);
     const float k2 = 2.f / total;
     float se = 0.f;
-    if (p < npx) {
+    // grid-stride: a few hundred workgroups per frame, so the per-workgroup atomic on the
+    // frame's one loss slot stays cheap (one workgroup per 256 pixels serialised ~1,500
+    // same-address atomics per frame: 124 us per 8-frame 512x768 iteration)
+    for (int64_t p = (int64_t)blockIdx.x * kT + threadIdx.x; p < npx; p += (int64_t)gridDim.x * kT) {
         const int py = (int)(p / g.W), px = (int)(p - (int64_t)py * g.W);
         const float *o = raw + (int64_t)b * 3 * npx + p;
         const float *T = tgt + (int64_t)b * tstride;
@@ -1810,7 +1833,7 @@ extern "C" int ccmi_train_step(const ccmi_train_args *a, void *stream)
     if (a->grad_raw) // the caller's d loss / d raw output (autograd); no built-in MSE term
         CCMI_HIP_CHECK(hipMemcpyAsync(graw, a->grad_raw, sizeof(float) * 3 * npx * B, hipMemcpyDeviceToDevice, s));
     else
-        hipLaunchKernelGGL(t_loss, grid1(npx, B), dim3(kT), 0, s, F(pl.z[g.n_sp]), g, a->target, a->target_stride,
+        hipLaunchKernelGGL(t_loss, dim3(std::min(grid1(npx, B).x, 256u), B), dim3(kT), 0, s, F(pl.z[g.n_sp]), g, a->target, a->target_stride,
                            a->yuv420, graw, acc4);
 
     // ---- synthesis backward
