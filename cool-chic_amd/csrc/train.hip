@@ -1212,9 +1212,9 @@ __global__ void t_ref_u(const float *__restrict__ X, int64_t xs, int h, int w, c
                         int koff, int Kp, float *__restrict__ U, int64_t us)
 {
     const int b = blockIdx.y;
-    const int64_t n = (int64_t)h * w, i = (int64_t)blockIdx.x * kT + threadIdx.x;
+    const int n = h * w, i = blockIdx.x * kT + threadIdx.x;
     if (i >= n) return;
-    const int r = (int)(i / w), x = (int)(i - (int64_t)r * w), P = Kp / 2;
+    const int r = i / w, x = i - r * w, P = Kp / 2;
     const float *wk = kf + (int64_t)b * kstride + koff, *src = X + (int64_t)b * xs + (int64_t)r * w;
     float a = 0.f;
     for (int k = 0; k < Kp; ++k) {
@@ -1229,11 +1229,11 @@ __global__ void t_ref_gu(const float *__restrict__ GY, int64_t gys, int h, int w
                          int kstride, int koff, int Kp, float *__restrict__ GU, int64_t us)
 {
     const int b = blockIdx.y;
-    const int64_t n = (int64_t)h * w, i = (int64_t)blockIdx.x * kT + threadIdx.x;
+    const int n = h * w, i = blockIdx.x * kT + threadIdx.x;
     if (i >= n) return;
     const int P = Kp / 2;
     const float *wk = kf + (int64_t)b * kstride + koff;
-    const int r = (int)(i / w), x = (int)(i - (int64_t)r * w);
+    const int r = i / w, x = i - r * w;
     const float *gy = GY + (int64_t)b * gys;
     float a = 0.f;
     for (int k = 0; k < Kp; ++k) {
@@ -1249,11 +1249,11 @@ __global__ void t_ref_gx(const float *__restrict__ GU, int64_t us, const float *
                          int64_t gxs)
 {
     const int b = blockIdx.y;
-    const int64_t n = (int64_t)h * w, i = (int64_t)blockIdx.x * kT + threadIdx.x;
+    const int n = h * w, i = blockIdx.x * kT + threadIdx.x;
     if (i >= n) return;
     const int P = Kp / 2;
     const float *wk = kf + (int64_t)b * kstride + koff;
-    const int r = (int)(i / w), m = (int)(i - (int64_t)r * w);
+    const int r = i / w, m = i - r * w;
     const float *gu = GU + (int64_t)b * us + (int64_t)r * w;
     float a = GY[(int64_t)b * gys + i];
     for (int k = 0; k < Kp; ++k) {
@@ -1301,7 +1301,7 @@ __global__ __launch_bounds__(kT) void t_ref_dw(const float *__restrict__ GY, int
 #pragma unroll
     for (int k = 0; k < KP; ++k) dw[k] = 0.f;
     for (int64_t i = (int64_t)blockIdx.x * kT + threadIdx.x; i < n; i += (int64_t)gridDim.x * kT) {
-        const int r = (int)(i / w), c = (int)(i - (int64_t)r * w);
+        const int r = (int)i / w, c = (int)i - r * w;
         const float gv = gy[i], guv = gu[i];
 #pragma unroll
         for (int k = 0; k < KP; ++k) {
@@ -1320,10 +1320,9 @@ __global__ void t_up_u(const float *__restrict__ S, int64_t ss, UpLevel A, const
                        int koff, float *__restrict__ U, int64_t us)
 {
     const int b = blockIdx.y;
-    const int64_t n = (int64_t)A.C * A.hs * A.wd, i = (int64_t)blockIdx.x * kT + threadIdx.x;
+    const int n = A.C * A.hs * A.wd, i = blockIdx.x * kT + threadIdx.x;
     if (i >= n) return;
-    const int xd = (int)(i % A.wd);
-    const int64_t cr = i / A.wd; // c * hs + r
+    const int cr = i / A.wd, xd = i - cr * A.wd; // cr = c * hs + r
     const float *wk = kf + (int64_t)b * kstride + koff, *src = S + (int64_t)b * ss + cr * A.ws;
     const int j = xd >> 1, a = xd & 1;
     float acc = 0.f;
@@ -1339,11 +1338,10 @@ __global__ void t_up_gu(const float *__restrict__ GY, int64_t gys, UpLevel A, co
                         int koff, float *__restrict__ GU, int64_t us)
 {
     const int b = blockIdx.y;
-    const int64_t n = (int64_t)A.C * A.hs * A.wd, i = (int64_t)blockIdx.x * kT + threadIdx.x;
+    const int n = A.C * A.hs * A.wd, i = blockIdx.x * kT + threadIdx.x;
     if (i >= n) return;
-    const int xd = (int)(i % A.wd);
-    const int64_t cr = i / A.wd;
-    const int c = (int)(cr / A.hs), r = (int)(cr - (int64_t)c * A.hs);
+    const int cr = i / A.wd, xd = i - cr * A.wd;
+    const int c = cr / A.hs, r = cr - c * A.hs;
     const float *wk = kf + (int64_t)b * kstride + koff;
     const float *gy = GY + (int64_t)b * gys + (int64_t)(c + 1) * A.hd * A.wd + xd; // channel c+1 of the dest stack
     const int nj = (A.hd + 1) >> 1;
@@ -1368,10 +1366,9 @@ __global__ void t_up_gs(const float *__restrict__ GU, int64_t us, UpLevel A, con
                         int koff, float *__restrict__ GS, int64_t gss, int accumulate)
 {
     const int b = blockIdx.y;
-    const int64_t n = (int64_t)A.C * A.hs * A.ws, i = (int64_t)blockIdx.x * kT + threadIdx.x;
+    const int n = A.C * A.hs * A.ws, i = blockIdx.x * kT + threadIdx.x;
     if (i >= n) return;
-    const int m = (int)(i % A.ws);
-    const int64_t cr = i / A.ws;
+    const int cr = i / A.ws, m = i - cr * A.ws;
     const float *wk = kf + (int64_t)b * kstride + koff;
     const float *gu = GU + (int64_t)b * us + cr * A.wd;
     const int nj = (A.wd + 1) >> 1;
@@ -1410,9 +1407,8 @@ __global__ __launch_bounds__(kT) void t_up_dw(const float *__restrict__ GY, int6
     const float *sb = S + (int64_t)b * ss;
     const int64_t nv = (int64_t)A.C * njy * A.wd;
     for (int64_t i = (int64_t)blockIdx.x * kT + threadIdx.x; i < nv; i += (int64_t)gridDim.x * kT) {
-        const int xd = (int)(i % A.wd);
-        const int64_t cj = i / A.wd;
-        const int c = (int)(cj / njy), j = (int)(cj - (int64_t)c * njy);
+        const int cj = (int)i / A.wd, xd = (int)i - cj * A.wd;
+        const int c = cj / njy, j = cj - c * njy;
         const float *gy = gyb + (int64_t)(c + 1) * A.hd * A.wd + xd;
         const float ge = gy[(int64_t)(2 * j) * A.wd];
         const float go = 2 * j + 1 < A.hd ? gy[(int64_t)(2 * j + 1) * A.wd] : 0.f;
@@ -1427,8 +1423,7 @@ __global__ __launch_bounds__(kT) void t_up_dw(const float *__restrict__ GY, int6
     }
     const int64_t nh = (int64_t)A.C * A.hs * njx;
     for (int64_t i = (int64_t)blockIdx.x * kT + threadIdx.x; i < nh; i += (int64_t)gridDim.x * kT) {
-        const int j = (int)(i % njx);
-        const int64_t cr = i / njx;
+        const int cr = (int)i / njx, j = (int)i - cr * njx;
         const float *gu = gub + cr * A.wd;
         const float ge = gu[2 * j];
         const float go = 2 * j + 1 < A.wd ? gu[2 * j + 1] : 0.f;
@@ -1915,7 +1910,7 @@ extern "C" int ccmi_train_step(const ccmi_train_args *a, void *stream)
 
     // ---- latent gradients, norm, Adam
     hipLaunchKernelGGL(t_latgrad, grid1(g.N, B), dim3(kT), 0, s, gq, dq, g.N, G, GS);
-    hipLaunchKernelGGL(t_sumsq, dim3((unsigned)std::min<int64_t>(ccmi_div_up((int)std::min<int64_t>(GS, 1 << 30), kT), 512), B),
+    hipLaunchKernelGGL(t_sumsq, dim3((unsigned)std::min<int64_t>(ccmi_div_up((int)std::min<int64_t>(GS, 1 << 30), kT), 64), B),
                        dim3(kT), 0, s, G, GS, GS, acc4);
     const float total = a->yuv420 ? (float)(npx + 2 * (int64_t)(g.H / 2) * (g.W / 2)) : (float)(3 * npx);
     if (a->loss_out) hipLaunchKernelGGL(t_finish, dim3(1), dim3(std::max(64, B)), 0, s, acc4, 1.f / total, lam_px, a->loss_out, B);
