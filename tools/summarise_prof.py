@@ -11,6 +11,7 @@ usage: python tools/summarise_prof.py gpurun_out/prof_r1 r1 [frames_per_launch=8
 """
 
 import csv
+import re
 import json
 import shutil
 import sys
@@ -36,7 +37,7 @@ def find(src: Path, dirs, suffix: str) -> Path:
 
 def stage_of(name: str):
     # the fused decode tail: syn_fused_kernel<CIN, CMID, true> ("Lb1E" in the mangled name)
-    if "syn_fused_kernel" in name and ("Lb1E" in name or "true>" in name):
+    if "syn_fused_kernel" in name and ("Lb1E" in name or re.search(r"syn_fused_kernel<\d+, \d+, true", name)):
         return "decode_fused"
     for k, v in STAGES.items():
         if k in name:
