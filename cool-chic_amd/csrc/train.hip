@@ -1055,6 +1055,18 @@ __global__ __launch_bounds__(kT) void t_sp_bwd(const float *__restrict__ gout, c
 // and feeds 4 pixels per MFMA (K = lane >> 4).  Accumulators live in registers across
 // every pixel chunk the workgroup visits (grid-stride) and are flushed once, with one
 // atomic per weight per wave.
+// diagnostic builds (tools/arm_diag.sh; wrong results, timing only): NOREC replaces the LDS
+// weight records by constants, NOHMFMA drops the weight-gradient MFMAs
+#if defined(CCMI_DIAG_ARM_NOREC)
+#define HEAD_BWD_REC(r, j) const float r[12] = {0.01f, 0.02f, 0.03f, 0.01f, 0.02f, 0.03f, 0.01f, 0.02f, 0.03f, 0.01f, 0.02f, 0.03f}
+#else
+#define HEAD_BWD_REC(r, j) const float *r = s_rec[j]
+#endif
+#if defined(CCMI_DIAG_ARM_NOHMFMA)
+#define HEAD_MFMA(a, b, c) (c)
+#else
+#define HEAD_MFMA(a, b, c) mfma4(a, b, c)
+#endif
 template <int CIN, int NT>
 __global__ __launch_bounds__(kHeadT) void t_head_bwd(const float *__restrict__ dense, const float *__restrict__ gz0, Geo g,
                                                      const float *__restrict__ th, int64_t ps, float *__restrict__ gdense,
@@ -1111,7 +1123,7 @@ __global__ __launch_bounds__(kHeadT) void t_head_bwd(const float *__restrict__ d
         float o0 = bo0, o1 = bo1, o2 = bo2;
 #pragma unroll 4
         for (int j = 0; j < hid; ++j) {
-            const float *r = s_rec[j];
+            HEAD_BWD_REC(r, j);
             float a = r[CIN];
 #pragma unroll
             for (int i = 0; i < CIN; ++i) a = fmaf(r[i], xv[i], a);
@@ -1138,7 +1150,7 @@ __global__ __launch_bounds__(kHeadT) void t_head_bwd(const float *__restrict__ d
             const int px = 4 * s + lk;
             const float a = sw[px * 4 + ia];
 #pragma unroll
-            for (int q = 0; q < NT; ++q) a1[q] = mfma4(a, sv[px * hp + 16 * q + ln], a1[q]);
+            for (int q = 0; q < NT; ++q) a1[q] = HEAD_MFMA(a, sv[px * hp + 16 * q + ln], a1[q]);
         }
         wave_lds_sync();
         // ---- g_h (replaces h in this lane's row), g_x
@@ -1147,7 +1159,7 @@ __global__ __launch_bounds__(kHeadT) void t_head_bwd(const float *__restrict__ d
         for (int i = 0; i < CIN; ++i) gxv[i] = 0.f;
 #pragma unroll 4
         for (int j = 0; j < hid; ++j) {
-            const float *r = s_rec[j];
+            HEAD_BWD_REC(r, j);
             float gh = r[CIN + 1] * gp1[0] + r[CIN + 2] * gp1[1] + r[CIN + 3] * gp1[2];
             if (g.r0 && sv[lane * hp + j] <= 0.f) gh = 0.f;
             sv[lane * hp + j] = gh;
@@ -1170,7 +1182,7 @@ __global__ __launch_bounds__(kHeadT) void t_head_bwd(const float *__restrict__ d
             const int px = 4 * s + lk;
             const float bb = sw[px * kXP + ib];
 #pragma unroll
-            for (int q = 0; q < NT; ++q) a0[q] = mfma4(sv[px * hp + 16 * q + ln], bb, a0[q]);
+            for (int q = 0; q < NT; ++q) a0[q] = HEAD_MFMA(sv[px * hp + 16 * q + ln], bb, a0[q]);
         }
         wave_lds_sync();
     }
