@@ -1277,6 +1277,23 @@ __global__ void t_ref_gx(const float *__restrict__ GU, int64_t us, const float *
 
 // Sum of per-thread tap gradients over the workgroup, folded onto the symmetric half
 // kernel (upsampling.py:46-68): one atomic per half tap per workgroup.
+// Upsampling kernel gradients: each workgroup of a t_*_dw reduction adds its taps into one
+// of kDwSlots copies of the frame's upsampling-parameter gradients (slot = workgroup %
+// kDwSlots), so the big levels can use many workgroups without serialising on one
+// address; t_dw_fold sums the slots into the gradient row once per step.
+constexpr int kDwSlots = 32;
+
+__global__ void t_dw_fold(const float *__restrict__ slots, int nreg, float *__restrict__ gth, int64_t gstride, int off)
+{
+    const int b = blockIdx.y, e = blockIdx.x * blockDim.x + threadIdx.x;
+    if (e >= nreg) return;
+    const float *sl = slots + (int64_t)b * kDwSlots * nreg + e;
+    float v = 0.f;
+#pragma unroll 8
+    for (int k = 0; k < kDwSlots; ++k) v += sl[(int64_t)k * nreg];
+    gth[(int64_t)b * gstride + off + e] += v;
+}
+
 template <int K>
 __device__ __forceinline__ void reduce_taps(float (&dw)[K], float *__restrict__ dst)
 {
@@ -1322,7 +1339,7 @@ __global__ __launch_bounds__(kT) void t_ref_dw(const float *__restrict__ GY, int
             if (cx >= 0 && cx < w) dw[k] = fmaf(guv, x[(int64_t)r * w + cx], dw[k]);
         }
     }
-    reduce_taps<KP>(dw, gth + (int64_t)b * gstride + hoff);
+    reduce_taps<KP>(dw, gth + ((int64_t)b * kDwSlots + blockIdx.x % kDwSlots) * gstride + hoff);
 }
 
 __device__ __forceinline__ int up_tap(int a, int d, int K) { return a + K / 2 - 1 - 2 * d; }
@@ -1404,6 +1421,94 @@ __global__ void t_up_gs(const float *__restrict__ GU, int64_t us, UpLevel A, con
 // upsample kernel gradient: vertical taps over destination row pairs (c, j, xd),
 // horizontal taps over destination column pairs (c, r, j); taps are compile-time per
 // parity: destination 2j + a, source offset d -> tap a + K/2 - 1 - 2d.
+// Compile-time-tap forms of the two upsampling adjoints for the reference's 8-tap kernel:
+// interior rows / columns (every source tap inside the stack, no clamping) take a fixed
+// unrolled sum in the generic kernel's summation order (d ascending, then parity), the
+// borders fall back to the generic loops -- same results, no runtime tap loops.
+template <int K>
+__global__ void t_up_gu_k(const float *__restrict__ GY, int64_t gys, UpLevel A, const float *__restrict__ kf, int kstride,
+                          int koff, float *__restrict__ GU, int64_t us)
+{
+    constexpr int K2 = K / 2, DLO = -((K2 + 1) / 2), DHI = K2 / 2;
+    const int b = blockIdx.y;
+    const int n = A.C * A.hs * A.wd, i = blockIdx.x * kT + threadIdx.x;
+    if (i >= n) return;
+    const int cr = i / A.wd, xd = i - cr * A.wd;
+    const int c = cr / A.hs, r = cr - c * A.hs;
+    const float *wk = kf + (int64_t)b * kstride + koff;
+    float w[K];
+#pragma unroll
+    for (int t = 0; t < K; ++t) w[t] = wk[t];
+    const float *gy = GY + (int64_t)b * gys + (int64_t)(c + 1) * A.hd * A.wd + xd;
+    const int nj = (A.hd + 1) >> 1;
+    float acc = 0.f;
+    if (r >= 1 && r <= A.hs - 2 && r - DHI >= 0 && r - DLO <= nj - 1 && 2 * (r - DLO) + 1 < A.hd) {
+#pragma unroll
+        for (int d = DLO; d <= DHI; ++d)
+#pragma unroll
+            for (int a = 0; a < 2; ++a) {
+                const int t = a + K2 - 1 - 2 * d;
+                if (t >= 0 && t < K) acc = fmaf(w[t], gy[(int64_t)(2 * (r - d) + a) * A.wd], acc);
+            }
+    } else {
+        for (int d = DLO; d <= DHI; ++d) {
+            int jlo = r == 0 ? 0 : r - d, jhi = r == A.hs - 1 ? nj - 1 : r - d;
+            jlo = max(jlo, 0);
+            jhi = min(jhi, nj - 1);
+            for (int j = jlo; j <= jhi; ++j) {
+                if (clampi(j + d, A.hs - 1) != r) continue;
+                for (int a = 0; a < 2; ++a) {
+                    const int yd = 2 * j + a, t = up_tap(a, d, K);
+                    if (yd < A.hd && t >= 0 && t < K) acc = fmaf(w[t], gy[(int64_t)yd * A.wd], acc);
+                }
+            }
+        }
+    }
+    GU[(int64_t)b * us + i] = acc;
+}
+
+template <int K>
+__global__ void t_up_gs_k(const float *__restrict__ GU, int64_t us, UpLevel A, const float *__restrict__ kf, int kstride,
+                          int koff, float *__restrict__ GS, int64_t gss, int accumulate)
+{
+    constexpr int K2 = K / 2, DLO = -((K2 + 1) / 2), DHI = K2 / 2;
+    const int b = blockIdx.y;
+    const int n = A.C * A.hs * A.ws, i = blockIdx.x * kT + threadIdx.x;
+    if (i >= n) return;
+    const int cr = i / A.ws, m = i - cr * A.ws;
+    const float *wk = kf + (int64_t)b * kstride + koff;
+    float w[K];
+#pragma unroll
+    for (int t = 0; t < K; ++t) w[t] = wk[t];
+    const float *gu = GU + (int64_t)b * us + cr * A.wd;
+    const int nj = (A.wd + 1) >> 1;
+    float acc = 0.f;
+    if (m >= 1 && m <= A.ws - 2 && m - DHI >= 0 && m - DLO <= nj - 1 && 2 * (m - DLO) + 1 < A.wd) {
+#pragma unroll
+        for (int d = DLO; d <= DHI; ++d)
+#pragma unroll
+            for (int a = 0; a < 2; ++a) {
+                const int t = a + K2 - 1 - 2 * d;
+                if (t >= 0 && t < K) acc = fmaf(w[t], gu[2 * (m - d) + a], acc);
+            }
+    } else {
+        for (int d = DLO; d <= DHI; ++d) {
+            int jlo = m == 0 ? 0 : m - d, jhi = m == A.ws - 1 ? nj - 1 : m - d;
+            jlo = max(jlo, 0);
+            jhi = min(jhi, nj - 1);
+            for (int j = jlo; j <= jhi; ++j) {
+                if (clampi(j + d, A.ws - 1) != m) continue;
+                for (int a = 0; a < 2; ++a) {
+                    const int xd = 2 * j + a, t = up_tap(a, d, K);
+                    if (xd < A.wd && t >= 0 && t < K) acc = fmaf(w[t], gu[xd], acc);
+                }
+            }
+        }
+    }
+    float *o = GS + (int64_t)b * gss + i;
+    *o = accumulate ? *o + acc : acc;
+}
+
 template <int K>
 __global__ __launch_bounds__(kT) void t_up_dw(const float *__restrict__ GY, int64_t gys, const float *__restrict__ U,
                                               const float *__restrict__ GU, int64_t us, const float *__restrict__ S,
@@ -1448,7 +1553,7 @@ __global__ __launch_bounds__(kT) void t_up_dw(const float *__restrict__ GY, int6
             if (to >= 0 && to < K) dw[to] = fmaf(go, sv, dw[to]);
         }
     }
-    reduce_taps<K>(dw, gth + (int64_t)b * gstride + hoff);
+    reduce_taps<K>(dw, gth + ((int64_t)b * kDwSlots + blockIdx.x % kDwSlots) * gstride + hoff);
 }
 
 // ------------------------------------------------------------------ latents, norm, Adam
@@ -1518,7 +1623,7 @@ struct Plan {
     int B, nblk_arm;
     // workspace offsets (bytes)
     size_t yq, dq, gq, kf, stacks, stacks_bytes, dense, z[kMaxSp + 1], graw, gbuf[2], gdense, gstack, tmpU, tmpG, G,
-        acc4, total;
+        acc4, slots, total;
     int64_t gstack_off[CCMI_MAX_GRIDS]; // per level k (1..L-2) inside gstack, elements per frame
     int64_t gstack_per, stack_per, tmp_per;
 };
@@ -1648,6 +1753,7 @@ int make_plan(const ccmi_train_args *a, Plan &pl)
     pl.tmpG = take(4 * B * tmax);
     pl.G = take(4 * B * ((size_t)g.N + g.P));
     pl.acc4 = take(4 * B * 4);
+    pl.slots = take(4 * B * kDwSlots * (size_t)(g.syn_off - g.up_off));
     pl.total = o;
     return CCMI_OK;
 }
@@ -1714,6 +1820,13 @@ dim3 grid1(int64_t n, int B) { return dim3((unsigned)((n + kT - 1) / kT), (unsig
 // workgroups for a grid-stride reduction over n items: enough to fill the chip with a
 // batch of frames, few enough that the per-workgroup atomics stay cheap
 unsigned red_blocks(int64_t n) { return (unsigned)std::max<int64_t>(1, std::min<int64_t>((n + kT - 1) / kT, 64)); }
+// kernel-gradient reductions spread over kDwSlots addresses: one item per thread (the
+// loops are latency-bound -- their inputs were just written by other XCDs, so every load
+// goes past the local L2 -- and a thread's items run one after another)
+unsigned dw_blocks(int64_t n, int per_thread = 1)
+{
+    return (unsigned)std::max<int64_t>(1, std::min<int64_t>((n + per_thread * kT - 1) / (per_thread * kT), 4096));
+}
 
 } // namespace
 
@@ -1781,7 +1894,10 @@ extern "C" int ccmi_train_step(const ccmi_train_args *a, void *stream)
     const int64_t npx = (int64_t)g.H * g.W;
     const float lam_px = a->lmbda / (float)npx;
 
-    CCMI_HIP_CHECK(hipMemsetAsync(acc4, 0, sizeof(float) * 4 * B, s));
+    // acc4 and the kernel-gradient slots are adjacent: one memset
+    CCMI_HIP_CHECK(hipMemsetAsync(acc4, 0, pl.total - pl.acc4, s));
+    float *slots = F(pl.slots);
+    const int nreg = g.syn_off - g.up_off; // upsampling kernels' parameters (half kernels)
     CCMI_HIP_CHECK(hipMemsetAsync(G, 0, sizeof(float) * GS * B, s));
 
     // ---- forward
@@ -1878,13 +1994,13 @@ extern "C" int ccmi_train_step(const ccmi_train_args *a, void *stream)
                                pl.tmp_per);
             hipLaunchKernelGGL(t_ref_gu, grid1(n, B), dim3(kT), 0, s, GY, gys, hd, wd, kf, g.kfull, koff, g.Kp, GU,
                                pl.tmp_per);
-            const dim3 gr(red_blocks(n), B);
+            const dim3 gr(dw_blocks(n), B);
             switch (g.Kp) {
-            case 1: hipLaunchKernelGGL(t_ref_dw<1>, gr, dim3(kT), 0, s, GY, gys, U, GU, pl.tmp_per, X, (int64_t)g.N, hd, wd, Gth, GS, hoff); break;
-            case 3: hipLaunchKernelGGL(t_ref_dw<3>, gr, dim3(kT), 0, s, GY, gys, U, GU, pl.tmp_per, X, (int64_t)g.N, hd, wd, Gth, GS, hoff); break;
-            case 5: hipLaunchKernelGGL(t_ref_dw<5>, gr, dim3(kT), 0, s, GY, gys, U, GU, pl.tmp_per, X, (int64_t)g.N, hd, wd, Gth, GS, hoff); break;
-            case 7: hipLaunchKernelGGL(t_ref_dw<7>, gr, dim3(kT), 0, s, GY, gys, U, GU, pl.tmp_per, X, (int64_t)g.N, hd, wd, Gth, GS, hoff); break;
-            default: hipLaunchKernelGGL(t_ref_dw<9>, gr, dim3(kT), 0, s, GY, gys, U, GU, pl.tmp_per, X, (int64_t)g.N, hd, wd, Gth, GS, hoff); break;
+            case 1: hipLaunchKernelGGL(t_ref_dw<1>, gr, dim3(kT), 0, s, GY, gys, U, GU, pl.tmp_per, X, (int64_t)g.N, hd, wd, slots, (int64_t)nreg, hoff - g.up_off); break;
+            case 3: hipLaunchKernelGGL(t_ref_dw<3>, gr, dim3(kT), 0, s, GY, gys, U, GU, pl.tmp_per, X, (int64_t)g.N, hd, wd, slots, (int64_t)nreg, hoff - g.up_off); break;
+            case 5: hipLaunchKernelGGL(t_ref_dw<5>, gr, dim3(kT), 0, s, GY, gys, U, GU, pl.tmp_per, X, (int64_t)g.N, hd, wd, slots, (int64_t)nreg, hoff - g.up_off); break;
+            case 7: hipLaunchKernelGGL(t_ref_dw<7>, gr, dim3(kT), 0, s, GY, gys, U, GU, pl.tmp_per, X, (int64_t)g.N, hd, wd, slots, (int64_t)nreg, hoff - g.up_off); break;
+            default: hipLaunchKernelGGL(t_ref_dw<9>, gr, dim3(kT), 0, s, GY, gys, U, GU, pl.tmp_per, X, (int64_t)g.N, hd, wd, slots, (int64_t)nreg, hoff - g.up_off); break;
             }
             hipLaunchKernelGGL(t_ref_gx, grid1(n, B), dim3(kT), 0, s, GU, pl.tmp_per, GY, gys, hd, wd, kf, g.kfull, koff,
                                g.Kp, gq + g.off[k - 1], (int64_t)g.N);
@@ -1905,20 +2021,29 @@ extern "C" int ccmi_train_step(const ccmi_train_args *a, void *stream)
             const int hoff = g.up_off + A.sidx * g.hu;
             const int64_t nu = (int64_t)C * A.hs * wd;
             hipLaunchKernelGGL(t_up_u, grid1(nu, B), dim3(kT), 0, s, S, ss, A, kf, g.kfull, koff, U, pl.tmp_per);
-            hipLaunchKernelGGL(t_up_gu, grid1(nu, B), dim3(kT), 0, s, GY, gys, A, kf, g.kfull, koff, GU, pl.tmp_per);
-            const dim3 gr(red_blocks((int64_t)C * hd * wd), B);
+            if (g.K == 8 && A.d_lo == -2 && A.d_hi == 2)
+                hipLaunchKernelGGL(t_up_gu_k<8>, grid1(nu, B), dim3(kT), 0, s, GY, gys, A, kf, g.kfull, koff, GU, pl.tmp_per);
+            else
+                hipLaunchKernelGGL(t_up_gu, grid1(nu, B), dim3(kT), 0, s, GY, gys, A, kf, g.kfull, koff, GU, pl.tmp_per);
+            const dim3 gr(dw_blocks((int64_t)C * hd * wd, 8), B); // measured: 8 items per thread beat 1 here
             switch (g.K) {
-            case 4: hipLaunchKernelGGL(t_up_dw<4>, gr, dim3(kT), 0, s, GY, gys, U, GU, pl.tmp_per, S, ss, A, Gth, GS, hoff); break;
-            case 6: hipLaunchKernelGGL(t_up_dw<6>, gr, dim3(kT), 0, s, GY, gys, U, GU, pl.tmp_per, S, ss, A, Gth, GS, hoff); break;
-            default: hipLaunchKernelGGL(t_up_dw<8>, gr, dim3(kT), 0, s, GY, gys, U, GU, pl.tmp_per, S, ss, A, Gth, GS, hoff); break;
+            case 4: hipLaunchKernelGGL(t_up_dw<4>, gr, dim3(kT), 0, s, GY, gys, U, GU, pl.tmp_per, S, ss, A, slots, (int64_t)nreg, hoff - g.up_off); break;
+            case 6: hipLaunchKernelGGL(t_up_dw<6>, gr, dim3(kT), 0, s, GY, gys, U, GU, pl.tmp_per, S, ss, A, slots, (int64_t)nreg, hoff - g.up_off); break;
+            default: hipLaunchKernelGGL(t_up_dw<8>, gr, dim3(kT), 0, s, GY, gys, U, GU, pl.tmp_per, S, ss, A, slots, (int64_t)nreg, hoff - g.up_off); break;
             }
             float *GSd = (k == g.L - 1) ? gq + g.off[k] : gst + pl.gstack_off[k];
             const int64_t gss = (k == g.L - 1) ? (int64_t)g.N : pl.gstack_per;
-            hipLaunchKernelGGL(t_up_gs, grid1((int64_t)C * A.hs * A.ws, B), dim3(kT), 0, s, GU, pl.tmp_per, A, kf, g.kfull,
-                               koff, GSd, gss, k == g.L - 1 ? 1 : 0);
+            if (g.K == 8 && A.d_lo == -2 && A.d_hi == 2)
+                hipLaunchKernelGGL(t_up_gs_k<8>, grid1((int64_t)C * A.hs * A.ws, B), dim3(kT), 0, s, GU, pl.tmp_per, A, kf,
+                                   g.kfull, koff, GSd, gss, k == g.L - 1 ? 1 : 0);
+            else
+                hipLaunchKernelGGL(t_up_gs, grid1((int64_t)C * A.hs * A.ws, B), dim3(kT), 0, s, GU, pl.tmp_per, A, kf,
+                                   g.kfull, koff, GSd, gss, k == g.L - 1 ? 1 : 0);
         }
     }
     CCMI_HIP_CHECK(hipGetLastError());
+
+    hipLaunchKernelGGL(t_dw_fold, dim3((unsigned)ccmi_div_up(nreg, 64), B), dim3(64), 0, s, slots, nreg, Gth, GS, g.up_off);
 
     // ---- latent gradients, norm, Adam
     hipLaunchKernelGGL(t_latgrad, grid1(g.N, B), dim3(kT), 0, s, gq, dq, g.N, G, GS);
