@@ -125,7 +125,6 @@ constexpr int kHsRows = kRH / 2 + 1 + FT::NS - 1; // half-res rows under <= kRH 
 constexpr int kHrRows = kRH + 7 - 1;              // refine rows incl. the 7-tap halo
 constexpr int kSW = kRW / 2 + 1 + FT::NS - 1 + 3; // raw source tile pitch (37 used)
 constexpr int kTW = kRW + 7 - 1 + 2;              // raw latent tile pitch (70 used, 72 read)
-constexpr int kPairs = kRW / 2 + 1;               // even/odd column pairs under <= kRW columns
 
 // MH: split-f16 MFMA first head layer (a separate instantiation: compiled into the default
 // kernel as a runtime branch, its registers pushed the VALU variant from 108 to 133 VGPRs,
@@ -194,9 +193,8 @@ __global__ __launch_bounds__(kFThreads) __attribute__((amdgpu_waves_per_eu(4))) 
         __syncthreads();
     }
 
-    // window's clamped image rectangle [Ya, Yb] x [Xa, Xb] (fused upsampling only)
-    const int Ya = clampi(oy, A.H - 1), Yb = clampi(oy + kRH - 1, A.H - 1);
-    const int Xa = clampi(ox, A.W - 1), Xb = clampi(ox + kRW - 1, A.W - 1);
+    // window's clamped image origin (fused upsampling only)
+    const int Ya = clampi(oy, A.H - 1), Xa = clampi(ox, A.W - 1);
     float wu[8], wr[7];
     if constexpr (UPS) {
         constexpr int C = CIN - 1;
@@ -205,113 +203,127 @@ __global__ __launch_bounds__(kFThreads) __attribute__((amdgpu_waves_per_eu(4))) 
         for (int k = 0; k < 8; ++k) wu[k] = uprm[U.up_off + k];
 #pragma unroll
         for (int k = 0; k < 7; ++k) wr[k] = uprm[U.pre_off + k];
-        const int nX = Xb - Xa + 1;
         const int jbase = Ya / 2 + FT::D0, ibase = Xa / 2 + FT::D0;
-        const int nj = Yb / 2 - Ya / 2 + FT::NS, ni = Xb / 2 - Xa / 2 + FT::NS;
-        const int nr = Yb - Ya + 7, nt = nX + 6;
-        // phase A: raw tiles, coalesced (lane-consecutive columns); fixed trip counts, so
-        // every load of a thread is issued before the first LDS store waits on one
+        // Phases A + B are row-parallel and wave-private: wave wv owns raw source rows
+        // r = wv + 8u of the [C][kHsRows] tile and raw latent rows yr = wv + 8u; lane = column.
+        // Row addresses are wave-uniform (scalar), so a load costs no VALU index math, and a
+        // wave's horizontal passes read back only rows it wrote itself -- a wave-level fence
+        // instead of a workgroup barrier between the raw tiles and the horizontal passes.
+        const int wv = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
+        const int lane = threadIdx.x & 63;
+        constexpr int kSR = C * kHsRows, kSU = (kSR + 7) / 8;     // source rows, per wave
+        constexpr int kLU = (kHrRows + 7) / 8;                    // latent rows per wave
+        static_assert(kSW <= 64 && kTW <= 128 && kTW > 64, "lane = raw column");
+        const float *src = U.src + (int64_t)b * U.src_stride;
+        const float *rs = U.ref_src + (int64_t)b * U.ref_stride;
+        float sv[kSU], tv[kLU][2];
         {
-            const float *src = U.src + (int64_t)b * U.src_stride;
+            // phase A: raw tiles; clamped source coordinates are always inside the stack
             const int64_t splane = (int64_t)U.hs * U.ws;
-            constexpr int NSI = C * kHsRows * kSW, NSU = (NSI + kFThreads - 1) / kFThreads;
-            float sv[NSU];
+            const int scol = clampi(ibase + lane, U.ws - 1);
 #pragma unroll
-            for (int u = 0; u < NSU; ++u) {
-                const int i = threadIdx.x + u * kFThreads;
-                const int ch = i / (kHsRows * kSW), rem = i - ch * (kHsRows * kSW);
-                const int jj = rem / kSW, ii = rem - jj * kSW;
+            for (int u = 0; u < kSU; ++u) {
+                const int r = wv + 8 * u;
                 sv[u] = 0.f;
-                if (i < NSI && jj < nj && ii < ni)
+                if (u < kSU - 1 || r < kSR) {
+                    const int ch = r / kHsRows, jj = r - ch * kHsRows;
+                    const float *row = src + ch * splane + (int64_t)clampi(jbase + jj, U.hs - 1) * U.ws;
 #if defined(CCMI_DIAG_NOLOAD) // diagnostic build only: phase A without its global loads
-                    sv[u] = 0.001f * (float)(jj + ii);
+                    sv[u] = 0.001f * (float)(jj + scol);
 #else
-                    sv[u] = src[ch * splane + (int64_t)clampi(jbase + jj, U.hs - 1) * U.ws + clampi(ibase + ii, U.ws - 1)];
+                    sv[u] = row[scol];
 #endif
+                }
             }
-            const float *rs = U.ref_src + (int64_t)b * U.ref_stride;
-            constexpr int NTI = kHrRows * kTW, NTU = (NTI + kFThreads - 1) / kFThreads;
-            float tv[NTU];
+            // latent tile: zero outside the image (the refine's zero padding)
+            int tx[2];
+            bool tin[2];
 #pragma unroll
-            for (int u = 0; u < NTU; ++u) {
-                const int i = threadIdx.x + u * kFThreads;
-                const int yr = i / kTW, xt = i - yr * kTW;
-                const int Y = Ya - 3 + yr, X = Xa - 3 + xt;
-                tv[u] = 0.f;
-                if (i < NTI && yr < nr && xt < nt && Y >= 0 && Y < U.hd && X >= 0 && X < U.wd)
+            for (int h = 0; h < 2; ++h) {
+                const int X = Xa - 3 + lane + 64 * h;
+                tin[h] = X >= 0 && X < U.wd && lane + 64 * h < kTW;
+                tx[h] = clampi(X, U.wd - 1);
+            }
+#pragma unroll
+            for (int u = 0; u < kLU; ++u) {
+                const int yr = wv + 8 * u;
+                const int Y = Ya - 3 + yr;
+                const float *row = rs + (int64_t)clampi(Y, U.hd - 1) * U.wd;
+#pragma unroll
+                for (int h = 0; h < 2; ++h) {
 #if defined(CCMI_DIAG_NOLOAD)
-                    tv[u] = 0.001f * (float)(yr + xt);
+                    tv[u][h] = 0.001f * (float)(yr + tx[h]);
 #else
-                    tv[u] = rs[(int64_t)Y * U.wd + X];
+                    tv[u][h] = row[tx[h]];
 #endif
+                }
             }
             stage_tables();
 #pragma unroll
-            for (int u = 0; u < NSU; ++u) {
-                const int i = threadIdx.x + u * kFThreads;
-                if (i < NSI) s_st[i] = U.src_quant ? rintf(U.gain * sv[u]) : sv[u];
+            for (int u = 0; u < kSU; ++u) {
+                const int r = wv + 8 * u;
+                if ((u < kSU - 1 || r < kSR) && lane < kSW) s_st[r * kSW + lane] = U.src_quant ? rintf(U.gain * sv[u]) : sv[u];
             }
 #pragma unroll
-            for (int u = 0; u < NTU; ++u) {
-                const int i = threadIdx.x + u * kFThreads;
-                if (i < NTI) s_yt[i] = U.ref_quant ? rintf(U.gain * tv[u]) : tv[u];
+            for (int u = 0; u < kLU; ++u) {
+                const int yr = wv + 8 * u;
+                if (yr >= kHrRows) continue;
+                const int Y = Ya - 3 + yr;
+                const bool yin = Y >= 0 && Y < U.hd;
+#pragma unroll
+                for (int h = 0; h < 2; ++h) {
+                    const float v = U.ref_quant ? rintf(U.gain * tv[u][h]) : tv[u][h];
+                    if (lane + 64 * h < kTW) s_yt[yr * kTW + lane + 64 * h] = (yin && tin[h]) ? v : 0.f;
+                }
             }
         }
-        __syncthreads();
+        // the wave reads back rows it wrote (other lanes' columns): order its LDS accesses
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
         FSTAMP(0);
-        // phase B: horizontal passes from LDS, in ups_level_fixed's operation order.
-        // Transposed conv: one item = the (even, odd) column pair 2k, 2k+1 of a source row,
-        // which share NS source samples (compile-time taps per parity).
+        // phase B: horizontal passes, in ups_level_fixed's operation order.  Transposed conv:
+        // lane = (row half, pair k = lane & 31); the (even, odd) outputs of pair k read source
+        // columns k .. k + NS - 1 and land in window columns 2k - (Xa & 1), +1.
         {
-            const int xe0 = Xa & ~1; // first even column of the pairs
-            // one item = 4 consecutive pairs of a source row: NS + 3 samples read once, the
-            // (even, odd) outputs of a pair accumulated as one packed FMA per sample
-            constexpr int kG = (kPairs + 3) / 4;
             f2 wp[FT::NS];
 #pragma unroll
             for (int m = 0; m < FT::NS; ++m) {
                 const int te = FT::tap(0, FT::D0 + m), to = FT::tap(1, FT::D0 + m);
                 wp[m] = f2{te >= 0 ? wu[te] : 0.f, to >= 0 ? wu[to] : 0.f};
             }
-            static_assert(4 * kG + FT::NS - 1 <= kSW, "group reads stay inside the source row");
-#pragma unroll 2
-            for (int i = threadIdx.x; i < C * kHsRows * kG; i += kFThreads) {
-                const int ch = i / (kHsRows * kG), rem = i - ch * (kHsRows * kG);
-                const int jj = rem / kG, g = rem - jj * kG;
-                if (jj >= nj) continue;
-                const float *sr = s_st + (ch * kHsRows + jj) * kSW + 4 * g;
-                float v[FT::NS + 3];
+            const int odd = Xa & 1;
+            const int k = lane & 31, hsel = lane >> 5;
+            const int xe = 2 * k - odd;
+            static_assert(32 + FT::NS - 1 < kSW, "pair 32 reads stay inside the source row");
+            auto pair = [&](int r, int kk, int xw) {
+                const float *sr = s_st + r * kSW + kk;
+                f2 eo = f2(0.f);
 #pragma unroll
-                for (int m = 0; m < FT::NS + 3; ++m) v[m] = sr[m];
-                float *hr = s_hs + (ch * kHsRows + jj) * kRW;
+                for (int m = 0; m < FT::NS; ++m) eo = __builtin_elementwise_fma(wp[m], f2(sr[m]), eo);
+                float *hr = s_hs + r * kRW;
+                if (xw >= 0) hr[xw] = eo.x;
+                if (xw + 1 < kRW) hr[xw + 1] = eo.y;
+            };
 #pragma unroll
-                for (int q = 0; q < 4; ++q) {
-                    f2 eo = f2(0.f);
-#pragma unroll
-                    for (int m = 0; m < FT::NS; ++m) eo = __builtin_elementwise_fma(wp[m], f2(v[q + m]), eo);
-                    const int xe = xe0 + 2 * (4 * g + q) - Xa; // window-relative column of the even output
-                    if (xe >= 0 && xe <= nX - 1) hr[xe] = eo.x;
-                    if (xe + 1 >= 0 && xe + 1 < nX) hr[xe + 1] = eo.y;
-                }
+            for (int u = 0; u < kSU; u += 2) {
+                const int r = wv + 8 * (u + hsel);
+                if (u + 1 < kSU - 1 || r < kSR) pair(r, k, xe);
             }
-        }
-        // refine: one item = 4 consecutive columns of a row (sliding 7-tap window)
-        for (int i = threadIdx.x; i < kHrRows * (kRW / 4); i += kFThreads) {
-            const int yr = i / (kRW / 4), x4 = (i - yr * (kRW / 4)) * 4;
-            if (yr >= nr || x4 >= nX) continue;
-            const float *tr = s_yt + yr * kTW + x4;
-            float t[10];
+            if (odd) { // pair 32 of every row (window columns 63, 64)
+                const int r = wv + 8 * lane;
+                if (lane < kSU && r < kSR) pair(r, 32, 63);
+            }
+            // refine: lane = window column, 7-tap sliding window over the wave's latent rows
 #pragma unroll
-            for (int k = 0; k < 10; ++k) t[k] = tr[k];
-            // rows outside the image are the vertical pass's zero padding
-            const int Y = Ya - 3 + yr;
-            const bool in_img = Y >= 0 && Y < U.hd;
-#pragma unroll
-            for (int q = 0; q < 4; ++q) {
+            for (int u = 0; u < kLU; ++u) {
+                const int yr = wv + 8 * u;
+                if (yr >= kHrRows) continue;
+                const float *tr = s_yt + yr * kTW + lane;
                 float acc = 0.f;
 #pragma unroll
-                for (int k = 0; k < 7; ++k) acc = fmaf(wr[k], t[q + k], acc);
-                s_hr[yr * kRW + x4 + q] = in_img ? acc : 0.f;
+                for (int q = 0; q < 7; ++q) acc = fmaf(wr[q], tr[q], acc);
+                s_hr[yr * kRW + lane] = acc;
             }
         }
         __syncthreads();
