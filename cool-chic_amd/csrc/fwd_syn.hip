@@ -62,20 +62,26 @@ constexpr int kRowsPerThread = kRH / (kFThreads / kRW); // 4
 // lut8 (8-bit output): the 256 quotients k / 255 in LDS, so the rounded value costs a
 // lookup instead of an IEEE division; clamping k to [0, 255] first gives the same value
 // as clamping the quotient (NaN -> 0 both ways).
+// 32-bit byte offsets from a wave-uniform base (a frame's planes stay below 4 GB, checked at
+// launch): the address is SGPR base + zero-extended VGPR offset, no 64-bit VALU arithmetic
+__device__ __forceinline__ float *at(float *base, uint32_t i) { return (float *)((char *)base + i * 4u); }
+__device__ __forceinline__ float ldu(const float *base, uint32_t i) { return *(const float *)((const char *)base + i * 4u); }
+
 __device__ __forceinline__ void store_out(const FusedArgs &A, float *out, int64_t plane, int m, int gy, int gx, float v,
                                           const float *lut8)
 {
+    const uint32_t pl = (uint32_t)plane, px = (uint32_t)(gy * A.W + gx);
     if (A.qmax <= 0.f) {
-        out[m * plane + (int64_t)gy * A.W + gx] = v;
+        *at(out, m * pl + px) = v;
         return;
     }
     const float q = lut8 ? lut8[(int)fminf(fmaxf(rintf(v * 255.f), 0.f), 255.f)]
                          : fminf(fmaxf(rintf(v * A.qmax) / A.qmax, 0.f), 1.f);
     if (!A.yuv420 || m == 0) {
-        out[m * plane + (int64_t)gy * A.W + gx] = q;
+        *at(out, m * pl + px) = q;
     } else if (!(gy & 1) && !(gx & 1) && (gy >> 1) < (A.H >> 1) && (gx >> 1) < (A.W >> 1)) {
-        const int64_t cp = (int64_t)(A.H >> 1) * (A.W >> 1);
-        out[plane + (m - 1) * cp + (int64_t)(gy >> 1) * (A.W >> 1) + (gx >> 1)] = q;
+        const uint32_t cp = (uint32_t)((A.H >> 1) * (A.W >> 1));
+        *at(out, pl + (m - 1) * cp + (uint32_t)((gy >> 1) * (A.W >> 1) + (gx >> 1))) = q;
     }
 }
 
@@ -231,7 +237,7 @@ __global__ __launch_bounds__(kFThreads) __attribute__((amdgpu_waves_per_eu(4))) 
 #if defined(CCMI_DIAG_NOLOAD) // diagnostic build only: phase A without its global loads
                     sv[u] = 0.001f * (float)(jj + scol);
 #else
-                    sv[u] = row[scol];
+                    sv[u] = ldu(row, (uint32_t)scol);
 #endif
                 }
             }
@@ -254,7 +260,7 @@ __global__ __launch_bounds__(kFThreads) __attribute__((amdgpu_waves_per_eu(4))) 
 #if defined(CCMI_DIAG_NOLOAD)
                     tv[u][h] = 0.001f * (float)(yr + tx[h]);
 #else
-                    tv[u][h] = row[tx[h]];
+                    tv[u][h] = ldu(row, (uint32_t)tx[h]);
 #endif
                 }
             }
@@ -610,18 +616,21 @@ __global__ __launch_bounds__(kFThreads) __attribute__((amdgpu_waves_per_eu(4))) 
     int lx[3];
 #pragma unroll
     for (int d = 0; d < 3; ++d) lx[d] = clampi(cxg + d - 1, A.W - 1) - ox;
-    const bool col_in = gx < A.W;
-    int cur = 0;
-    for (int s = 0; s < A.n_sp; ++s) {
+    // windows whose rows all lie strictly inside the image write no replicate rows
+    const bool inner = oy > 0 && oy + kRH < A.H;
+    // one 3x3 layer from buf(cur) into buf(cur ^ 1); the last one also lands in LDS (each
+    // thread at its own pixels) and the stores to HBM follow in their own pass, so the FMA
+    // loop carries no output-format branches
+    auto layer = [&](auto LAST, int s, int cur) {
+        constexpr bool last = decltype(LAST)::value;
         __syncthreads();
-        const int t = s + 1;
-        const bool last = s == A.n_sp - 1;
         const cfloat_ptr wt = prm + A.sp[s].w_off;
         const cfloat_ptr bs = prm + A.sp[s].b_off;
-        const float lo = A.sp[s].relu ? 0.f : -INFINITY;
-        const float rsd = A.sp[s].residual ? 1.f : 0.f;
+        const f2 lo = f2(A.sp[s].relu ? 0.f : -INFINITY);
+        const f2 rsd = f2(A.sp[s].residual ? 1.f : 0.f);
         // plane row of window row (rb - 1) in this thread's column
         const float *src = &buf(cur)[0][0] + rb * kRW + c;
+        float *dst = &buf(cur ^ 1)[0][0] + (rb + 1) * kRW + c;
 #pragma unroll
         for (int q = 0; q < NR / 2; ++q) {
             // output rows rb + 2q, rb + 2q + 1 read window rows rb + 2q - 1 .. rb + 2q + 2
@@ -648,28 +657,71 @@ __global__ __launch_bounds__(kFThreads) __attribute__((amdgpu_waves_per_eu(4))) 
 #pragma unroll
                         for (int dx = 0; dx < 3; ++dx)
                             acc = __builtin_elementwise_fma(f2(wm[(k * 3 + dy) * 3 + dx]), P[dy][k][dx], acc);
-                // residual: the input at the centre (select chain: no indexed registers)
-                f2 ctr = P[1][0][1];
+                // residual: the input at the centre, re-read from LDS (a runtime-indexed
+                // register select would cost a VALU chain per channel)
+                const float *e = src + m * kPlane + (2 * q + 1) * kRW + (lx[1] - c);
+                acc = __builtin_elementwise_max(__builtin_elementwise_fma(rsd, f2{e[0], e[kRW]}, acc), lo);
+                float *d = dst + m * kPlane + 2 * q * kRW;
+                if (last || inner) {
+                    d[0] = acc.x;
+                    d[kRW] = acc.y;
+                } else {
 #pragma unroll
-                for (int k = 1; k < CMID; ++k) ctr = m == k ? P[1][k][1] : ctr;
-                acc = __builtin_elementwise_max(__builtin_elementwise_fma(f2(rsd), ctr, acc), f2(lo));
-#pragma unroll
-                for (int h = 0; h < 2; ++h) {
-                    const int r = rb + 2 * q + h, gy = oy + r;
-                    const float v = h ? acc.y : acc.x;
-                    if (last) {
-                        if (r >= t && r < kRH - t && c >= t && c < kRW - t && gy < A.H && col_in)
-                            store_out(A, out, plane, m, gy, gx, v, lut8);
-                    } else if (gy >= 0 && gy < A.H) {
-                        float *dst = &buf(cur ^ 1)[m][0] + (r + 1) * kRW + c;
-                        dst[0] = v;
-                        if (gy == 0) dst[-kRW] = v;     // replicate above the image
-                        if (gy == A.H - 1) dst[kRW] = v; // and below it
+                    for (int h = 0; h < 2; ++h) {
+                        const int gy = oy + rb + 2 * q + h;
+                        const float v = h ? acc.y : acc.x;
+                        if (gy >= 0 && gy < A.H) {
+                            d[h * kRW] = v;
+                            if (gy == 0) d[(h - 1) * kRW] = v;     // replicate above the image
+                            if (gy == A.H - 1) d[(h + 1) * kRW] = v; // and below it
+                        }
                     }
                 }
             }
         }
-        cur ^= 1;
+    };
+    int cur = 0;
+    for (int s = 0; s < A.n_sp - 1; ++s, cur ^= 1) layer(std::false_type{}, s, cur);
+    layer(std::true_type{}, A.n_sp - 1, cur);
+    cur ^= 1;
+    // stores: this thread's own pixels of the last layer, back from LDS (program order, no
+    // barrier), one branch-free loop per output format
+    {
+        const int t = A.n_sp;
+        const float *fin = &buf(cur)[0][0] + (rb + 1) * kRW + c;
+        const bool col_ok = c >= t && c < kRW - t && gx < A.W;
+        const uint32_t pl = (uint32_t)plane;
+        const uint32_t cw = (uint32_t)(A.W >> 1), cp = (uint32_t)((A.H >> 1) * (A.W >> 1));
+        const bool cx_ok = !(gx & 1) && (gx >> 1) < (A.W >> 1);
+        auto emit = [&](auto MODE) {
+            constexpr int md = decltype(MODE)::value; // 0 raw, 1 444, 2 420; +2: 8-bit table
+            constexpr bool tab = md >= 3;
+            constexpr int fmt = tab ? md - 2 : md;
+#pragma unroll
+            for (int p = 0; p < NR; ++p) {
+                const int r = rb + p, gy = oy + r;
+                if (!(col_ok && r >= t && r < kRH - t && gy < A.H)) continue;
+                const uint32_t px = (uint32_t)(gy * A.W + gx);
+                const bool cy_ok = fmt == 2 && cx_ok && !(gy & 1) && (gy >> 1) < (A.H >> 1);
+                const uint32_t cpx = (uint32_t)((gy >> 1) * (int)cw + (gx >> 1));
+#pragma unroll
+                for (int m = 0; m < CMID; ++m) {
+                    float v = fin[m * kPlane + p * kRW];
+                    if constexpr (fmt > 0) {
+                        v = tab ? lut8[(int)fminf(fmaxf(rintf(v * 255.f), 0.f), 255.f)]
+                                : fminf(fmaxf(rintf(v * A.qmax) / A.qmax, 0.f), 1.f);
+                    }
+                    if (fmt < 2 || m == 0) *at(out, m * pl + px) = v;
+                    else if (cy_ok) *at(out, pl + (m - 1) * cp + cpx) = v;
+                }
+            }
+        };
+        if (A.qmax <= 0.f) emit(std::integral_constant<int, 0>{});
+        else if (lut8) {
+            if (A.yuv420) emit(std::integral_constant<int, 4>{});
+            else emit(std::integral_constant<int, 3>{});
+        } else if (A.yuv420) emit(std::integral_constant<int, 2>{});
+        else emit(std::integral_constant<int, 1>{});
     }
     FSTAMP(4);
 }
@@ -793,6 +845,8 @@ bool make_plan(const ccmi_syn_args *a, Plan *P)
     for (int l = n_head; l < a->n_layers; ++l)
         if (L[l].ks != 3 || L[l].n_out != cmid) return false;
     if (cmid != 3 && cmid != 4) return false; // instantiated shapes
+    // the fused kernel addresses its output with 32-bit byte offsets
+    if ((int64_t)4 * cmid * a->h * a->w >= ((int64_t)1 << 32)) return false;
     FusedArgs &f = P->fa;
     f = FusedArgs{};
     f.cin = a->c_in;
