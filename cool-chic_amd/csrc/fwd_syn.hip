@@ -65,7 +65,7 @@ constexpr int kRowsPerThread = kRH / (kFThreads / kRW); // 4
 // 32-bit byte offsets from a wave-uniform base (a frame's planes stay below 4 GB, checked at
 // launch): the address is SGPR base + zero-extended VGPR offset, no 64-bit VALU arithmetic
 __device__ __forceinline__ float *at(float *base, uint32_t i) { return (float *)((char *)base + i * 4u); }
-__device__ __forceinline__ float ldu(const float *base, uint32_t i) { return *(const float *)((const char *)base + i * 4u); }
+__device__ __forceinline__ float ldu(const float *base, uint32_t byte) { return *(const float *)((const char *)base + byte); }
 
 __device__ __forceinline__ void store_out(const FusedArgs &A, float *out, int64_t plane, int m, int gy, int gx, float v,
                                           const float *lut8)
@@ -135,7 +135,9 @@ constexpr int kTW = kRW + 7 - 1 + 2;              // raw latent tile pitch (70 u
 // MH: split-f16 MFMA first head layer (a separate instantiation: compiled into the default
 // kernel as a runtime branch, its registers pushed the VALU variant from 108 to 133 VGPRs,
 // i.e. from 4 to 3 waves per SIMD, and decode_fused from 0.97 to 1.40 ms per 32 frames)
-template <int CIN, int CMID, bool UPS, bool MH = false>
+// HID > 0: the 2-layer head's hidden width fixed at compile time (fully unrolled unit loop:
+// weight records at immediate LDS offsets, no loop counter or record rotation)
+template <int CIN, int CMID, bool UPS, bool MH = false, int HID = 0>
 __global__ __launch_bounds__(kFThreads) __attribute__((amdgpu_waves_per_eu(4))) void syn_fused_kernel(FusedArgs A, LevelArgs U)
 {
     constexpr int NR = kRowsPerThread;
@@ -161,6 +163,11 @@ __global__ __launch_bounds__(kFThreads) __attribute__((amdgpu_waves_per_eu(4))) 
     // ahead of use, unlike the SGPR path whose scalar loads the compiler waits on at once
     __shared__ __attribute__((aligned(16))) float s_head[kMaxHid][16];
     static_assert(CIN + 1 + CMID <= 16, "hidden-unit record");
+    // field f of a record sits at slot hr(f): slots 3, 7, 11, 15 (the last dword of each
+    // ds_read_b128) stay empty when the fields fit without them, because the compiler
+    // copies a broadcast operand out of that position into a fresh register pair first
+    constexpr bool kPadRec = CIN + 1 + CMID <= 12;
+    auto hr = [](int f) constexpr { return kPadRec ? f + f / 3 : f; };
 
     const int b = blockIdx.y;
     const int halo = A.n_sp;
@@ -191,7 +198,7 @@ __global__ __launch_bounds__(kFThreads) __attribute__((amdgpu_waves_per_eu(4))) 
                 if (f < CIN) v = prm[A.w0_off + j * CIN + f];
                 else if (f == CIN) v = prm[A.b0_off + j];
                 else if (f <= CIN + CMID) v = prm[A.w1_off + (f - CIN - 1) * A.hid + j];
-                s_head[j][f] = v;
+                if (f <= CIN + CMID) s_head[j][hr(f)] = v; // other slots are never operands
             }
     };
     if constexpr (!UPS) {
@@ -219,48 +226,52 @@ __global__ __launch_bounds__(kFThreads) __attribute__((amdgpu_waves_per_eu(4))) 
         const int lane = threadIdx.x & 63;
         constexpr int kSR = C * kHsRows, kSU = (kSR + 7) / 8;     // source rows, per wave
         constexpr int kLU = (kHrRows + 7) / 8;                    // latent rows per wave
-        static_assert(kSW <= 64 && kTW <= 128 && kTW > 64, "lane = raw column");
+        static_assert(kSW <= 64 && kTW <= 128 && kTW > 64 && kHsRows >= 8, "lane = raw column, one row wrap per step");
         const float *src = U.src + (int64_t)b * U.src_stride;
         const float *rs = U.ref_src + (int64_t)b * U.ref_stride;
         float sv[kSU], tv[kLU][2];
         {
             // phase A: raw tiles; clamped source coordinates are always inside the stack
-            const int64_t splane = (int64_t)U.hs * U.ws;
-            const int scol = clampi(ibase + lane, U.ws - 1);
+            // (channel, row) of r = wv + 8u in 32-bit scalar registers (a frame's stack stays
+            // below 2 GB; checked at launch)
+            const int splane = U.hs * U.ws;
+            const uint32_t scol = 4u * (uint32_t)clampi(ibase + lane, U.ws - 1);
 #pragma unroll
             for (int u = 0; u < kSU; ++u) {
                 const int r = wv + 8 * u;
+                // ch = r / kHsRows without a division: wv < 8 moves r past at most one boundary
+                const int c0 = (8 * u) / kHsRows, tb = kHsRows * (c0 + 1) - 8 * u; // folded (u unrolled)
+                const int ch = c0 + (wv >= tb ? 1 : 0), jj = r - ch * kHsRows;
                 sv[u] = 0.f;
                 if (u < kSU - 1 || r < kSR) {
-                    const int ch = r / kHsRows, jj = r - ch * kHsRows;
-                    const float *row = src + ch * splane + (int64_t)clampi(jbase + jj, U.hs - 1) * U.ws;
+                    const int row = ch * splane + clampi(jbase + jj, U.hs - 1) * U.ws;
 #if defined(CCMI_DIAG_NOLOAD) // diagnostic build only: phase A without its global loads
                     sv[u] = 0.001f * (float)(jj + scol);
 #else
-                    sv[u] = ldu(row, (uint32_t)scol);
+                    sv[u] = ldu(src + row, scol);
 #endif
                 }
             }
             // latent tile: zero outside the image (the refine's zero padding)
-            int tx[2];
+            uint32_t tx[2];
             bool tin[2];
 #pragma unroll
             for (int h = 0; h < 2; ++h) {
                 const int X = Xa - 3 + lane + 64 * h;
                 tin[h] = X >= 0 && X < U.wd && lane + 64 * h < kTW;
-                tx[h] = clampi(X, U.wd - 1);
+                tx[h] = 4u * (uint32_t)clampi(X, U.wd - 1);
             }
 #pragma unroll
             for (int u = 0; u < kLU; ++u) {
                 const int yr = wv + 8 * u;
                 const int Y = Ya - 3 + yr;
-                const float *row = rs + (int64_t)clampi(Y, U.hd - 1) * U.wd;
+                const int row = clampi(Y, U.hd - 1) * U.wd;
 #pragma unroll
                 for (int h = 0; h < 2; ++h) {
 #if defined(CCMI_DIAG_NOLOAD)
                     tv[u][h] = 0.001f * (float)(yr + tx[h]);
 #else
-                    tv[u][h] = ldu(row, (uint32_t)tx[h]);
+                    tv[u][h] = ldu(rs + row, tx[h]);
 #endif
                 }
             }
@@ -433,7 +444,7 @@ __global__ __launch_bounds__(kFThreads) __attribute__((amdgpu_waves_per_eu(4))) 
             {
                 auto wrow = [&](int u, float (&v)[8]) {
 #pragma unroll
-                    for (int j = 0; j < 8; ++j) v[j] = (u < hid && j <= CIN) ? s_head[u][j] : 0.f;
+                    for (int j = 0; j < 8; ++j) v[j] = (u < hid && j <= CIN) ? s_head[u][hr(j)] : 0.f;
                 };
                 float v[8];
                 h8 hi, lo, z = {};
@@ -451,8 +462,8 @@ __global__ __launch_bounds__(kFThreads) __attribute__((amdgpu_waves_per_eu(4))) 
             const float4 *w1v = reinterpret_cast<const float4 *>(&s_head[0][0]);
             auto wl2 = [&](int u) -> float4 { // w1[0..CMID)[u]
                 const float *r = s_head[u];
-                return float4{r[CIN + 1], CMID > 1 ? r[CIN + 2] : 0.f, CMID > 2 ? r[CIN + 3] : 0.f,
-                              CMID > 3 ? r[CIN + 4] : 0.f};
+                return float4{r[hr(CIN + 1)], CMID > 1 ? r[hr(CIN + 2)] : 0.f, CMID > 2 ? r[hr(CIN + 3)] : 0.f,
+                              CMID > 3 ? r[hr(CIN + 4)] : 0.f};
             };
             (void)w1v;
             const float lo0 = A.relu0 ? 0.f : -INFINITY;
@@ -528,7 +539,7 @@ __global__ __launch_bounds__(kFThreads) __attribute__((amdgpu_waves_per_eu(4))) 
                 }
             }
         } else if (A.n_head == 2) {
-            const int hid = A.hid;
+            const int hid = HID > 0 ? HID : A.hid;
             // fmaxf(acc, lo0) is the optional ReLU without a per-element select
             const f2 lo0 = f2(A.relu0 ? 0.f : -INFINITY);
             f2 xp[NR / 2][CIN], op[NR / 2][CMID];
@@ -541,30 +552,41 @@ __global__ __launch_bounds__(kFThreads) __attribute__((amdgpu_waves_per_eu(4))) 
             }
             __syncthreads(); // s_head staged
             // software pipelined: the record of unit j+2 is loaded while unit j+1 computes
-            struct Rec { float4 v[4]; };
+            typedef float f4v __attribute__((ext_vector_type(4)));
+            struct Rec { f4v v[4]; };
+            // records through an LDS pointer the compiler cannot fold to a constant, so the
+            // unrolled reads are base + immediate offset (not one v_mov of an address each)
+            typedef const __attribute__((address_space(3))) f4v *lds_f4;
+            lds_f4 hb = (lds_f4)(&s_head[0][0]);
+            asm volatile("" : "+v"(hb));
             auto load = [&](int j) {
-                const float4 *p = reinterpret_cast<const float4 *>(s_head[j < hid ? j : hid - 1]);
+                const lds_f4 p = hb + 4 * (j < hid ? j : hid - 1);
                 return Rec{{p[0], p[1], p[2], p[3]}};
             };
             auto unit = [&](const Rec &r) {
                 const float *u = reinterpret_cast<const float *>(r.v);
-                const f2 bj = f2(u[CIN]);
+                const f2 bj = f2(u[hr(CIN)]);
 #pragma unroll
                 for (int q = 0; q < NR / 2; ++q) {
                     f2 acc = bj;
 #pragma unroll
-                    for (int k = 0; k < CIN; ++k) acc = __builtin_elementwise_fma(f2(u[k]), xp[q][k], acc);
+                    for (int k = 0; k < CIN; ++k) acc = __builtin_elementwise_fma(f2(u[hr(k)]), xp[q][k], acc);
                     acc = __builtin_elementwise_max(acc, lo0);
 #pragma unroll
-                    for (int m = 0; m < CMID; ++m) op[q][m] = __builtin_elementwise_fma(f2(u[CIN + 1 + m]), acc, op[q][m]);
+                    for (int m = 0; m < CMID; ++m) op[q][m] = __builtin_elementwise_fma(f2(u[hr(CIN + 1 + m)]), acc, op[q][m]);
                 }
             };
-            Rec ra = load(0), rb2 = load(1);
-            for (int j = 0; j < hid; j += 2) {
-                unit(ra);
-                ra = load(j + 2);
-                if (j + 1 < hid) unit(rb2);
-                rb2 = load(j + 3);
+            if constexpr (HID > 0) {
+#pragma unroll
+                for (int j = 0; j < HID; ++j) unit(load(j));
+            } else {
+                Rec ra = load(0), rb2 = load(1);
+                for (int j = 0; j < hid; j += 2) {
+                    unit(ra);
+                    ra = load(j + 2);
+                    if (j + 1 < hid) unit(rb2);
+                    rb2 = load(j + 3);
+                }
             }
             const float lo1 = A.relu1 ? 0.f : -INFINITY;
 #pragma unroll
@@ -787,6 +809,12 @@ __global__ __launch_bounds__(kThreads) void post_kernel(const float *__restrict_
 template <int CMID, bool UPS>
 void launch_fused(dim3 grid, hipStream_t s, const FusedArgs &fa, const LevelArgs &u)
 {
+    // the presets' 7-grid decoders with a 48-wide head (hop and its relatives): unrolled head
+    static const bool generic_head = getenv("CCMI_SYN_HEAD_LOOP") != nullptr; // A/B switch
+    if (fa.cin == 7 && fa.n_head == 2 && fa.hid == 48 && !generic_head) {
+        hipLaunchKernelGGL((syn_fused_kernel<7, CMID, UPS, false, 48>), grid, dim3(kFThreads), 0, s, fa, u);
+        return;
+    }
     switch (fa.cin) {
     case 1: hipLaunchKernelGGL((syn_fused_kernel<1, CMID, false>), grid, dim3(kFThreads), 0, s, fa, u); break;
 #define CCMI_FUSED_CASE(N) \
@@ -983,6 +1011,9 @@ extern "C" int ccmi_decode_forward_f32(const ccmi_decode_args *a, void *stream)
     LevelArgs last{};
     if (int rc = ups_pyramid(&u, s, &last, (stages & 1) != 0)) return rc;
     if (!(stages & 2)) return CCMI_OK;
+    if ((int64_t)4 * last.C * last.hs * last.ws >= ((int64_t)1 << 31) || (int64_t)4 * last.hd * last.wd >= ((int64_t)1 << 31))
+        return ccmi_set_error(CCMI_ERR_UNSUPPORTED, "decode: level-1 stack of %d x %d x %d exceeds 2 GB buffer addressing", last.C,
+                              last.hs, last.ws);
     P.fa.in = nullptr;
     P.fa.params = y.params;
     P.fa.pstride = y.param_stride;

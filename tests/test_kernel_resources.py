@@ -17,8 +17,9 @@ LLVM = Path("/opt/rocm/lib/llvm/bin")
 
 # demangled-name prefix -> (max VGPRs, max VGPR spills, scratch bytes allowed)
 BUDGET = {
-    "syn_fused_kernel<7, 3, true, false>": (128, 0, 0),   # path A headline (hop, 7 grids)
-    "syn_fused_kernel<7, 4, true, false>": (128, 0, 0),
+    "syn_fused_kernel<7, 3, true, false, 0>": (128, 0, 0),  # path A, 7 grids, any head width
+    "syn_fused_kernel<7, 4, true, false, 0>": (128, 0, 0),
+    "syn_fused_kernel<7, 3, true, false, 48>": (128, 0, 0),  # path A headline (hop): unrolled head
     "arm_fwd_kernel<16>": (128, 0, 0),                      # path A ARM + rate
     "ups_level_fixed<8, 7>": (64, 0, 0),                    # upsampling pyramid
     "dec_arm_kernel<16, 2>": (128, 0, 0),                   # path B ARM + CABAC
