@@ -235,7 +235,8 @@ __global__ __launch_bounds__(kFThreads) __attribute__((amdgpu_waves_per_eu(4))) 
             // (channel, row) of r = wv + 8u in 32-bit scalar registers (a frame's stack stays
             // below 2 GB; checked at launch)
             const int splane = U.hs * U.ws;
-            const uint32_t scol = 4u * (uint32_t)clampi(ibase + lane, U.ws - 1);
+            // lanes past the tile re-read the last column (same cache lines, no extra fetch)
+            const uint32_t scol = 4u * (uint32_t)clampi(ibase + (lane < kSW ? lane : kSW - 1), U.ws - 1);
 #pragma unroll
             for (int u = 0; u < kSU; ++u) {
                 const int r = wv + 8 * u;
@@ -257,8 +258,8 @@ __global__ __launch_bounds__(kFThreads) __attribute__((amdgpu_waves_per_eu(4))) 
             bool tin[2];
 #pragma unroll
             for (int h = 0; h < 2; ++h) {
-                const int X = Xa - 3 + lane + 64 * h;
-                tin[h] = X >= 0 && X < U.wd && lane + 64 * h < kTW;
+                const int X = Xa - 3 + (lane + 64 * h < kTW ? lane + 64 * h : kTW - 1);
+                tin[h] = X >= 0 && X < U.wd;
                 tx[h] = 4u * (uint32_t)clampi(X, U.wd - 1);
             }
 #pragma unroll
@@ -812,7 +813,10 @@ void launch_fused(dim3 grid, hipStream_t s, const FusedArgs &fa, const LevelArgs
     // the presets' 7-grid decoders with a 48-wide head (hop and its relatives): unrolled head
     static const bool generic_head = getenv("CCMI_SYN_HEAD_LOOP") != nullptr; // A/B switch
     if (fa.cin == 7 && fa.n_head == 2 && fa.hid == 48 && !generic_head) {
-        hipLaunchKernelGGL((syn_fused_kernel<7, CMID, UPS, false, 48>), grid, dim3(kFThreads), 0, s, fa, u);
+        // CCMI_SYN_LDS_PAD (experiments only): extra dynamic LDS per workgroup, to measure how
+        // the kernel responds to fewer resident workgroups per CU
+        static const int pad = getenv("CCMI_SYN_LDS_PAD") ? atoi(getenv("CCMI_SYN_LDS_PAD")) : 0;
+        hipLaunchKernelGGL((syn_fused_kernel<7, CMID, UPS, false, 48>), grid, dim3(kFThreads), pad, s, fa, u);
         return;
     }
     switch (fa.cin) {
