@@ -132,28 +132,49 @@ constexpr int kHrRows = kRH + 7 - 1;              // refine rows incl. the 7-tap
 constexpr int kSW = kRW / 2 + 1 + FT::NS - 1 + 3; // raw source tile pitch (37 used)
 constexpr int kTW = kRW + 7 - 1 + 2;              // raw latent tile pitch (70 used, 72 read)
 
+// Fused upsampling stages the level-1 channels in NG groups of GC (one group's raw tile and
+// horizontal passes in LDS at a time), and the head's weight records live in region 1 once the
+// gathers are done: 52 KB of LDS for the 7-grid hop decoder, three resident workgroups per CU
+// (measured: one workgroup per CU instead of two costs +41 %, tools/occ_probe.sh).
+constexpr int fused_groups(int cin, bool ups) { return ups && cin - 1 >= 4 ? 2 : 1; }
+constexpr int fused_lds_floats(int cin, int cmid, bool ups)
+{
+    const int C = ups ? cin - 1 : 0, GC = (C + fused_groups(cin, ups) - 1) / fused_groups(cin, ups);
+    const int raw = ups ? GC * kHsRows * kSW + kHrRows * kTW : 0;
+    const int stage = ups ? GC * kHsRows * kRW + kHrRows * kRW : 0;
+    const int b0 = cmid * kPlane > raw ? cmid * kPlane : raw;
+    int b1 = cmid * kPlane > stage ? cmid * kPlane : stage;
+    b1 = b1 > kMaxHid * 16 ? b1 : kMaxHid * 16;
+    return b0 + b1 + 256; // + the 8-bit quotient table
+}
+// waves per SIMD the register allocation must allow: 3 workgroups of 8 waves on 4 SIMDs when
+// the LDS fits three (<= 160 KB / 3), else 2
+constexpr int fused_wpe(int cin, int cmid, bool ups) { return 4 * fused_lds_floats(cin, cmid, ups) <= 160 * 1024 / 3 ? 6 : 4; }
+
 // MH: split-f16 MFMA first head layer (a separate instantiation: compiled into the default
 // kernel as a runtime branch, its registers pushed the VALU variant from 108 to 133 VGPRs,
 // i.e. from 4 to 3 waves per SIMD, and decode_fused from 0.97 to 1.40 ms per 32 frames)
 // HID > 0: the 2-layer head's hidden width fixed at compile time (fully unrolled unit loop:
 // weight records at immediate LDS offsets, no loop counter or record rotation)
 template <int CIN, int CMID, bool UPS, bool MH = false, int HID = 0>
-__global__ __launch_bounds__(kFThreads) __attribute__((amdgpu_waves_per_eu(4))) void syn_fused_kernel(FusedArgs A, LevelArgs U)
+__global__ __launch_bounds__(kFThreads) __attribute__((amdgpu_waves_per_eu(fused_wpe(CIN, CMID, UPS)))) void syn_fused_kernel(FusedArgs A, LevelArgs U)
 {
     constexpr int NR = kRowsPerThread;
-    // region 0: raw input tiles (UPS, phase A-B), then the head output / 3x3 buffer 0
-    // region 1: horizontal-pass results (UPS, phase B-C), then the 3x3 buffer 1
-    constexpr int kRaw = UPS ? (CIN - 1) * kHsRows * kSW + kHrRows * kTW : 0;
-    constexpr int kStage = UPS ? (CIN - 1) * kHsRows * kRW + kHrRows * kRW : 0;
+    constexpr int C = UPS ? CIN - 1 : 0, NG = fused_groups(CIN, UPS), GC = (C + NG - 1) / NG;
+    // region 0: raw input tiles of a channel group (UPS, phases A-B), then the head output /
+    // 3x3 buffer 0; region 1: the group's horizontal-pass results (UPS), then the head's
+    // weight records, then the 3x3 buffer 1
+    constexpr int kRaw = UPS ? GC * kHsRows * kSW + kHrRows * kTW : 0;
     constexpr int kBuf0 = CMID * kPlane > kRaw ? CMID * kPlane : kRaw;
-    constexpr int kBuf1 = CMID * kPlane > kStage ? CMID * kPlane : kStage;
-    __shared__ __attribute__((aligned(16))) float s_pool[kBuf0 + kBuf1];
+    constexpr int kTot = fused_lds_floats(CIN, CMID, UPS);
+    __shared__ __attribute__((aligned(16))) float s_pool[kTot];
     float(*s_buf0)[kPlane] = reinterpret_cast<float(*)[kPlane]>(s_pool);
     float(*s_buf1)[kPlane] = reinterpret_cast<float(*)[kPlane]>(s_pool + kBuf0);
-    float *s_st = s_pool;                           // [CIN-1][kHsRows][kSW] raw source tile (UPS only)
-    float *s_yt = s_st + (CIN - 1) * kHsRows * kSW; // [kHrRows][kTW] raw latent tile (UPS only)
-    float *s_hs = s_pool + kBuf0;                   // [CIN-1][kHsRows][kRW]   (UPS only)
-    float *s_hr = s_hs + (CIN - 1) * kHsRows * kRW; // [kHrRows][kRW]          (UPS only)
+    float *s_st = s_pool;                      // [GC][kHsRows][kSW] raw source tile (UPS only)
+    float *s_yt = s_st + GC * kHsRows * kSW;   // [kHrRows][kTW] raw latent tile (UPS only)
+    float *s_hs = s_pool + kBuf0;              // [GC][kHsRows][kRW]   (UPS only)
+    float *s_hr = s_hs + GC * kHsRows * kRW;   // [kHrRows][kRW]       (UPS only)
+    float *s_lut8 = s_pool + kTot - 256;
     auto buf = [&](int which) { return which ? s_buf1 : s_buf0; };
 #if defined(CCMI_ARM_STAMPS)
     unsigned long long t_prev = __builtin_amdgcn_s_memtime();
@@ -161,7 +182,7 @@ __global__ __launch_bounds__(kFThreads) __attribute__((amdgpu_waves_per_eu(4))) 
     // head hidden unit j as 16 floats: w0[j][0..CIN), b0[j], w1[0..CMID)[j]; read back as
     // four broadcast ds_read_b128 (all lanes, one address) -- the loads are issued well
     // ahead of use, unlike the SGPR path whose scalar loads the compiler waits on at once
-    __shared__ __attribute__((aligned(16))) float s_head[kMaxHid][16];
+    float(*s_head)[16] = reinterpret_cast<float(*)[16]>(s_pool + kBuf0);
     static_assert(CIN + 1 + CMID <= 16, "hidden-unit record");
     // field f of a record sits at slot hr(f): slots 3, 7, 11, 15 (the last dword of each
     // ds_read_b128) stay empty when the fields fit without them, because the compiler
@@ -184,78 +205,93 @@ __global__ __launch_bounds__(kFThreads) __attribute__((amdgpu_waves_per_eu(4))) 
     const int gx = ox + c;
     const int cxg = clampi(gx, A.W - 1);
 
-    __shared__ float s_lut8[256];
     const float *lut8 = A.qmax == 255.f ? s_lut8 : nullptr;
-    // per-frame tables in LDS (8-bit output quotients, head weight records); with fused
-    // upsampling this runs while the raw tile loads are in flight, and the phase-A
-    // barrier publishes it
-    auto stage_tables = [&]() {
-        if (lut8) s_lut8[threadIdx.x & 255] = (float)(threadIdx.x & 255) / 255.f;
-        if (A.n_head == 2)
-            for (int i = threadIdx.x; i < A.hid * 16; i += kFThreads) {
-                const int j = i >> 4, f = i & 15;
-                float v = 0.f;
-                if (f < CIN) v = prm[A.w0_off + j * CIN + f];
-                else if (f == CIN) v = prm[A.b0_off + j];
-                else if (f <= CIN + CMID) v = prm[A.w1_off + (f - CIN - 1) * A.hid + j];
-                if (f <= CIN + CMID) s_head[j][hr(f)] = v; // other slots are never operands
-            }
+    // per-frame tables in LDS: the 8-bit output quotients (own area, staged at once) and the
+    // head's weight records (region 1: before anything else without fused upsampling, after
+    // the gathers with it -- the values are fetched into registers up front, kHeadRegs each)
+    if (lut8) s_lut8[threadIdx.x & 255] = (float)(threadIdx.x & 255) / 255.f;
+    constexpr int kHeadRegs = kMaxHid * 16 / kFThreads;
+    float hv[kHeadRegs];
+#pragma unroll
+    for (int k = 0; k < kHeadRegs; ++k) {
+        const int i = threadIdx.x + k * kFThreads, j = i >> 4, f = i & 15;
+        float v = 0.f;
+        if (A.n_head == 2 && j < A.hid) {
+            if (f < CIN) v = prm[A.w0_off + j * CIN + f];
+            else if (f == CIN) v = prm[A.b0_off + j];
+            else if (f <= CIN + CMID) v = prm[A.w1_off + (f - CIN - 1) * A.hid + j];
+        }
+        hv[k] = v;
+    }
+    auto stage_head = [&]() {
+#pragma unroll
+        for (int k = 0; k < kHeadRegs; ++k) {
+            const int i = threadIdx.x + k * kFThreads, j = i >> 4, f = i & 15;
+            if (f <= CIN + CMID) s_head[j][hr(f)] = hv[k]; // other slots are never operands
+        }
     };
     if constexpr (!UPS) {
-        stage_tables();
+        stage_head();
         __syncthreads();
     }
 
+    float x[NR][CIN];
     // window's clamped image origin (fused upsampling only)
     const int Ya = clampi(oy, A.H - 1), Xa = clampi(ox, A.W - 1);
-    float wu[8], wr[7];
+    // interior windows (no row clamping): the thread's 4 rows are consecutive, so the
+    // vertical passes share their LDS rows -- 10 refine rows and 6 or 7 half-res rows per
+    // channel for 4 pixels, offsets fixed by the parity of the window's first row
+    const bool interior = oy >= 0 && oy + kRH <= A.H;
     if constexpr (UPS) {
-        constexpr int C = CIN - 1;
+        float wu[8], wr[7];
         const float *uprm = U.params + (int64_t)b * U.pstride;
 #pragma unroll
         for (int k = 0; k < 8; ++k) wu[k] = uprm[U.up_off + k];
 #pragma unroll
         for (int k = 0; k < 7; ++k) wr[k] = uprm[U.pre_off + k];
         const int jbase = Ya / 2 + FT::D0, ibase = Xa / 2 + FT::D0;
-        // Phases A + B are row-parallel and wave-private: wave wv owns raw source rows
-        // r = wv + 8u of the [C][kHsRows] tile and raw latent rows yr = wv + 8u; lane = column.
+        // Phases A + B are row-parallel and wave-private: wave wv owns the rows r = wv + 8u of
+        // a group's [GC][kHsRows] raw tile and the raw latent rows yr = wv + 8u; lane = column.
         // Row addresses are wave-uniform (scalar), so a load costs no VALU index math, and a
         // wave's horizontal passes read back only rows it wrote itself -- a wave-level fence
         // instead of a workgroup barrier between the raw tiles and the horizontal passes.
         const int wv = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
         const int lane = threadIdx.x & 63;
-        constexpr int kSR = C * kHsRows, kSU = (kSR + 7) / 8;     // source rows, per wave
-        constexpr int kLU = (kHrRows + 7) / 8;                    // latent rows per wave
+        constexpr int kSR = GC * kHsRows, kSU = (kSR + 7) / 8; // a group's source rows, per wave
+        constexpr int kLU = (kHrRows + 7) / 8;                 // latent rows per wave
         static_assert(kSW <= 64 && kTW <= 128 && kTW > 64 && kHsRows >= 8, "lane = raw column, one row wrap per step");
         const float *src = U.src + (int64_t)b * U.src_stride;
         const float *rs = U.ref_src + (int64_t)b * U.ref_stride;
-        float sv[kSU], tv[kLU][2];
+        float sv[NG][kSU], tv[kLU][2];
+        bool tin[2];
+        // phase A: every group's raw rows and the latent tile, all loads in flight at once;
+        // clamped source coordinates are always inside the stack.  (channel, row) of
+        // r = wv + 8u in 32-bit scalar registers (a frame's stack stays below 2 GB; checked
+        // at launch)
         {
-            // phase A: raw tiles; clamped source coordinates are always inside the stack
-            // (channel, row) of r = wv + 8u in 32-bit scalar registers (a frame's stack stays
-            // below 2 GB; checked at launch)
             const int splane = U.hs * U.ws;
             // lanes past the tile re-read the last column (same cache lines, no extra fetch)
             const uint32_t scol = 4u * (uint32_t)clampi(ibase + (lane < kSW ? lane : kSW - 1), U.ws - 1);
 #pragma unroll
-            for (int u = 0; u < kSU; ++u) {
-                const int r = wv + 8 * u;
-                // ch = r / kHsRows without a division: wv < 8 moves r past at most one boundary
-                const int c0 = (8 * u) / kHsRows, tb = kHsRows * (c0 + 1) - 8 * u; // folded (u unrolled)
-                const int ch = c0 + (wv >= tb ? 1 : 0), jj = r - ch * kHsRows;
-                sv[u] = 0.f;
-                if (u < kSU - 1 || r < kSR) {
-                    const int row = ch * splane + clampi(jbase + jj, U.hs - 1) * U.ws;
+            for (int G = 0; G < NG; ++G)
+#pragma unroll
+                for (int u = 0; u < kSU; ++u) {
+                    const int r = wv + 8 * u;
+                    // ch = r / kHsRows without a division: wv < 8 moves r past at most one boundary
+                    const int c0 = (8 * u) / kHsRows, tb = kHsRows * (c0 + 1) - 8 * u; // folded (u unrolled)
+                    const int lc = c0 + (wv >= tb ? 1 : 0), jj = r - lc * kHsRows;
+                    sv[G][u] = 0.f;
+                    if ((u < kSU - 1 || r < kSR) && G * GC + lc < C) {
+                        const int row = (G * GC + lc) * splane + clampi(jbase + jj, U.hs - 1) * U.ws;
 #if defined(CCMI_DIAG_NOLOAD) // diagnostic build only: phase A without its global loads
-                    sv[u] = 0.001f * (float)(jj + scol);
+                        sv[G][u] = 0.001f * (float)(jj + scol);
 #else
-                    sv[u] = ldu(src + row, scol);
+                        sv[G][u] = ldu(src + row, scol);
 #endif
+                    }
                 }
-            }
             // latent tile: zero outside the image (the refine's zero padding)
             uint32_t tx[2];
-            bool tin[2];
 #pragma unroll
             for (int h = 0; h < 2; ++h) {
                 const int X = Xa - 3 + (lane + 64 * h < kTW ? lane + 64 * h : kTW - 1);
@@ -276,94 +312,89 @@ __global__ __launch_bounds__(kFThreads) __attribute__((amdgpu_waves_per_eu(4))) 
 #endif
                 }
             }
-            stage_tables();
+        }
+        f2 wp[FT::NS];
+#pragma unroll
+        for (int m = 0; m < FT::NS; ++m) {
+            const int te = FT::tap(0, FT::D0 + m), to = FT::tap(1, FT::D0 + m);
+            wp[m] = f2{te >= 0 ? wu[te] : 0.f, to >= 0 ? wu[to] : 0.f};
+        }
+        auto group = [&](auto GI) {
+            constexpr int G = decltype(GI)::value;
+            if constexpr (G > 0) __syncthreads(); // every wave done with the previous group
 #pragma unroll
             for (int u = 0; u < kSU; ++u) {
                 const int r = wv + 8 * u;
-                if ((u < kSU - 1 || r < kSR) && lane < kSW) s_st[r * kSW + lane] = U.src_quant ? rintf(U.gain * sv[u]) : sv[u];
+                if ((u < kSU - 1 || r < kSR) && lane < kSW)
+                    s_st[r * kSW + lane] = U.src_quant ? rintf(U.gain * sv[G][u]) : sv[G][u];
             }
+            if constexpr (G == 0) {
 #pragma unroll
-            for (int u = 0; u < kLU; ++u) {
-                const int yr = wv + 8 * u;
-                if (yr >= kHrRows) continue;
-                const int Y = Ya - 3 + yr;
-                const bool yin = Y >= 0 && Y < U.hd;
+                for (int u = 0; u < kLU; ++u) {
+                    const int yr = wv + 8 * u;
+                    if (yr >= kHrRows) continue;
+                    const int Y = Ya - 3 + yr;
+                    const bool yin = Y >= 0 && Y < U.hd;
 #pragma unroll
-                for (int h = 0; h < 2; ++h) {
-                    const float v = U.ref_quant ? rintf(U.gain * tv[u][h]) : tv[u][h];
-                    if (lane + 64 * h < kTW) s_yt[yr * kTW + lane + 64 * h] = (yin && tin[h]) ? v : 0.f;
+                    for (int h = 0; h < 2; ++h) {
+                        const float v = U.ref_quant ? rintf(U.gain * tv[u][h]) : tv[u][h];
+                        if (lane + 64 * h < kTW) s_yt[yr * kTW + lane + 64 * h] = (yin && tin[h]) ? v : 0.f;
+                    }
                 }
             }
-        }
-        // the wave reads back rows it wrote (other lanes' columns): order its LDS accesses
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-        __builtin_amdgcn_wave_barrier();
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-        FSTAMP(0);
-        // phase B: horizontal passes, in ups_level_fixed's operation order.  Transposed conv:
-        // lane = (row half, pair k = lane & 31); the (even, odd) outputs of pair k read source
-        // columns k .. k + NS - 1 and land in window columns 2k - (Xa & 1), +1.
-        {
-            f2 wp[FT::NS];
+            // the wave reads back rows it wrote (other lanes' columns): order its LDS accesses
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+            __builtin_amdgcn_wave_barrier();
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+            if constexpr (G == 0) FSTAMP(0);
+            // phase B: horizontal passes, in ups_level_fixed's operation order.  Transposed
+            // conv: lane = (row half, pair k = lane & 31); the (even, odd) outputs of pair k read
+            // source columns k .. k + NS - 1 and land in window columns 2k - (Xa & 1), +1.
+            {
+                const int odd = Xa & 1;
+                const int k = lane & 31, hsel = lane >> 5;
+                const int xe = 2 * k - odd;
+                static_assert(32 + FT::NS - 1 < kSW, "pair 32 reads stay inside the source row");
+                auto pair = [&](int r, int kk, int xw) {
+                    const float *sr = s_st + r * kSW + kk;
+                    f2 eo = f2(0.f);
 #pragma unroll
-            for (int m = 0; m < FT::NS; ++m) {
-                const int te = FT::tap(0, FT::D0 + m), to = FT::tap(1, FT::D0 + m);
-                wp[m] = f2{te >= 0 ? wu[te] : 0.f, to >= 0 ? wu[to] : 0.f};
+                    for (int m = 0; m < FT::NS; ++m) eo = __builtin_elementwise_fma(wp[m], f2(sr[m]), eo);
+                    float *hrow = s_hs + r * kRW;
+                    if (xw >= 0) hrow[xw] = eo.x;
+                    if (xw + 1 < kRW) hrow[xw + 1] = eo.y;
+                };
+#pragma unroll
+                for (int u = 0; u < kSU; u += 2) {
+                    const int r = wv + 8 * (u + hsel);
+                    if (u + 1 < kSU - 1 || r < kSR) pair(r, k, xe);
+                }
+                if (odd) { // pair 32 of every row (window columns 63, 64)
+                    const int r = wv + 8 * lane;
+                    if (lane < kSU && r < kSR) pair(r, 32, 63);
+                }
+                if constexpr (G == 0) {
+                    // refine: lane = window column, 7-tap sliding window over the wave's latent rows
+#pragma unroll
+                    for (int u = 0; u < kLU; ++u) {
+                        const int yr = wv + 8 * u;
+                        if (yr >= kHrRows) continue;
+                        const float *tr = s_yt + yr * kTW + lane;
+                        float acc = 0.f;
+#pragma unroll
+                        for (int q = 0; q < 7; ++q) acc = fmaf(wr[q], tr[q], acc);
+                        s_hr[yr * kRW + lane] = acc;
+                    }
+                }
             }
-            const int odd = Xa & 1;
-            const int k = lane & 31, hsel = lane >> 5;
-            const int xe = 2 * k - odd;
-            static_assert(32 + FT::NS - 1 < kSW, "pair 32 reads stay inside the source row");
-            auto pair = [&](int r, int kk, int xw) {
-                const float *sr = s_st + r * kSW + kk;
-                f2 eo = f2(0.f);
-#pragma unroll
-                for (int m = 0; m < FT::NS; ++m) eo = __builtin_elementwise_fma(wp[m], f2(sr[m]), eo);
-                float *hr = s_hs + r * kRW;
-                if (xw >= 0) hr[xw] = eo.x;
-                if (xw + 1 < kRW) hr[xw + 1] = eo.y;
-            };
-#pragma unroll
-            for (int u = 0; u < kSU; u += 2) {
-                const int r = wv + 8 * (u + hsel);
-                if (u + 1 < kSU - 1 || r < kSR) pair(r, k, xe);
-            }
-            if (odd) { // pair 32 of every row (window columns 63, 64)
-                const int r = wv + 8 * lane;
-                if (lane < kSU && r < kSR) pair(r, 32, 63);
-            }
-            // refine: lane = window column, 7-tap sliding window over the wave's latent rows
-#pragma unroll
-            for (int u = 0; u < kLU; ++u) {
-                const int yr = wv + 8 * u;
-                if (yr >= kHrRows) continue;
-                const float *tr = s_yt + yr * kTW + lane;
-                float acc = 0.f;
-#pragma unroll
-                for (int q = 0; q < 7; ++q) acc = fmaf(wr[q], tr[q], acc);
-                s_hr[yr * kRW + lane] = acc;
-            }
-        }
-        __syncthreads();
-    }
-
-    FSTAMP(1);
-    // ------------------------ pass 0: per-pixel 1x1 head ------------------------
-    {
-        const cfloat_ptr w0 = prm + A.w0_off, b0 = prm + A.b0_off;
-        const cfloat_ptr b1 = prm + A.b1_off;
-        float x[NR][CIN];
-        float o[NR][CMID];
-        // interior windows (no row clamping): the thread's 4 rows are consecutive, so the
-        // vertical passes share their LDS rows -- 10 refine rows and 6 or 7 half-res rows
-        // per channel for 4 pixels, offsets fixed by the parity of the window's first row
-        bool done = false;
-        if constexpr (UPS) {
-            if (oy >= 0 && oy + kRH <= A.H) {
-                const int xi = cxg - Xa;
+            __syncthreads();
+            if constexpr (G == 0) FSTAMP(1);
+            // gather: the vertical passes of this group's channels (+ the refine for G = 0)
+            const int xi = cxg - Xa;
+            if (interior) {
                 auto gather = [&](auto par) {
                     constexpr int P = decltype(par)::value; // parity of oy (and of row rb)
-                    {
+                    if constexpr (G == 0) {
                         float h[NR + 6];
 #pragma unroll
                         for (int k = 0; k < NR + 6; ++k) h[k] = s_hr[(rb + k) * kRW + xi];
@@ -378,10 +409,14 @@ __global__ __launch_bounds__(kFThreads) __attribute__((amdgpu_waves_per_eu(4))) 
                     constexpr int NH = FT::NS + (NR / 2) - 1 + P; // half-res rows for 4 pixels
                     const int j0 = rb / 2;
 #pragma unroll
-                    for (int k = 1; k < CIN; ++k) {
+                    for (int lc = 0; lc < GC; ++lc) {
+                        constexpr int dummy = 0;
+                        (void)dummy;
+                        const int k = 1 + G * GC + lc;
+                        if (k >= CIN) break;
                         float h[NH];
 #pragma unroll
-                        for (int m = 0; m < NH; ++m) h[m] = s_hs[((k - 1) * kHsRows + j0 + m) * kRW + xi];
+                        for (int m = 0; m < NH; ++m) h[m] = s_hs[(lc * kHsRows + j0 + m) * kRW + xi];
 #pragma unroll
                         for (int p = 0; p < NR; ++p) {
                             const int a = (P + p) & 1, off = (P + p) >> 1;
@@ -397,43 +432,58 @@ __global__ __launch_bounds__(kFThreads) __attribute__((amdgpu_waves_per_eu(4))) 
                 };
                 if (oy & 1) gather(std::integral_constant<int, 1>{});
                 else gather(std::integral_constant<int, 0>{});
-                done = true;
+            } else {
+#pragma unroll
+                for (int p = 0; p < NR; ++p) {
+                    // vertical passes at the clamped row, in ups_level_fixed's operation order
+                    const int Y = clampi(oy + rb + p, A.H - 1);
+                    const int yi = Y - Ya;
+                    if constexpr (G == 0) {
+                        float acc = 0.f;
+#pragma unroll
+                        for (int k = 0; k < 7; ++k) acc = fmaf(wr[k], s_hr[(yi + k) * kRW + xi], acc);
+                        // residual: the (quantised) latent, from the raw tile still in LDS
+                        x[p][0] = acc + s_yt[(yi + 3) * kTW + xi + 3];
+                    }
+                    const int jj0 = Y / 2 - Ya / 2, a = Y & 1;
+#pragma unroll
+                    for (int lc = 0; lc < GC; ++lc) {
+                        const int k = 1 + G * GC + lc;
+                        if (k >= CIN) break;
+                        const float *h = s_hs + (lc * kHsRows + jj0) * kRW + xi;
+                        float acc = 0.f;
+#pragma unroll
+                        for (int m = 0; m < FT::NS; ++m) {
+                            const int te = FT::tap(0, FT::D0 + m), to = FT::tap(1, FT::D0 + m);
+                            if ((a ? to : te) >= 0) acc = fmaf(wu[a ? to : te], h[m * kRW], acc);
+                        }
+                        x[p][k] = acc;
+                    }
+                }
             }
-        }
+        };
+        group(std::integral_constant<int, 0>{});
+        if constexpr (NG > 1) group(std::integral_constant<int, 1>{});
+    } else {
 #pragma unroll
         for (int p = 0; p < NR; ++p) {
-            if (done) break;
-            const int Y = clampi(oy + rb + p, A.H - 1);
-            if constexpr (UPS) {
-                // vertical passes, in ups_level_fixed's operation order
-                const int xi = cxg - Xa, yi = Y - Ya;
-                {
-                    float acc = 0.f;
+            const int64_t pix = (int64_t)clampi(oy + rb + p, A.H - 1) * A.W + cxg;
 #pragma unroll
-                    for (int k = 0; k < 7; ++k) acc = fmaf(wr[k], s_hr[(yi + k) * kRW + xi], acc);
-                    // residual: the (quantised) latent, from the raw tile still in LDS
-                    x[p][0] = acc + s_yt[(yi + 3) * kTW + xi + 3];
-                }
-                const int jj0 = Y / 2 - Ya / 2, a = Y & 1;
-#pragma unroll
-                for (int k = 1; k < CIN; ++k) {
-                    const float *h = s_hs + ((k - 1) * kHsRows + jj0) * kRW + xi;
-                    float acc = 0.f;
-#pragma unroll
-                    for (int m = 0; m < FT::NS; ++m) {
-                        const int te = FT::tap(0, FT::D0 + m), to = FT::tap(1, FT::D0 + m);
-                        if ((a ? to : te) >= 0) acc = fmaf(wu[a ? to : te], h[m * kRW], acc);
-                    }
-                    x[p][k] = acc;
-                }
-            } else {
-                const int64_t pix = (int64_t)Y * A.W + cxg;
-#pragma unroll
-                for (int k = 0; k < CIN; ++k) x[p][k] = in[k * plane + pix];
-            }
+            for (int k = 0; k < CIN; ++k) x[p][k] = in[k * plane + pix];
         }
-        // the raw tiles (region 0) are overwritten by the head output below
-        if constexpr (UPS) __syncthreads();
+    }
+
+    // ------------------------ pass 0: per-pixel 1x1 head ------------------------
+    {
+        const cfloat_ptr w0 = prm + A.w0_off, b0 = prm + A.b0_off;
+        const cfloat_ptr b1 = prm + A.b1_off;
+        float o[NR][CMID];
+        // region 1 (the last group's horizontal passes) is free once every wave has gathered:
+        // the head's weight records go there
+        if constexpr (UPS) {
+            __syncthreads();
+            stage_head();
+        }
         FSTAMP(2);
         if constexpr (MH) {
             // ---- split-f16 MFMA first layer, second layer on VALU from the accumulators
