@@ -1067,7 +1067,12 @@ __global__ __launch_bounds__(kT) void t_sp_bwd(const float *__restrict__ gout, c
 #else
 #define HEAD_MFMA(a, b, c) mfma4(a, b, c)
 #endif
-template <int CIN, int NT>
+// PAIR (default; CCMI_HEAD_BWD_OLD=1 keeps the unit-at-a-time form for A/B): the per-pixel
+// work runs over PAIRS of hidden units with packed FMAs -- records interleave the two units'
+// weights ({w0[j][i], w0[j+1][i]}, {b0[j], b0[j+1]}, {w1[k][j], w1[k][j+1]}), so every
+// packed operand is an aligned register pair -- and the output / g_x sums keep one partial
+// per unit parity, added at the end: 26 VALU per unit pair instead of 46.
+template <int CIN, int NT, bool PAIR>
 __global__ __launch_bounds__(kHeadT) void t_head_bwd(const float *__restrict__ dense, const float *__restrict__ gz0, Geo g,
                                                      const float *__restrict__ th, int64_t ps, float *__restrict__ gdense,
                                                      float *__restrict__ gth, int64_t gstride)
@@ -1087,15 +1092,32 @@ __global__ __launch_bounds__(kHeadT) void t_head_bwd(const float *__restrict__ d
     constexpr int hp = 16 * NT + 1;
     const int64_t npx = (int64_t)g.H * g.W;
     const float *P = th + (int64_t)b * ps;
-    for (int e = t; e < 64 * 12; e += kHeadT) {
-        const int j = e / 12, f = e - j * 12;
-        float v = 0.f;
-        if (j < hid) {
-            if (f < CIN) v = P[g.w0 + j * CIN + f];
-            else if (f == CIN) v = P[g.b0 + j];
-            else if (f <= CIN + 3) v = P[g.w1 + (f - CIN - 1) * hid + j];
+    // pair records: unit pair jp = units 2jp, 2jp + 1, field f interleaved as [2f + parity]
+    constexpr int kPR = 2 * (CIN + 4) <= 24 ? 24 : 32;
+    float(*s_rec2)[kPR] = reinterpret_cast<float(*)[kPR]>(&s_rec[0][0]);
+    static_assert(32 * kPR <= 64 * 12, "pair records fit in the record area");
+    if constexpr (!PAIR) {
+        for (int e = t; e < 64 * 12; e += kHeadT) {
+            const int j = e / 12, f = e - j * 12;
+            float v = 0.f;
+            if (j < hid) {
+                if (f < CIN) v = P[g.w0 + j * CIN + f];
+                else if (f == CIN) v = P[g.b0 + j];
+                else if (f <= CIN + 3) v = P[g.w1 + (f - CIN - 1) * hid + j];
+            }
+            s_rec[j][f] = v;
         }
-        s_rec[j][f] = v;
+    } else {
+        for (int e = t; e < 32 * kPR; e += kHeadT) {
+            const int jp = e / kPR, r = e - jp * kPR, f = r >> 1, j = 2 * jp + (r & 1);
+            float v = 0.f;
+            if (j < hid) {
+                if (f < CIN) v = P[g.w0 + j * CIN + f];
+                else if (f == CIN) v = P[g.b0 + j];
+                else if (f <= CIN + 3) v = P[g.w1 + (f - CIN - 1) * hid + j];
+            }
+            s_rec2[jp][r] = v;
+        }
     }
     const float bo0 = P[g.b1], bo1 = P[g.b1 + 1], bo2 = P[g.b1 + 2];
     float *sv = s_dyn + w * 64 * (hp + kXP), *sw = sv + 64 * hp;
@@ -1121,17 +1143,38 @@ __global__ __launch_bounds__(kHeadT) void t_head_bwd(const float *__restrict__ d
         gp1[2] = valid ? G[2 * npx] : 0.f;
         // ---- hidden layer (kept in this lane's LDS row) and the output pre-activations
         float o0 = bo0, o1 = bo1, o2 = bo2;
-#pragma unroll 4
-        for (int j = 0; j < hid; ++j) {
-            HEAD_BWD_REC(r, j);
-            float a = r[CIN];
+        if constexpr (PAIR) {
+            using ccmi_fwd::f2;
+            const f2 lo0 = f2(g.r0 ? 0.f : -INFINITY);
+            f2 op[3] = {f2(0.f), f2(0.f), f2(0.f)};
+#pragma unroll 2
+            for (int jp = 0; jp < (hid + 1) / 2; ++jp) {
+                const f2 *r = reinterpret_cast<const f2 *>(s_rec2[jp]);
+                f2 a = r[CIN];
 #pragma unroll
-            for (int i = 0; i < CIN; ++i) a = fmaf(r[i], xv[i], a);
-            if (g.r0) a = fmaxf(a, 0.f);
-            sv[lane * hp + j] = a;
-            o0 = fmaf(r[CIN + 1], a, o0);
-            o1 = fmaf(r[CIN + 2], a, o1);
-            o2 = fmaf(r[CIN + 3], a, o2);
+                for (int i = 0; i < CIN; ++i) a = __builtin_elementwise_fma(r[i], f2(xv[i]), a);
+                a = __builtin_elementwise_max(a, lo0);
+                sv[lane * hp + 2 * jp] = a.x;
+                sv[lane * hp + 2 * jp + 1] = a.y;
+#pragma unroll
+                for (int k = 0; k < 3; ++k) op[k] = __builtin_elementwise_fma(r[CIN + 1 + k], a, op[k]);
+            }
+            o0 += op[0].x + op[0].y;
+            o1 += op[1].x + op[1].y;
+            o2 += op[2].x + op[2].y;
+        } else {
+#pragma unroll 4
+            for (int j = 0; j < hid; ++j) {
+                HEAD_BWD_REC(r, j);
+                float a = r[CIN];
+#pragma unroll
+                for (int i = 0; i < CIN; ++i) a = fmaf(r[i], xv[i], a);
+                if (g.r0) a = fmaxf(a, 0.f);
+                sv[lane * hp + j] = a;
+                o0 = fmaf(r[CIN + 1], a, o0);
+                o1 = fmaf(r[CIN + 2], a, o1);
+                o2 = fmaf(r[CIN + 3], a, o2);
+            }
         }
         if (g.r1) {
             if (o0 <= 0.f) gp1[0] = 0.f;
@@ -1157,14 +1200,39 @@ __global__ __launch_bounds__(kHeadT) void t_head_bwd(const float *__restrict__ d
         float gxv[CIN];
 #pragma unroll
         for (int i = 0; i < CIN; ++i) gxv[i] = 0.f;
-#pragma unroll 4
-        for (int j = 0; j < hid; ++j) {
-            HEAD_BWD_REC(r, j);
-            float gh = r[CIN + 1] * gp1[0] + r[CIN + 2] * gp1[1] + r[CIN + 3] * gp1[2];
-            if (g.r0 && sv[lane * hp + j] <= 0.f) gh = 0.f;
-            sv[lane * hp + j] = gh;
+        if constexpr (PAIR) {
+            using ccmi_fwd::f2;
+            f2 gxp[CIN];
 #pragma unroll
-            for (int i = 0; i < CIN; ++i) gxv[i] = fmaf(r[i], gh, gxv[i]);
+            for (int i = 0; i < CIN; ++i) gxp[i] = f2(0.f);
+#pragma unroll 2
+            for (int jp = 0; jp < (hid + 1) / 2; ++jp) {
+                const f2 *r = reinterpret_cast<const f2 *>(s_rec2[jp]);
+                f2 gh = r[CIN + 1] * f2(gp1[0]);
+                gh = __builtin_elementwise_fma(r[CIN + 2], f2(gp1[1]), gh);
+                gh = __builtin_elementwise_fma(r[CIN + 3], f2(gp1[2]), gh);
+                float *row = sv + lane * hp + 2 * jp;
+                if (g.r0) {
+                    if (row[0] <= 0.f) gh.x = 0.f;
+                    if (row[1] <= 0.f) gh.y = 0.f;
+                }
+                row[0] = gh.x;
+                row[1] = gh.y;
+#pragma unroll
+                for (int i = 0; i < CIN; ++i) gxp[i] = __builtin_elementwise_fma(r[i], gh, gxp[i]);
+            }
+#pragma unroll
+            for (int i = 0; i < CIN; ++i) gxv[i] = gxp[i].x + gxp[i].y;
+        } else {
+#pragma unroll 4
+            for (int j = 0; j < hid; ++j) {
+                HEAD_BWD_REC(r, j);
+                float gh = r[CIN + 1] * gp1[0] + r[CIN + 2] * gp1[1] + r[CIN + 3] * gp1[2];
+                if (g.r0 && sv[lane * hp + j] <= 0.f) gh = 0.f;
+                sv[lane * hp + j] = gh;
+#pragma unroll
+                for (int i = 0; i < CIN; ++i) gxv[i] = fmaf(r[i], gh, gxv[i]);
+            }
         }
         if (valid) {
             float *gd = gdense + (int64_t)b * CIN * npx + p;
@@ -1793,12 +1861,19 @@ void launch_head(bool bwd, dim3 grid, hipStream_t s, const float *dense, const f
     else {
         constexpr int kXP = CIN + 2 > 4 ? CIN + 2 : 4; // t_head_bwd's per-wave LDS rows
         const size_t lds = sizeof(float) * (kHeadT / 64) * 64 * (16 * ((g.hid + 15) / 16) + 1 + kXP);
+        static const bool old = getenv("CCMI_HEAD_BWD_OLD") != nullptr; // A/B switch
+#define CCMI_HB(N)                                                                                                     \
+    do {                                                                                                               \
+        auto *kfn = old ? t_head_bwd<CIN, N, false> : t_head_bwd<CIN, N, true>;                                        \
+        hipLaunchKernelGGL(kfn, grid, dim3(kHeadT), lds, s, dense, gz0, g, th, ps, z0_or_gdense, gth, gstride);         \
+    } while (0)
         switch ((g.hid + 15) / 16) {
-        case 1: hipLaunchKernelGGL((t_head_bwd<CIN, 1>), grid, dim3(kHeadT), lds, s, dense, gz0, g, th, ps, z0_or_gdense, gth, gstride); break;
-        case 2: hipLaunchKernelGGL((t_head_bwd<CIN, 2>), grid, dim3(kHeadT), lds, s, dense, gz0, g, th, ps, z0_or_gdense, gth, gstride); break;
-        case 3: hipLaunchKernelGGL((t_head_bwd<CIN, 3>), grid, dim3(kHeadT), lds, s, dense, gz0, g, th, ps, z0_or_gdense, gth, gstride); break;
-        default: hipLaunchKernelGGL((t_head_bwd<CIN, 4>), grid, dim3(kHeadT), lds, s, dense, gz0, g, th, ps, z0_or_gdense, gth, gstride); break;
+        case 1: CCMI_HB(1); break;
+        case 2: CCMI_HB(2); break;
+        case 3: CCMI_HB(3); break;
+        default: CCMI_HB(4); break;
         }
+#undef CCMI_HB
     }
 }
 
@@ -1964,7 +2039,8 @@ extern "C" int ccmi_train_step(const ccmi_train_args *a, void *stream)
     for (int i = g.n_sp - 1; i >= 0; --i) {
         float *gin = F(pl.gbuf[i & 1]);
         const int ntile = ccmi_div_up(g.W, kSX) * ccmi_div_up(g.H, kSY);
-        const unsigned nb = (unsigned)std::max(1, std::min(ntile, 1024 / B));
+        static const int sp_nb = getenv("CCMI_SP_NB") ? atoi(getenv("CCMI_SP_NB")) : 0; // experiments: WGs per frame
+        const unsigned nb = (unsigned)std::max(1, std::min(ntile, sp_nb > 0 ? sp_nb : 1024 / B));
         hipLaunchKernelGGL(t_sp_bwd, dim3(nb, B), dim3(kT), 0, s, gcur, g.sp_relu[i] ? F(pl.z[i + 1]) : nullptr, F(pl.z[i]),
                            g, a->params, a->param_stride, g.sp_w[i], g.sp_b[i], g.sp_res[i], gin, Gth, GS);
         gcur = gin;
@@ -1972,7 +2048,8 @@ extern "C" int ccmi_train_step(const ccmi_train_args *a, void *stream)
     {
         // grid-stride over pixel chunks: about one resident wave of workgroups for the batch
         const int64_t nchunk = (npx + kHeadT - 1) / kHeadT;
-        const unsigned nb = (unsigned)std::max<int64_t>(1, std::min<int64_t>(nchunk, 1024 / B));
+        static const int hb_nb = getenv("CCMI_HB_NB") ? atoi(getenv("CCMI_HB_NB")) : 0; // experiments: WGs per frame
+        const unsigned nb = (unsigned)std::max<int64_t>(1, std::min<int64_t>(nchunk, hb_nb > 0 ? hb_nb : 1024 / B));
         head_dispatch(g.L, true, dim3(nb, B), s, dense, gcur, g, a->params, a->param_stride, gd, Gth, GS);
     }
 

@@ -32,7 +32,7 @@ BUDGET = {
     # registers and spills a few values across its tile loop: measured faster than the
     # spill-free 2-wave build (profiles/r2_train_ab.json), so the spills are budgeted
     "t_arm16<2>": (168, 16, 64),
-    "t_head_bwd<7, 3>": (168, 0, 0),
+    "t_head_bwd<7, 3, true>": (168, 0, 0),  # unit-pair packed form (default)
     "t_sp_bwd": (168, 0, 0),
 }
 
