@@ -928,12 +928,18 @@ __device__ __forceinline__ void qrange(int p, int dd, int n, int &lo, int &hi)
 //    an interior pixel p is the plain correlation sum_{c,k} W[c][i][k] G[c][p - d_k]; a
 //    pixel on the image border also collects the taps that the replicate padding clamps
 //    onto it (qrange), all within the ring.
+// MODE: 1 = input gradient only, 2 = weight / bias gradients only, 3 = both.  The step runs
+// the two halves as separate launches: the input-gradient kernel holds no 84 accumulators, so
+// it keeps many more waves resident to hide its tile loads (the combined kernel sat 71 % of
+// its wave cycles in s_waitcnt / barrier waits, SQ_WAIT_ANY), and needs no reduction.
 constexpr int kSY = 16, kSX = 64;
+template <int MODE>
 __global__ __launch_bounds__(kT) void t_sp_bwd(const float *__restrict__ gout, const float *__restrict__ outp,
                                                const float *__restrict__ in, Geo g, const float *__restrict__ th,
                                                int64_t ps, int wo, int bo, int res, float *__restrict__ gin,
                                                float *__restrict__ gth, int64_t gstride)
 {
+    constexpr bool DX = (MODE & 1) != 0, DW = (MODE & 2) != 0;
     constexpr int RH = kSY + 2, RW = kSX + 2;
     __shared__ float sX[3][RH][RW];
     __shared__ float sG[3][RH][RW];
@@ -948,9 +954,9 @@ __global__ __launch_bounds__(kT) void t_sp_bwd(const float *__restrict__ gout, c
     float *Ib = gin + (int64_t)b * 3 * npx;
     const int tx = (W + kSX - 1) / kSX, ntile = tx * ((H + kSY - 1) / kSY);
     const int c = threadIdx.x & 63, rb = (threadIdx.x >> 6) * 4;
-    float acc[84];
+    float acc[DW ? 84 : 1];
 #pragma unroll
-    for (int e = 0; e < 84; ++e) acc[e] = 0.f;
+    for (int e = 0; e < (DW ? 84 : 1); ++e) acc[e] = 0.f;
     for (int t = blockIdx.x; t < ntile; t += gridDim.x) {
         const int y0 = (t / tx) * kSY, x0 = (t % tx) * kSX;
         __syncthreads();
@@ -961,7 +967,7 @@ __global__ __launch_bounds__(kT) void t_sp_bwd(const float *__restrict__ gout, c
             const bool in_img = y >= 0 && y < H && x >= 0 && x < W;
 #pragma unroll
             for (int ch = 0; ch < 3; ++ch) {
-                sX[ch][r][q] = Xb[ch * npx + cl];
+                if (DW) sX[ch][r][q] = Xb[ch * npx + cl];
                 float gv = 0.f;
                 if (in_img) {
                     gv = Gb[ch * npx + cl];
@@ -980,16 +986,19 @@ __global__ __launch_bounds__(kT) void t_sp_bwd(const float *__restrict__ gout, c
             float gp[3];
 #pragma unroll
             for (int ch = 0; ch < 3; ++ch) gp[ch] = sG[ch][ry + 1][c + 1];
+            if constexpr (DW) {
 #pragma unroll
-            for (int i = 0; i < 3; ++i)
+                for (int i = 0; i < 3; ++i)
 #pragma unroll
-                for (int k = 0; k < 9; ++k) {
-                    const float xv = sX[i][ry + k / 3][c + k % 3];
+                    for (int k = 0; k < 9; ++k) {
+                        const float xv = sX[i][ry + k / 3][c + k % 3];
 #pragma unroll
-                    for (int oc = 0; oc < 3; ++oc) acc[(oc * 3 + i) * 9 + k] = fmaf(gp[oc], xv, acc[(oc * 3 + i) * 9 + k]);
-                }
+                        for (int oc = 0; oc < 3; ++oc) acc[(oc * 3 + i) * 9 + k] = fmaf(gp[oc], xv, acc[(oc * 3 + i) * 9 + k]);
+                    }
 #pragma unroll
-            for (int oc = 0; oc < 3; ++oc) acc[81 + oc] += gp[oc];
+                for (int oc = 0; oc < 3; ++oc) acc[81 + oc] += gp[oc];
+            }
+            if constexpr (!DX) continue;
             // input gradient at p = (py, px)
             float gi[3] = {0.f, 0.f, 0.f};
             if (py > 0 && py < H - 1 && px > 0 && px < W - 1) {
@@ -1028,6 +1037,7 @@ __global__ __launch_bounds__(kT) void t_sp_bwd(const float *__restrict__ gout, c
             for (int i = 0; i < 3; ++i) Ib[i * npx + pi] = gi[i] + (res ? gp[i] : 0.f);
         }
     }
+    if constexpr (!DW) return;
     // block reduction of the 84 weight / bias gradients
     const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
 #pragma unroll
@@ -2041,8 +2051,18 @@ extern "C" int ccmi_train_step(const ccmi_train_args *a, void *stream)
         const int ntile = ccmi_div_up(g.W, kSX) * ccmi_div_up(g.H, kSY);
         static const int sp_nb = getenv("CCMI_SP_NB") ? atoi(getenv("CCMI_SP_NB")) : 0; // experiments: WGs per frame
         const unsigned nb = (unsigned)std::max(1, std::min(ntile, sp_nb > 0 ? sp_nb : 1024 / B));
-        hipLaunchKernelGGL(t_sp_bwd, dim3(nb, B), dim3(kT), 0, s, gcur, g.sp_relu[i] ? F(pl.z[i + 1]) : nullptr, F(pl.z[i]),
-                           g, a->params, a->param_stride, g.sp_w[i], g.sp_b[i], g.sp_res[i], gin, Gth, GS);
+        static const bool fused_bwd = getenv("CCMI_SP_BWD_FUSED") != nullptr; // A/B switch: one kernel
+        const float *outp = g.sp_relu[i] ? F(pl.z[i + 1]) : nullptr;
+        if (fused_bwd) {
+            hipLaunchKernelGGL(t_sp_bwd<3>, dim3(nb, B), dim3(kT), 0, s, gcur, outp, F(pl.z[i]), g, a->params,
+                               a->param_stride, g.sp_w[i], g.sp_b[i], g.sp_res[i], gin, Gth, GS);
+        } else {
+            // input gradient: one tile per workgroup; weight gradients: grid-stride as before
+            hipLaunchKernelGGL(t_sp_bwd<1>, dim3((unsigned)ntile, B), dim3(kT), 0, s, gcur, outp, F(pl.z[i]), g, a->params,
+                               a->param_stride, g.sp_w[i], g.sp_b[i], g.sp_res[i], gin, Gth, GS);
+            hipLaunchKernelGGL(t_sp_bwd<2>, dim3(nb, B), dim3(kT), 0, s, gcur, outp, F(pl.z[i]), g, a->params,
+                               a->param_stride, g.sp_w[i], g.sp_b[i], g.sp_res[i], gin, Gth, GS);
+        }
         gcur = gin;
     }
     {
