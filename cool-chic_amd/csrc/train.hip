@@ -767,54 +767,67 @@ __global__ void t_colsum(const float *__restrict__ part, int nrows, int ncols, f
 }
 
 // ------------------------------------------------------------------ synthesis
+// Two pixels per thread (p and p + kT of the workgroup's 2 kT) on packed FMAs: each broadcast
+// weight record serves both, halving the LDS record traffic per pixel (the one-pixel form
+// sat 56 % of its wave cycles in SQ_WAIT_INST_LDS).  Record slots 3, 7, 11 stay empty when
+// the fields fit without them (the compiler copies a broadcast operand out of the last dword
+// of a ds_read_b128 first), as in the path-A fused kernel.
 template <int CIN>
 __global__ __launch_bounds__(kT) void t_head_fwd(const float *__restrict__ dense, Geo g, const float *__restrict__ th,
                                                  int64_t ps, float *__restrict__ z0)
 {
-    // hidden unit j as one LDS record w0[j][0..CIN), b0[j], w1[0..3)[j] (broadcast reads, as
-    // t_head_bwd; scalar loads of the weights in the unit loop stalled on their waits)
-    __shared__ __attribute__((aligned(16))) float s_rec[64][12];
-    static_assert(CIN + 4 <= 12, "hidden-unit record");
+    using ccmi_fwd::f2;
+    constexpr bool kPad = CIN + 4 <= 12;
+    auto hr = [](int f) constexpr { return kPad ? f + f / 3 : f; };
+    __shared__ __attribute__((aligned(16))) float s_rec[64][16];
+    static_assert(CIN + 4 <= 16, "hidden-unit record");
     const int b = blockIdx.y, hid = g.hid;
     const cfloat_ptr P = (cfloat_ptr)(size_t)(th + (int64_t)b * ps);
-    for (int e = threadIdx.x; e < 64 * 12; e += kT) {
-        const int j = e / 12, f = e - j * 12;
+    for (int e = threadIdx.x; e < 64 * 16; e += kT) {
+        const int j = e >> 4, f = e & 15;
         float v = 0.f;
         if (j < hid) {
             if (f < CIN) v = P[g.w0 + j * CIN + f];
             else if (f == CIN) v = P[g.b0 + j];
             else if (f <= CIN + 3) v = P[g.w1 + (f - CIN - 1) * hid + j];
         }
-        s_rec[j][f] = v;
+        if (f <= CIN + 3) s_rec[j][hr(f)] = v;
     }
     __syncthreads();
-    const int64_t npx = (int64_t)g.H * g.W, p = (int64_t)blockIdx.x * kT + threadIdx.x;
-    if (p >= npx) return;
-    const float *x = dense + (int64_t)b * CIN * npx + p;
-    float xv[CIN];
+    const int64_t npx = (int64_t)g.H * g.W, p0 = (int64_t)blockIdx.x * 2 * kT + threadIdx.x, p1 = p0 + kT;
+    if (p0 >= npx) return;
+    const bool v1 = p1 < npx;
+    const float *x = dense + (int64_t)b * CIN * npx;
+    f2 xv[CIN];
 #pragma unroll
-    for (int i = 0; i < CIN; ++i) xv[i] = x[i * npx];
-    float o0 = P[g.b1], o1 = P[g.b1 + 1], o2 = P[g.b1 + 2];
+    for (int i = 0; i < CIN; ++i) xv[i] = f2{x[i * npx + p0], v1 ? x[i * npx + p1] : 0.f};
+    const f2 lo0 = f2(g.r0 ? 0.f : -INFINITY);
+    f2 o0 = f2(P[g.b1]), o1 = f2(P[g.b1 + 1]), o2 = f2(P[g.b1 + 2]);
 #pragma unroll 4
     for (int j = 0; j < hid; ++j) {
         const float *r = s_rec[j];
-        float h = r[CIN];
+        f2 h = f2(r[hr(CIN)]);
 #pragma unroll
-        for (int i = 0; i < CIN; ++i) h = fmaf(r[i], xv[i], h);
-        if (g.r0) h = fmaxf(h, 0.f);
-        o0 = fmaf(r[CIN + 1], h, o0);
-        o1 = fmaf(r[CIN + 2], h, o1);
-        o2 = fmaf(r[CIN + 3], h, o2);
+        for (int i = 0; i < CIN; ++i) h = __builtin_elementwise_fma(f2(r[hr(i)]), xv[i], h);
+        h = __builtin_elementwise_max(h, lo0);
+        o0 = __builtin_elementwise_fma(f2(r[hr(CIN + 1)]), h, o0);
+        o1 = __builtin_elementwise_fma(f2(r[hr(CIN + 2)]), h, o1);
+        o2 = __builtin_elementwise_fma(f2(r[hr(CIN + 3)]), h, o2);
     }
     if (g.r1) {
-        o0 = fmaxf(o0, 0.f);
-        o1 = fmaxf(o1, 0.f);
-        o2 = fmaxf(o2, 0.f);
+        o0 = __builtin_elementwise_max(o0, f2(0.f));
+        o1 = __builtin_elementwise_max(o1, f2(0.f));
+        o2 = __builtin_elementwise_max(o2, f2(0.f));
     }
-    float *z = z0 + (int64_t)b * 3 * npx + p;
-    z[0] = o0;
-    z[npx] = o1;
-    z[2 * npx] = o2;
+    float *z = z0 + (int64_t)b * 3 * npx;
+    z[p0] = o0.x;
+    z[npx + p0] = o1.x;
+    z[2 * npx + p0] = o2.x;
+    if (v1) {
+        z[p1] = o0.y;
+        z[npx + p1] = o1.y;
+        z[2 * npx + p1] = o2.y;
+    }
 }
 
 // 3x3, 3 -> 3, replicate padding (synthesis.py:69-84), optional residual / ReLU.
@@ -932,9 +945,11 @@ __device__ __forceinline__ void qrange(int p, int dd, int n, int &lo, int &hi)
 // the two halves as separate launches: the input-gradient kernel holds no 84 accumulators, so
 // it keeps many more waves resident to hide its tile loads (the combined kernel sat 71 % of
 // its wave cycles in s_waitcnt / barrier waits, SQ_WAIT_ANY), and needs no reduction.
+// (Measured and dropped: the input gradient one channel per iteration with 27 scalar weights
+// each instead of all 81 at once -- 74 vs 40 us, the scalar-load waits per channel.)
 constexpr int kSY = 16, kSX = 64;
 template <int MODE>
-__global__ __launch_bounds__(kT) void t_sp_bwd(const float *__restrict__ gout, const float *__restrict__ outp,
+__global__ __launch_bounds__(kT) __attribute__((amdgpu_waves_per_eu(MODE == 2 ? 4 : 1))) void t_sp_bwd(const float *__restrict__ gout, const float *__restrict__ outp,
                                                const float *__restrict__ in, Geo g, const float *__restrict__ th,
                                                int64_t ps, int wo, int bo, int res, float *__restrict__ gin,
                                                float *__restrict__ gth, int64_t gstride)
@@ -960,20 +975,39 @@ __global__ __launch_bounds__(kT) void t_sp_bwd(const float *__restrict__ gout, c
     for (int t = blockIdx.x; t < ntile; t += gridDim.x) {
         const int y0 = (t / tx) * kSY, x0 = (t % tx) * kSX;
         __syncthreads();
-        for (int i = threadIdx.x; i < RH * RW; i += kT) {
-            const int r = i / RW, q = i - r * RW;
-            const int y = y0 - 1 + r, x = x0 - 1 + q;
-            const int64_t cl = (int64_t)clampi(y, H - 1) * W + clampi(x, W - 1);
-            const bool in_img = y >= 0 && y < H && x >= 0 && x < W;
+        // the ring in batches of UN elements per thread: a batch's loads are all in flight
+        // before its LDS stores (the input-gradient kernel, with few registers, takes the
+        // whole ring in one batch; the weight-gradient kernel two per batch)
+        constexpr int NU = (RH * RW + kT - 1) / kT, UN = DW ? 2 : NU;
 #pragma unroll
-            for (int ch = 0; ch < 3; ++ch) {
-                if (DW) sX[ch][r][q] = Xb[ch * npx + cl];
-                float gv = 0.f;
-                if (in_img) {
-                    gv = Gb[ch * npx + cl];
-                    if (Ob && Ob[ch * npx + cl] <= 0.f) gv = 0.f;
+        for (int u0 = 0; u0 < NU; u0 += UN) {
+            float xs[UN][3], gs[UN][3], os[UN][3];
+            bool inb[UN];
+#pragma unroll
+            for (int uu = 0; uu < UN; ++uu) {
+                const int i = threadIdx.x + (u0 + uu) * kT;
+                const int r = i / RW, q = i - r * RW;
+                const int y = y0 - 1 + r, x = x0 - 1 + q;
+                const int64_t cl = (int64_t)clampi(y, H - 1) * W + clampi(x, W - 1);
+                inb[uu] = y >= 0 && y < H && x >= 0 && x < W;
+                const bool live = u0 + uu < NU && i < RH * RW;
+#pragma unroll
+                for (int ch = 0; ch < 3; ++ch) {
+                    xs[uu][ch] = (DW && live) ? Xb[ch * npx + cl] : 0.f;
+                    gs[uu][ch] = (live && inb[uu]) ? Gb[ch * npx + cl] : 0.f;
+                    os[uu][ch] = (Ob && live && inb[uu]) ? Ob[ch * npx + cl] : 1.f;
                 }
-                sG[ch][r][q] = gv;
+            }
+#pragma unroll
+            for (int uu = 0; uu < UN; ++uu) {
+                const int i = threadIdx.x + (u0 + uu) * kT;
+                if (u0 + uu >= NU || i >= RH * RW) continue;
+                const int r = i / RW, q = i - r * RW;
+#pragma unroll
+                for (int ch = 0; ch < 3; ++ch) {
+                    if (DW) sX[ch][r][q] = xs[uu][ch];
+                    sG[ch][r][q] = os[uu][ch] <= 0.f ? 0.f : gs[uu][ch];
+                }
             }
         }
         __syncthreads();
@@ -2024,7 +2058,8 @@ extern "C" int ccmi_train_step(const ccmi_train_args *a, void *stream)
         u.batch = B;
         if (int rc = ccmi_launch_ups_f32(&u, s)) return rc;
     }
-    head_dispatch(g.L, false, grid1(npx, B), s, dense, nullptr, g, a->params, a->param_stride, F(pl.z[0]), nullptr, 0);
+    head_dispatch(g.L, false, dim3((unsigned)((npx + 2 * kT - 1) / (2 * kT)), (unsigned)B), s, dense, nullptr, g, a->params,
+                  a->param_stride, F(pl.z[0]), nullptr, 0); // two pixels per thread
     for (int i = 0; i < g.n_sp; ++i)
         hipLaunchKernelGGL(t_sp_fwd, grid1(npx, B), dim3(kT), 0, s, F(pl.z[i]), g, a->params, a->param_stride, g.sp_w[i],
                            g.sp_b[i], g.sp_res[i], g.sp_relu[i], F(pl.z[i + 1]));
@@ -2051,16 +2086,14 @@ extern "C" int ccmi_train_step(const ccmi_train_args *a, void *stream)
         const int ntile = ccmi_div_up(g.W, kSX) * ccmi_div_up(g.H, kSY);
         static const int sp_nb = getenv("CCMI_SP_NB") ? atoi(getenv("CCMI_SP_NB")) : 0; // experiments: WGs per frame
         const unsigned nb = (unsigned)std::max(1, std::min(ntile, sp_nb > 0 ? sp_nb : 1024 / B));
-        static const bool fused_bwd = getenv("CCMI_SP_BWD_FUSED") != nullptr; // A/B switch: one kernel
         const float *outp = g.sp_relu[i] ? F(pl.z[i + 1]) : nullptr;
-        if (fused_bwd) {
-            hipLaunchKernelGGL(t_sp_bwd<3>, dim3(nb, B), dim3(kT), 0, s, gcur, outp, F(pl.z[i]), g, a->params,
-                               a->param_stride, g.sp_w[i], g.sp_b[i], g.sp_res[i], gin, Gth, GS);
-        } else {
+        {
             // input gradient: one tile per workgroup; weight gradients: grid-stride as before
             hipLaunchKernelGGL(t_sp_bwd<1>, dim3((unsigned)ntile, B), dim3(kT), 0, s, gcur, outp, F(pl.z[i]), g, a->params,
                                a->param_stride, g.sp_w[i], g.sp_b[i], g.sp_res[i], gin, Gth, GS);
-            hipLaunchKernelGGL(t_sp_bwd<2>, dim3(nb, B), dim3(kT), 0, s, gcur, outp, F(pl.z[i]), g, a->params,
+            static const int spw_nb = getenv("CCMI_SPW_NB") ? atoi(getenv("CCMI_SPW_NB")) : 0; // experiments
+            const unsigned nbw = spw_nb > 0 ? (unsigned)std::max(1, std::min(ntile, spw_nb)) : nb;
+            hipLaunchKernelGGL(t_sp_bwd<2>, dim3(nbw, B), dim3(kT), 0, s, gcur, outp, F(pl.z[i]), g, a->params,
                                a->param_stride, g.sp_w[i], g.sp_b[i], g.sp_res[i], gin, Gth, GS);
         }
         gcur = gin;

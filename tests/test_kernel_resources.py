@@ -33,7 +33,8 @@ BUDGET = {
     # spill-free 2-wave build (profiles/r2_train_ab.json), so the spills are budgeted
     "t_arm16<2>": (168, 16, 64),
     "t_head_bwd<7, 3, true>": (168, 0, 0),  # unit-pair packed form (default)
-    "t_sp_bwd": (168, 0, 0),
+    "t_sp_bwd<1>": (128, 0, 0),  # 3x3 backward, input gradient
+    "t_sp_bwd<2>": (128, 0, 0),  # 3x3 backward, weight gradients (4 waves / SIMD)
 }
 
 

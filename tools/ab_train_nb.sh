@@ -15,7 +15,7 @@ import csv,sys,re
 out={}
 for r in csv.DictReader(open(sys.argv[1])):
     m=re.search(r'(t_\w+)(<[^>]*>)?', r['Name'])
-    if m and m.group(1) in ('t_sp_bwd','t_arm16','t_head_bwd'): out[m.group(0)]=round(float(r['AverageNs'])/1e3,1)
+    if m and m.group(1) in ('t_sp_bwd','t_arm16','t_head_bwd','t_head_fwd'): out[m.group(0)]=round(float(r['AverageNs'])/1e3,1)
 print(sys.argv[2], out)
 PY
 done < ${VARIANTS:-$R/tools/ab_train_nb.txt}
