@@ -208,22 +208,25 @@ __global__ __launch_bounds__(kFThreads) __attribute__((amdgpu_waves_per_eu(fused
     const float *lut8 = A.qmax == 255.f ? s_lut8 : nullptr;
     // per-frame tables in LDS: the 8-bit output quotients (own area, staged at once) and the
     // head's weight records (region 1: before anything else without fused upsampling, after
-    // the gathers with it -- the values are fetched into registers up front, kHeadRegs each)
+    // the gathers with it)
     if (lut8) s_lut8[threadIdx.x & 255] = (float)(threadIdx.x & 255) / 255.f;
+    // the records are fetched right where they are staged (L2-resident: every workgroup of a
+    // frame reads the same ones); holding them in registers across the upsampling phases
+    // cost spill slots at the 80-VGPR budget
     constexpr int kHeadRegs = kMaxHid * 16 / kFThreads;
-    float hv[kHeadRegs];
-#pragma unroll
-    for (int k = 0; k < kHeadRegs; ++k) {
-        const int i = threadIdx.x + k * kFThreads, j = i >> 4, f = i & 15;
-        float v = 0.f;
-        if (A.n_head == 2 && j < A.hid) {
-            if (f < CIN) v = prm[A.w0_off + j * CIN + f];
-            else if (f == CIN) v = prm[A.b0_off + j];
-            else if (f <= CIN + CMID) v = prm[A.w1_off + (f - CIN - 1) * A.hid + j];
-        }
-        hv[k] = v;
-    }
     auto stage_head = [&]() {
+        float hv[kHeadRegs];
+#pragma unroll
+        for (int k = 0; k < kHeadRegs; ++k) {
+            const int i = threadIdx.x + k * kFThreads, j = i >> 4, f = i & 15;
+            float v = 0.f;
+            if (A.n_head == 2 && j < A.hid) {
+                if (f < CIN) v = prm[A.w0_off + j * CIN + f];
+                else if (f == CIN) v = prm[A.b0_off + j];
+                else if (f <= CIN + CMID) v = prm[A.w1_off + (f - CIN - 1) * A.hid + j];
+            }
+            hv[k] = v;
+        }
 #pragma unroll
         for (int k = 0; k < kHeadRegs; ++k) {
             const int i = threadIdx.x + k * kFThreads, j = i >> 4, f = i & 15;
@@ -779,6 +782,7 @@ __global__ __launch_bounds__(kFThreads) __attribute__((amdgpu_waves_per_eu(fused
                 const uint32_t cpx = (uint32_t)((gy >> 1) * (int)cw + (gx >> 1));
 #pragma unroll
                 for (int m = 0; m < CMID; ++m) {
+                    if (fmt == 2 && m > 0 && (gy & 1)) break; // 420: odd rows carry no chroma (wave-uniform)
                     float v = fin[m * kPlane + p * kRW];
                     if constexpr (fmt > 0) {
                         v = tab ? lut8[(int)fminf(fmaxf(rintf(v * 255.f), 0.f), 255.f)]
