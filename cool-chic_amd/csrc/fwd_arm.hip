@@ -78,7 +78,9 @@ __device__ __forceinline__ float laplace_cdf(float x, float mu, float inv_scale)
     return 0.5f - 0.5f * sg * (__expf(-fabsf(s) * inv_scale) - 1.f);
 }
 
-template <int D>
+// NH >= 0: the hidden-layer count fixed at compile time (the layer loop unrolled, so the
+// next layer's scalar weight loads can be scheduled under the current layer's FMAs)
+template <int D, int NH = -1>
 __global__ __launch_bounds__(kThreads) void arm_fwd_kernel(
     const float *__restrict__ lat, int64_t lat_stride, ArmGeom g, float gain, int quantize, int nh,
     const float *__restrict__ params, int64_t pstride, float *__restrict__ o_mu, float *__restrict__ o_scale,
@@ -129,6 +131,8 @@ __global__ __launch_bounds__(kThreads) void arm_fwd_kernel(
                          tile[cy0 + (2 * q + 1) * kRowsPerPass + kHalo + dy][cx + kHalo + dx]};
     }
 
+    if constexpr (NH >= 0) nh = NH;
+#pragma unroll
     for (int layer = 0; layer < nh; ++layer) {
         const cfloat_ptr Wl = p + layer * (D * D + D);
         const cfloat_ptr bl = Wl + D * D;
@@ -487,9 +491,18 @@ int ccmi_launch_arm_f32(const ccmi_arm_args *a, hipStream_t s)
     hipLaunchKernelGGL(arm_fwd_kernel<DD>, grid, dim3(kThreads), 0, s, a->latent, a->latent_stride, g, a->gain, \
                        a->quantize, a->n_hidden, a->params, a->param_stride, a->mu, a->scale, a->log_scale,     \
                        a->rate, a->out_stride)
+    static const bool nh_rt = getenv("CCMI_ARM_NH_RUNTIME") != nullptr; // A/B switch
     switch (a->dim_arm) {
     case 8: CCMI_ARM_LAUNCH(8); break;
-    case 16: CCMI_ARM_LAUNCH(16); break;
+    case 16:
+        if (a->n_hidden == 2 && !nh_rt) {
+            hipLaunchKernelGGL((arm_fwd_kernel<16, 2>), grid, dim3(kThreads), 0, s, a->latent, a->latent_stride, g, a->gain,
+                               a->quantize, a->n_hidden, a->params, a->param_stride, a->mu, a->scale, a->log_scale,
+                               a->rate, a->out_stride);
+        } else {
+            CCMI_ARM_LAUNCH(16);
+        }
+        break;
     case 24: CCMI_ARM_LAUNCH(24); break;
     case 32: CCMI_ARM_LAUNCH(32); break;
     default: return ccmi_set_error(CCMI_ERR_UNSUPPORTED, "arm: dim_arm must be 8, 16, 24 or 32 (got %d)", a->dim_arm);
