@@ -100,15 +100,23 @@ __global__ __launch_bounds__(kThreads) void arm_fwd_kernel(
     const int x0 = (lt % g.tiles_x[l]) * kTX;
     const float *src = lat + (int64_t)b * lat_stride + g.off[l];
 
-    for (int i = threadIdx.x; i < kLH * kLW; i += kThreads) {
-        const int r = i / kLW, c = i - r * kLW;
-        const int y = y0 - kHalo + r, x = x0 - kHalo + c;
-        float v = 0.f;
-        if (y >= 0 && y < H && x >= 0 && x < W) {
-            v = src[y * W + x];
-            if (quantize) v = rintf(gain * v);
+    // fixed trip count, unrolled: every load of the thread is in flight before the first
+    // LDS store waits on one
+    {
+        constexpr int NU = (kLH * kLW + kThreads - 1) / kThreads;
+        float lv[NU];
+#pragma unroll
+        for (int u = 0; u < NU; ++u) {
+            const int i = threadIdx.x + u * kThreads;
+            const int r = i / kLW, c = i - r * kLW;
+            const int y = y0 - kHalo + r, x = x0 - kHalo + c;
+            lv[u] = (i < kLH * kLW && y >= 0 && y < H && x >= 0 && x < W) ? src[y * W + x] : 0.f;
         }
-        tile[r][c] = v;
+#pragma unroll
+        for (int u = 0; u < NU; ++u) {
+            const int i = threadIdx.x + u * kThreads;
+            if (i < kLH * kLW) tile[i / kLW][i % kLW] = quantize ? rintf(gain * lv[u]) : lv[u];
+        }
     }
     __syncthreads();
 
