@@ -168,15 +168,23 @@ __global__ __launch_bounds__(kThreads) void ups_level_fixed(LevelArgs A)
         for (int k = 0; k < KP; ++k) wr[k] = prm[A.pre_off + k];
         float *s_ref = s_mem, *s_refh = s_mem + T::RH * T::RW;
         const float *rs = A.ref_src + (int64_t)b * A.ref_stride;
-        for (int i = tid; i < T::RH * T::RW; i += kThreads) {
-            const int r = i / T::RW, c = i - r * T::RW;
-            const int y = y0 - T::PAD + r, x = x0 - T::PAD + c;
-            float v = 0.f;
-            if (y >= 0 && y < A.hd && x >= 0 && x < A.wd) {
-                v = rs[y * A.wd + x];
-                if (A.ref_quant) v = rintf(A.gain * v);
+        // fixed trip counts, unrolled: all of a thread's tile loads are in flight before the
+        // first LDS store waits on one (the rolled loop paid one memory latency per pass)
+        {
+            constexpr int NU = (T::RH * T::RW + kThreads - 1) / kThreads;
+            float lv[NU];
+#pragma unroll
+            for (int u = 0; u < NU; ++u) {
+                const int i = tid + u * kThreads;
+                const int r = i / T::RW, c = i - r * T::RW;
+                const int y = y0 - T::PAD + r, x = x0 - T::PAD + c;
+                lv[u] = (i < T::RH * T::RW && y >= 0 && y < A.hd && x >= 0 && x < A.wd) ? rs[y * A.wd + x] : 0.f;
             }
-            s_ref[i] = v;
+#pragma unroll
+            for (int u = 0; u < NU; ++u) {
+                const int i = tid + u * kThreads;
+                if (i < T::RH * T::RW) s_ref[i] = A.ref_quant ? rintf(A.gain * lv[u]) : lv[u];
+            }
         }
         __syncthreads();
         for (int i = tid; i < T::RH * kTX; i += kThreads) {
@@ -209,12 +217,19 @@ __global__ __launch_bounds__(kThreads) void ups_level_fixed(LevelArgs A)
     {
         const float *src = A.src + (int64_t)b * A.src_stride + (int64_t)c * A.hs * A.ws;
         const int sy0 = y0 / 2 + T::D0, sx0 = x0 / 2 + T::D0;
-        for (int i = tid; i < T::SH * T::SW; i += kThreads) {
+        constexpr int NU = (T::SH * T::SW + kThreads - 1) / kThreads;
+        float lv[NU];
+#pragma unroll
+        for (int u = 0; u < NU; ++u) {
+            const int i = tid + u * kThreads;
             const int r = i / T::SW, cc = i - r * T::SW;
             const int y = clampi(sy0 + r, A.hs - 1), x = clampi(sx0 + cc, A.ws - 1);
-            float v = src[y * A.ws + x];
-            if (A.src_quant) v = rintf(A.gain * v);
-            s_src[i] = v;
+            lv[u] = i < T::SH * T::SW ? src[y * A.ws + x] : 0.f;
+        }
+#pragma unroll
+        for (int u = 0; u < NU; ++u) {
+            const int i = tid + u * kThreads;
+            if (i < T::SH * T::SW) s_src[i] = A.src_quant ? rintf(A.gain * lv[u]) : lv[u];
         }
     }
     __syncthreads();

@@ -23,7 +23,8 @@ BUDGET = {
     "syn_fused_kernel<7, 3, true, false, 0>": (80, 8, 40),   # any head width
     "syn_fused_kernel<7, 3, true, false, 48>": (80, 8, 40),  # headline (hop): unrolled head
     "syn_fused_kernel<7, 4, true, false, 0>": (128, 0, 0),   # 4-channel tail: 2 workgroups
-    "arm_fwd_kernel<16>": (128, 0, 0),                      # path A ARM + rate
+    "arm_fwd_kernel<16, 2>": (128, 0, 0),                   # path A ARM + rate (hop: 2 hidden layers)
+    "arm_fwd_kernel<16, -1>": (128, 0, 0),                  # any hidden-layer count
     "ups_level_fixed<8, 7>": (64, 0, 0),                    # upsampling pyramid
     "dec_arm_kernel<16, 2>": (128, 0, 0),                   # path B ARM + CABAC
     "dec_arm_spec_kernel<16, 2>": (128, 0, 0),
