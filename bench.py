@@ -113,6 +113,8 @@ def make_inputs(B, dev, seed, H=H, W=W):
 class Pipeline:
     """Preallocated buffers + direct C-ABI launches (no per-step allocation)."""
 
+    head = 0  # ccmi_decode_args.head (CCMI_HEAD_*), set from --head
+
     def __init__(self, inp, B, dev):
         import ctypes
         import ccmi
@@ -144,7 +146,7 @@ class Pipeline:
         # fused decode tail: pyramid (levels 6 -> 1) then ONE kernel for the last
         # upsampling step + synthesis + 420 post (no dense stack, no raw synthesis output)
         self.dec = [ccmi.DecodeArgs(ups=self.ups, syn=self.synargs, bitdepth=8, yuv420=1, out=p(self.yuv),
-                                    out_stride=self.yuv.shape[1], stages=st) for st in (1, 2)]
+                                    out_stride=self.yuv.shape[1], stages=st, head=Pipeline.head) for st in (1, 2)]
         self.byref = ctypes.byref
         self.stream = torch.cuda.current_stream(dev)
         # the ARM (rate) and the decode tail (pixels) only share the latents: with overlap
@@ -445,7 +447,7 @@ def bench_encoder(images: int, scale: float, lambdas, rank: int, world: int, dis
                 for lm in lambdas:
                     r = rd.encode_batch(tg, Hh, Wh, lm, arch, names=[n for n, _ in items], seeds=[rank] * len(items),
                                         preset="c3x", scale=scale)
-                    flop += encoder_flops_per_iteration(Hh, Wh) * r[0].iterations * len(items)
+                    flop += encoder_flops_per_iteration(Hh, Wh) * sum(x.iterations for x in r)
                     out += r
             return out, flop
         keys = sorted(groups.items())
@@ -609,6 +611,8 @@ def main():
     ap.add_argument("--no-graph", action="store_true",
                     help="time the eager launches instead of HIP-graph replays of the fused pipeline")
     ap.add_argument("--hd-steps", type=int, default=20, help="steps of the 1920x1080 float-forward leg (0: skip)")
+    ap.add_argument("--head", choices=("default", "valu", "mfma"), default="default",
+                    help="the fused kernel's 1x1 synthesis head: fp32 VALU or f32 MFMA (CCMI_HEAD_*)")
     ap.add_argument("--hd-decode-reps", type=int, default=64,
                     help="class-B (1080p) stream copies for the bit-exact decode leg (0: skip)")
     args = ap.parse_args()
@@ -633,6 +637,7 @@ def main():
     torch.cuda.set_device(dev)
 
     B = args.batch
+    Pipeline.head = {"default": 0, "valu": 1, "mfma": 2}[args.head]
     inp = make_inputs(B, dev, seed=1000 * rank + 1)
     mode = "staged" if args.staged else "fused"
     ovp = args.overlap_pyramid and not args.serial and mode == "fused"
@@ -721,7 +726,8 @@ def main():
             "value": round(tot, 2), "per_gpu": round(tot / world, 2), "unit": "images/hr", "n_gpus": world,
             "images": n_enc, "lambdas": lambdas, "encodes": len(recs), "seconds_max_over_ranks": round(secs, 2),
             "schedule": f"c3x x{args.encode_scale:g}: warm-up 5x400 + 2x400 candidates, phases 10600 + 1500 + 1000 "
-                        f"iterations ({recs[0]['iterations'] if recs else 0} per image); quantize_model after "
+                        f"iterations (mean {np.mean([r['iterations'] for r in recs]) if recs else 0:.0f} per image, "
+                        f"patience early stops included); quantize_model after "
                         f"the second phase; images of one geometry and lambda overfit together as one batch, "
                         f"the geometry batches concurrently on separate HIP streams",
             "psnr_db_mean": round(float(np.mean([r["psnr_db"] for r in recs])), 3),

@@ -90,8 +90,11 @@ class PostArgs(C.Structure):
 class DecodeArgs(C.Structure):
     _fields_ = [
         ("ups", UpsArgs), ("syn", SynArgs), ("bitdepth", C.c_int), ("yuv420", C.c_int),
-        ("out", C.c_void_p), ("out_stride", C.c_int64), ("stages", C.c_int),
+        ("out", C.c_void_p), ("out_stride", C.c_int64), ("stages", C.c_int), ("head", C.c_int),
     ]
+
+
+HEAD_DEFAULT, HEAD_VALU, HEAD_MFMA = 0, 1, 2  # ccmi_decode_args.head (CCMI_HEAD_*)
 
 
 _lib = None

@@ -173,11 +173,12 @@ def post_forward(x: torch.Tensor, bitdepth: int = 8, yuv420: bool = False) -> to
 
 def decode_forward(latent: torch.Tensor, sizes, ups_params: torch.Tensor, ups_k: int, n_ups: int, pre_k: int,
                    n_pre: int, layers, syn_params: torch.Tensor, gain: float = 16.0, quantize: bool = True,
-                   bitdepth: int = 8, yuv420: bool = False) -> torch.Tensor:
+                   bitdepth: int = 8, yuv420: bool = False, head: int = 0) -> torch.Tensor:
     """Fused upsampling -> synthesis -> post (ccmi_decode_forward_f32): latent [B, N] ->
     post-processed frames (layout of post_forward), or with bitdepth=0 the raw synthesis
-    output [B, C_out, H, W].  Raises CcmiError(ERR_UNSUPPORTED) for architectures
-    without a fused kernel (use ups_forward / syn_forward / post_forward)."""
+    output [B, C_out, H, W].  head: ccmi.HEAD_* (the 1x1 head on the VALU or on f32 MFMA).
+    Raises CcmiError(ERR_UNSUPPORTED) for architectures without a fused kernel (use
+    ups_forward / syn_forward / post_forward)."""
     squeeze = latent.dim() == 1
     latent = latent.unsqueeze(0) if squeeze else latent
     B, N = latent.shape
@@ -211,7 +212,8 @@ def decode_forward(latent: torch.Tensor, sizes, ups_params: torch.Tensor, ups_k:
     y = _syn_args(latent, layers, syn_params, out.view(B, -1, H, W) if (bitdepth == 0 or not yuv420) else out,
                   B, L, H, W, syn_stride)
     y.in_ = None
-    a = DecodeArgs(ups=u, syn=y, bitdepth=int(bitdepth), yuv420=int(bool(yuv420)), out=ptr(out), out_stride=n)
+    a = DecodeArgs(ups=u, syn=y, bitdepth=int(bitdepth), yuv420=int(bool(yuv420)), out=ptr(out), out_stride=n,
+                   head=int(head))
     check(lib().ccmi_decode_forward_f32(a, stream_handle(latent.device)))
     if bitdepth == 0 or not yuv420:
         out = out.view(B, n_out, H, W)

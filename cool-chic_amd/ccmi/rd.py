@@ -92,10 +92,8 @@ def encode_batch(targets: torch.Tensor, H: int, W: int, lmbda: float, arch, *, n
                           warmup=warm, phases=phases)
     torch.cuda.synchronize()
     dt = time.perf_counter() - t0
-    # counted as the reference's results columns count them: every warm-up candidate's
-    # iterations (3 x 10 + 2 x 10 for debug), then the phases
-    its = sum(n * max(1, int(p.max_itr * scale)) for n, p in warm) + \
-        sum(max(1, int(p.max_itr * scale)) for p in phases)
+    # counted as the reference's iterations_counter: every warm-up candidate's iterations
+    # (3 x 10 + 2 x 10 for debug), then each frame's phases up to its early stop
     out = []
     for b in range(B):
         mse, rate_lat = quantize.evaluate(arch, of.latents[b], of.params[b], of.targets[b], yuv420=yuv420, bitdepth=8)
@@ -103,7 +101,7 @@ def encode_batch(targets: torch.Tensor, H: int, W: int, lmbda: float, arch, *, n
         nn_bits = sum(qm.nn_bits.values()) if qm else 0.0
         rec = Record(image=names[b], lmbda=float(lmbda), seed=int(seeds[b]), psnr_db=-10 * math.log10(mse + 1e-10),
                      rate_bpp=(rate_lat + nn_bits) / npx, rate_latent_bpp=rate_lat / npx, rate_nn_bpp=nn_bits / npx,
-                     iterations=its, seconds=dt / B)
+                     iterations=int(of.iterations[b]), seconds=dt / B)
         if write and qm is not None:
             rec.cool_bpp = 8 * len(encode.write_cool(arch, of.latents[b], qm, yuv420=yuv420)) / npx
         out.append(rec)

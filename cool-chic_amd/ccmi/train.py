@@ -40,7 +40,7 @@ class TrainArgs(C.Structure):
         ("noise_in", C.c_void_p), ("grad_out", C.c_void_p), ("loss_out", C.c_void_p), ("update", C.c_int),
         ("workspace", C.c_void_p), ("workspace_bytes", C.c_size_t),
         ("forward_only", C.c_int), ("raw_out", C.c_void_p), ("rate_out", C.c_void_p), ("grad_raw", C.c_void_p),
-        ("grad_rate", C.c_void_p),
+        ("grad_rate", C.c_void_p), ("adam_steps", C.c_void_p),
     ]
 
 
@@ -142,6 +142,10 @@ class Overfitter:
         dev = self.latents.device
         self.m = torch.zeros(self.B, self.N + P, device=dev)
         self.v = torch.zeros(self.B, self.N + P, device=dev)
+        # each frame's Adam step (frames diverge when one reloads its best optimizer state,
+        # train.py:226-236); uniform steps use the scalar path
+        self.steps = torch.zeros(self.B, dtype=torch.int32, device=dev)
+        self.steps_uniform = True
         self.loss = torch.zeros(self.B, 4, device=dev)
         self.ws = torch.empty(L.ccmi_train_workspace_bytes(C.byref(a)), dtype=torch.uint8, device=dev)
 
@@ -149,7 +153,15 @@ class Overfitter:
         """A new torch.optim.Adam: every training phase builds its own (train.py:184)."""
         self.m.zero_()
         self.v.zero_()
+        self.steps.zero_()
+        self.steps_uniform = True
         self.t = 0
+
+    def _realloc(self):
+        self.loss = torch.zeros(self.B, 4, device=self.latents.device)
+        a = self._args()
+        self.ws = torch.empty(_bind().ccmi_train_workspace_bytes(C.byref(a)), dtype=torch.uint8,
+                              device=self.latents.device)
 
     def keep(self, idx: torch.Tensor):
         """Keep frames idx (a [B'] index tensor) of the batch, in that order."""
@@ -158,11 +170,22 @@ class Overfitter:
         self.params = self.params[idx].contiguous()
         self.targets = self.targets[idx].contiguous()
         self.m, self.v = self.m[idx].contiguous(), self.v[idx].contiguous()
+        self.steps = self.steps[idx].contiguous()
         self.B = int(idx.numel())
-        self.loss = torch.zeros(self.B, 4, device=self.latents.device)
-        a = self._args()
-        self.ws = torch.empty(_bind().ccmi_train_workspace_bytes(C.byref(a)), dtype=torch.uint8,
-                              device=self.latents.device)
+        self._realloc()
+
+    def reset_batch(self, latents: torch.Tensor, params: torch.Tensor, targets: torch.Tensor):
+        """Replace the batch (fresh optimizer state)."""
+        self.latents, self.params = latents.float().contiguous(), params.float().contiguous()
+        self.targets = targets.float().contiguous()
+        self.B = self.latents.shape[0]
+        dev = self.latents.device
+        self.m = torch.zeros(self.B, self.N + self.P, device=dev)
+        self.v = torch.zeros(self.B, self.N + self.P, device=dev)
+        self.steps = torch.zeros(self.B, dtype=torch.int32, device=dev)
+        self.steps_uniform = True
+        self.t = 0
+        self._realloc()
 
     def validate(self, lmbda: float) -> torch.Tensor:
         """Loss of the hard-rounded forward (train.py test(): quantizer "hardround", no
@@ -194,6 +217,9 @@ class Overfitter:
         a = self._args()
         if update:
             self.t += 1
+            self.steps += 1
+            if not self.steps_uniform:
+                a.adam_steps = self.steps.data_ptr()
         a.adam_m, a.adam_v = self.m.data_ptr(), self.v.data_ptr()
         a.quantizer, a.noise = Q_TYPES[quantizer_type], NOISE_TYPES[quantizer_noise_type]
         a.temperature, a.noise_param, a.lmbda = float(soft_round_temperature), float(noise_parameter), float(lmbda)
@@ -283,34 +309,89 @@ def run_phase(of: Overfitter, ph: Phase, lmbda: float, scale: float = 1.0) -> to
     temperature / noise schedules, validation every freq_valid iterations keeping each
     frame's best parameters (restored at the end of the phase).  A validation is a new
     record when its loss is lower AND it gains more than 0.001 dB or loses less than
-    0.001 bpp (train.py:280-289).  Patience-based early stopping is not applied: the batch
-    runs max_itr and keeps each frame's best record, which can only be at least as good as
-    the record the reference stops at.  Returns the best validation [B, 4]."""
+    0.001 bpp (train.py:280-289).
+
+    Patience, per frame, as train.py:226-240: at the start of iteration cnt, a frame whose
+    last record is more than `patience` iterations old either reloads its best parameters
+    and Adam state (cosine-scheduled phases; the learning rate stays the schedule's) or
+    stops (other phases: it leaves the batch, so the remaining frames run alone).  With
+    scale < 1, patience and freq_valid are scaled like max_itr (as tools/gen_golden_rd.py
+    scales the reference's presets).  Sets of.phase_iterations (per frame of the batch, in
+    batch order).  Returns the best validation [B, 4]."""
     n = max(1, int(ph.max_itr * scale))
     freq = max(1, int(ph.freq_valid * scale)) if scale < 1 else ph.freq_valid
+    pat = max(1, int(ph.patience * scale)) if scale < 1 else ph.patience
     npx = of.arch.sizes[0][0] * of.arch.sizes[0][1]
+    B0 = of.B
+    dev = of.latents.device
     of.reset_optimizer()
-    best = of.validate(lmbda)
+    best = of.validate(lmbda).clone()
     best_lat, best_prm = of.latents.clone(), of.params.clone()
+    # reload targets: Adam moments and steps at the record (cosine phases only)
+    reload = ph.schedule_lr and pat < n
+    if reload:
+        best_m, best_v, best_st = of.m.clone(), of.v.clone(), of.steps.clone()
+    full_tg = of.targets
+    rows = list(range(B0))                   # frame (original batch index) of each row of `of`
+    rec = [0] * B0                           # cnt_record per frame
+    its = [0] * B0
     T = ph.softround_temperature[0]
     nz = ph.noise_parameter[0]
     upd = "latent" if ph.optimized_module == "latent" else True
     for cnt in range(n):
+        late = [r for r, f in enumerate(rows) if cnt - rec[f] > pat]
+        if late:
+            if reload:
+                ri = torch.tensor(late, device=dev)
+                fi = torch.tensor([rows[r] for r in late], device=dev)
+                of.latents[ri] = best_lat[fi]
+                of.params[ri] = best_prm[fi]
+                of.m[ri] = best_m[fi]
+                of.v[ri] = best_v[fi]
+                of.steps[ri] = best_st[fi]
+                of.steps_uniform = False
+                for r in late:
+                    rec[rows[r]] = cnt
+            else:
+                keep = [r for r in range(len(rows)) if r not in late]
+                if not keep:
+                    break
+                of.keep(torch.tensor(keep, device=dev))
+                rows = [rows[r] for r in keep]
         lr = cosine_lr(ph.lr, ph.end_lr, cnt, n, freq) if ph.schedule_lr else ph.lr
         of.step(ph.quantizer_type, ph.quantizer_noise_type, T, nz, lmbda, lr=lr, update=upd)
+        for f in rows:
+            its[f] += 1
         if (cnt + 1) % freq == 0 or cnt + 1 == n:
             cur = of.validate(lmbda)
-            d_psnr = 10 * torch.log10(best[:, 1].clamp_min(1e-10) / cur[:, 1].clamp_min(1e-10))
-            d_bpp = (cur[:, 2] - best[:, 2]) / npx
-            better = (cur[:, 0] < best[:, 0]) & ((d_bpp < 1e-3) | (d_psnr > 1e-3))
-            if bool(better.any()):
-                best = torch.where(better[:, None], cur, best)
-                best_lat = torch.where(better[:, None], of.latents, best_lat)
-                best_prm = torch.where(better[:, None], of.params, best_prm)
+            fi = torch.tensor(rows, device=dev)
+            bst = best[fi]
+            d_psnr = 10 * torch.log10(bst[:, 1].clamp_min(1e-10) / cur[:, 1].clamp_min(1e-10))
+            d_bpp = (cur[:, 2] - bst[:, 2]) / npx
+            better = (cur[:, 0] < bst[:, 0]) & ((d_bpp < 1e-3) | (d_psnr > 1e-3))
+            bl = better.tolist()
+            if any(bl):
+                ri = torch.tensor([r for r, v in enumerate(bl) if v], device=dev)
+                fb = fi[ri]
+                best[fb] = cur[ri]
+                best_lat[fb] = of.latents[ri]
+                best_prm[fb] = of.params[ri]
+                if reload:
+                    best_m[fb] = of.m[ri]
+                    best_v[fb] = of.v[ri]
+                    best_st[fb] = of.steps[ri]
+                for r, v in enumerate(bl):
+                    if v:
+                        rec[rows[r]] = cnt
             T = linear(ph.softround_temperature[0], ph.softround_temperature[1], cnt, n)
             nz = linear(ph.noise_parameter[0], ph.noise_parameter[1], cnt, n)
-    of.latents.copy_(best_lat)
-    of.params.copy_(best_prm)
+    # every frame ends on its best record (train.py:372-373)
+    if len(rows) == B0:
+        of.latents.copy_(best_lat)
+        of.params.copy_(best_prm)
+    else:
+        of.reset_batch(best_lat, best_prm, full_tg)
+    of.phase_iterations = its
     return best
 
 
@@ -321,8 +402,8 @@ def overfit(arch: Arch, targets: torch.Tensor, lmbda: float, yuv420: bool = True
     as one batch; after each warm-up stage each frame keeps its best candidates.  After a
     phase flagged quantize_model, every frame's networks are quantised
     (ccmi.quantize.quantize_model, as video.py:302-310) and later phases train with them;
-    the per-frame QuantizedModel list is state.quantized (None if no phase asks for it).
-    Returns (state, best validation)."""
+    the per-frame QuantizedModel list is state.quantized (None if no phase asks for it);
+    state.iterations the per-frame iteration counts.  Returns (state, best validation)."""
     dev = targets.device
     B = targets.shape[0]
     n0 = warmup[0][0] if warmup else 1
@@ -331,8 +412,12 @@ def overfit(arch: Arch, targets: torch.Tensor, lmbda: float, yuv420: bool = True
     lat = torch.zeros(B * n0, arch.n_latents, device=dev)
     of = Overfitter(arch, lat, params, targets.repeat_interleave(n0, dim=0), yuv420=yuv420, seed=seed)
     ncand = n0
+    # iterations per image as the reference's FrameEncoderManager.iterations_counter counts
+    # them: every warm-up candidate's, then the phases' (early stops included)
+    warm_its = 0
     for i, (_, ph) in enumerate(warmup):
         res = run_phase(of, ph, lmbda, scale)
+        warm_its += ncand * max(of.phase_iterations)
         keep = warmup[i + 1][0] if i + 1 < len(warmup) else 1
         order = torch.argsort(res[:, 0].view(B, ncand), dim=1)[:, :keep]
         idx = (order + torch.arange(B, device=order.device)[:, None] * ncand).reshape(-1)
@@ -340,8 +425,10 @@ def overfit(arch: Arch, targets: torch.Tensor, lmbda: float, yuv420: bool = True
         ncand = keep
     best = None
     of.quantized = None
+    of.iterations = [warm_its] * of.B
     for ph in phases:
         best = run_phase(of, ph, lmbda, scale)
+        of.iterations = [a + b for a, b in zip(of.iterations, of.phase_iterations)]
         if ph.quantize_model:
             from .quantize import quantize_model
             qms = []

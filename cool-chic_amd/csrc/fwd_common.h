@@ -31,7 +31,7 @@ struct FusedArgs {
     int cin, H, W;
     int n_head;          // 1 or 2 1x1 layers
     int hid;             // hidden width of a 2-layer head
-    int head_mfma;       // 2-layer head: first layer on split-f16 MFMA (fwd_syn.hip)
+    int head_mfma;       // 2-layer head on the f32 MFMA form (fwd_syn.hip, CCMI_HEAD_MFMA)
     int w0_off, b0_off, relu0;
     int w1_off, b1_off, relu1;
     int n_sp;            // 3x3 layers after the head

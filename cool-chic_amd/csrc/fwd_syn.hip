@@ -85,30 +85,30 @@ __device__ __forceinline__ void store_out(const FusedArgs &A, float *out, int64_
     }
 }
 
-// ---- split-f16 MFMA head (first 1x1 layer) ---------------------------------------------
-// v_mfma_f32_32x32x16_f16 (2.5 PF dense) with every f32 operand split as hi = f16(v),
-// lo = f16(v - hi): W X ~= Wh Xh + Wh Xl + Wl Xh, the dropped Wl Xl and the rounding of the lo
-// parts leave ~2^-22 of sum |w x| (tools/mfma_f16_probe.hip: 4.7e-7 worst on 8-term dots),
-// accumulation in f32.  Operands need |v| < 65504 (f16 range).
-// Lane maps (probe-checked): A[m = l & 31][k = 8 (l >> 5) + j], B[k = 8 (l >> 5) + j][n = l & 31],
-// accumulator register r of lane l = D[m = (r & 3) + 8 (r >> 2) + 4 (l >> 5)][n = l & 31].
-// K = 16 is [Xh | Xl] (half 0 | half 1 of the wave), the input's 8 slots being c_in channels,
-// a constant 1 (the bias column) and zeros.  Hidden tiles of 32 units take two MFMAs
-// (A = [Wh | Wh], then [Wl | 0]); a tile of <= 16 units takes one, its rows 0..15 carrying
-// [Wh | Wh] and rows 16..31 [Wl | 0] of the same units, summed afterwards (registers r, r + 8).
-typedef _Float16 h8 __attribute__((ext_vector_type(8)));
-typedef float f16x __attribute__((ext_vector_type(16)));
-typedef unsigned u4v __attribute__((ext_vector_type(4)));
+// ---- exact-f32 MFMA head (both 1x1 layers' products of the first, the hidden layer) -------
+// v_mfma_f32_16x16x4_f32: D[16 x 16] += A[16 x 4] B[4 x 16], each product an exact f32 fma
+// (the instruction is an fmaf chain over its K = 4, MI355X_MICROARCH.md "Matrix cores").
+// Lane l = (g = l >> 4, r = l & 15) supplies A[m = r][k = g] and B[k = g][n = r] and holds
+// D[m = 4 g + i][n = r] in accumulator register i.  The head's first layer is
+// H[unit][px] = W0[unit][ch] X[ch][px] with M = 16 hidden units per tile, N = 16 pixels,
+// K = 8 = the c_in channels, a constant 1 (its weight is the bias) and zeros, in two
+// K-steps; the MFMA pipe then carries 7/10 of the head's multiply-adds while the VALU does
+// the ReLU and the 48 -> 3 layer from the accumulators.
+typedef float v4f __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ v4f mfma16(float a, float b, v4f c) { return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0); }
 
-__device__ __forceinline__ f16x mfma32(h8 a, h8 b, f16x c) { return __builtin_amdgcn_mfma_f32_32x32x16_f16(a, b, c, 0, 0, 0); }
-
-__device__ __forceinline__ void split8(const float (&v)[8], h8 &hi, h8 &lo)
+// 4 x 4 transpose of 16-lane rows over four registers: on return, row j of t[g] is row g of
+// the input v[j] (two permlane16 swaps, then two permlane32 swaps)
+__device__ __forceinline__ void rows_transpose4(const float (&v)[4], float (&t)[4])
 {
-#pragma unroll
-    for (int j = 0; j < 8; ++j) {
-        hi[j] = (_Float16)v[j];
-        lo[j] = (_Float16)(v[j] - (float)hi[j]);
-    }
+    const auto p = __builtin_amdgcn_permlane16_swap(__float_as_uint(v[0]), __float_as_uint(v[1]), false, false);
+    const auto q = __builtin_amdgcn_permlane16_swap(__float_as_uint(v[2]), __float_as_uint(v[3]), false, false);
+    const auto a = __builtin_amdgcn_permlane32_swap(p[0], q[0], false, false);
+    const auto b = __builtin_amdgcn_permlane32_swap(p[1], q[1], false, false);
+    t[0] = __uint_as_float(a[0]);
+    t[1] = __uint_as_float(b[0]);
+    t[2] = __uint_as_float(a[1]);
+    t[3] = __uint_as_float(b[1]);
 }
 
 #if defined(CCMI_ARM_STAMPS)
@@ -144,12 +144,15 @@ constexpr int fused_lds_floats(int cin, int cmid, bool ups)
     const int stage = ups ? GC * kHsRows * kRW + kHrRows * kRW : 0;
     const int b0 = cmid * kPlane > raw ? cmid * kPlane : raw;
     int b1 = cmid * kPlane > stage ? cmid * kPlane : stage;
-    b1 = b1 > kMaxHid * 16 ? b1 : kMaxHid * 16;
+    b1 = b1 > kMaxHid * 16 + 256 ? b1 : kMaxHid * 16 + 256; // head records (+ the MFMA head's weight table)
     return b0 + b1 + 256; // + the 8-bit quotient table
 }
 // waves per SIMD the register allocation must allow: 3 workgroups of 8 waves on 4 SIMDs when
 // the LDS fits three (<= 160 KB / 3), else 2
-constexpr int fused_wpe(int cin, int cmid, bool ups) { return 4 * fused_lds_floats(cin, cmid, ups) <= 160 * 1024 / 3 ? 6 : 4; }
+constexpr int fused_wpe(int cin, int cmid, bool ups, bool mh = false)
+{
+    return !mh && 4 * fused_lds_floats(cin, cmid, ups) <= 160 * 1024 / 3 ? 6 : 4;
+}
 
 // MH: split-f16 MFMA first head layer (a separate instantiation: compiled into the default
 // kernel as a runtime branch, its registers pushed the VALU variant from 108 to 133 VGPRs,
@@ -157,7 +160,7 @@ constexpr int fused_wpe(int cin, int cmid, bool ups) { return 4 * fused_lds_floa
 // HID > 0: the 2-layer head's hidden width fixed at compile time (fully unrolled unit loop:
 // weight records at immediate LDS offsets, no loop counter or record rotation)
 template <int CIN, int CMID, bool UPS, bool MH = false, int HID = 0>
-__global__ __launch_bounds__(kFThreads) __attribute__((amdgpu_waves_per_eu(fused_wpe(CIN, CMID, UPS)))) void syn_fused_kernel(FusedArgs A, LevelArgs U)
+__global__ __launch_bounds__(kFThreads) __attribute__((amdgpu_waves_per_eu(fused_wpe(CIN, CMID, UPS, MH)))) void syn_fused_kernel(FusedArgs A, LevelArgs U)
 {
     constexpr int NR = kRowsPerThread;
     constexpr int C = UPS ? CIN - 1 : 0, NG = fused_groups(CIN, UPS), GC = (C + NG - 1) / NG;
@@ -183,6 +186,7 @@ __global__ __launch_bounds__(kFThreads) __attribute__((amdgpu_waves_per_eu(fused
     // four broadcast ds_read_b128 (all lanes, one address) -- the loads are issued well
     // ahead of use, unlike the SGPR path whose scalar loads the compiler waits on at once
     float(*s_head)[16] = reinterpret_cast<float(*)[16]>(s_pool + kBuf0);
+    float *s_w1p = s_pool + kBuf0 + kMaxHid * 16; // MH: the second layer's weights by lane row
     static_assert(CIN + 1 + CMID <= 16, "hidden-unit record");
     // field f of a record sits at slot hr(f): slots 3, 7, 11, 15 (the last dword of each
     // ds_read_b128) stay empty when the fields fit without them, because the compiler
@@ -215,10 +219,11 @@ __global__ __launch_bounds__(kFThreads) __attribute__((amdgpu_waves_per_eu(fused
     // cost spill slots at the 80-VGPR budget
     constexpr int kHeadRegs = kMaxHid * 16 / kFThreads;
     auto stage_head = [&]() {
+        const int tid = threadIdx.x;
         float hv[kHeadRegs];
 #pragma unroll
         for (int k = 0; k < kHeadRegs; ++k) {
-            const int i = threadIdx.x + k * kFThreads, j = i >> 4, f = i & 15;
+            const int i = tid + k * kFThreads, j = i >> 4, f = i & 15;
             float v = 0.f;
             if (A.n_head == 2 && j < A.hid) {
                 if (f < CIN) v = prm[A.w0_off + j * CIN + f];
@@ -229,8 +234,19 @@ __global__ __launch_bounds__(kFThreads) __attribute__((amdgpu_waves_per_eu(fused
         }
 #pragma unroll
         for (int k = 0; k < kHeadRegs; ++k) {
-            const int i = threadIdx.x + k * kFThreads, j = i >> 4, f = i & 15;
+            const int i = tid + k * kFThreads, j = i >> 4, f = i & 15;
             if (f <= CIN + CMID) s_head[j][hr(f)] = hv[k]; // other slots are never operands
+        }
+        if constexpr (MH) {
+            // [tile][lane row][m][4 units]: the second layer's weights of the 4 hidden units a
+            // lane's accumulator registers hold (one ds_read_b128 per output channel)
+            constexpr int n = (HID / 16) * 4 * CMID * 4;
+            static_assert(n <= kFThreads, "one entry per thread");
+            const int i = tid;
+            if (i < n) {
+                const int u4 = i & 3, m = (i >> 2) % CMID, lgi = (i / (4 * CMID)) & 3, mt = i / (16 * CMID);
+                s_w1p[i] = prm[A.w1_off + m * A.hid + 16 * mt + 4 * lgi + u4];
+            }
         }
     };
     if constexpr (!UPS) {
@@ -489,107 +505,81 @@ __global__ __launch_bounds__(kFThreads) __attribute__((amdgpu_waves_per_eu(fused
         }
         FSTAMP(2);
         if constexpr (MH) {
-            // ---- split-f16 MFMA first layer, second layer on VALU from the accumulators
-            const int hid = A.hid, lane = threadIdx.x & 63, hh = lane >> 5, m32 = lane & 31;
-            const bool t1_full = hid > 16, t2 = hid > 32, t2_full = hid > 48;
-            __syncthreads(); // s_head staged
-            // A operands of this lane (row m32 of each hidden tile)
-            h8 a1h, a1l, a2h, a2l;
-            {
-                auto wrow = [&](int u, float (&v)[8]) {
+            // ---- exact-f32 MFMA first layer (+ bias), ReLU and the second layer on the VALU
+            // from the accumulators; per window row, four 16-pixel groups per wave
+            static_assert(HID % 16 == 0 && HID <= kMaxHid && CIN + 1 <= 8 && CMID <= 4, "f32-MFMA head shape");
+            constexpr int NT = HID / 16;
+            const int lane = threadIdx.x & 63, lr = lane & 15, lg = lane >> 4;
+            __syncthreads(); // s_head / s_w1p staged
+            float a1[NT][2]; // A[m = lr][k = lg] of K-step s: W0[16 mt + lr][4 s + lg] (channel c_in: the bias)
 #pragma unroll
-                    for (int j = 0; j < 8; ++j) v[j] = (u < hid && j <= CIN) ? s_head[u][hr(j)] : 0.f;
-                };
-                float v[8];
-                h8 hi, lo, z = {};
-                // tile 1: units 0..31 (full) or 0..15 (packed: rows >= 16 hold the lo parts)
-                wrow(t1_full ? m32 : (m32 & 15), v);
-                split8(v, hi, lo);
-                a1h = (t1_full || m32 < 16) ? hi : (hh == 0 ? lo : z);
-                a1l = hh == 0 ? lo : z;
-                wrow(t2_full ? 32 + m32 : 32 + (m32 & 15), v);
-                split8(v, hi, lo);
-                a2h = (t2_full || m32 < 16) ? hi : (hh == 0 ? lo : z);
-                a2l = hh == 0 ? lo : z;
-            }
-            // second-layer weights of the units this lane's accumulator registers hold
-            const float4 *w1v = reinterpret_cast<const float4 *>(&s_head[0][0]);
-            auto wl2 = [&](int u) -> float4 { // w1[0..CMID)[u]
-                const float *r = s_head[u];
-                return float4{r[hr(CIN + 1)], CMID > 1 ? r[hr(CIN + 2)] : 0.f, CMID > 2 ? r[hr(CIN + 3)] : 0.f,
-                              CMID > 3 ? r[hr(CIN + 4)] : 0.f};
-            };
-            (void)w1v;
-            const float lo0 = A.relu0 ? 0.f : -INFINITY;
+            for (int mt = 0; mt < NT; ++mt)
+#pragma unroll
+                for (int k = 0; k < 2; ++k) {
+                    const int ch = 4 * k + lg;
+                    a1[mt][k] = ch <= CIN ? s_head[16 * mt + lr][hr(ch < CIN ? ch : CIN)] : 0.f;
+                }
+            const f2 lo0 = f2(A.relu0 ? 0.f : -INFINITY);
+            const float lo1 = A.relu1 ? 0.f : -INFINITY;
+            typedef const __attribute__((address_space(3))) v4f *lds_v4;
+            lds_v4 wb = (lds_v4)s_w1p;
+            asm volatile("" : "+v"(wb));
 #pragma unroll
             for (int p = 0; p < NR; ++p) {
-                // this lane's pixel (column c, row p): [x | 1 | 0] split, then both 32-pixel
-                // operands by one lane-half swap per dword
-                float xv[8];
+                // the weight table re-read per row (an opaque base: held across rows it costs 36
+                // registers)
+                asm volatile("" : "+v"(wb));
+                // B operands: channel 4 s + lg of pixel 16 g + lr, by two 16-lane-row transposes
+                float T[2][4];
+                {
+                    float v0[4], v1[4];
 #pragma unroll
-                for (int j = 0; j < 8; ++j) xv[j] = j < CIN ? x[p][j] : (j == CIN ? 1.f : 0.f);
-                h8 xh, xl;
-                split8(xv, xh, xl);
-                const u4v uh = __builtin_bit_cast(u4v, xh), ul = __builtin_bit_cast(u4v, xl);
-                u4v b0u, b1u;
-#pragma unroll
-                for (int d = 0; d < 4; ++d) {
-                    const auto r = __builtin_amdgcn_permlane32_swap(uh[d], ul[d], false, false);
-                    b0u[d] = r[0]; // columns 0..31: [Xh | Xl]
-                    b1u[d] = r[1]; // columns 32..63
+                    for (int k = 0; k < 4; ++k) {
+                        v0[k] = k < CIN ? x[p][k] : (k == CIN ? 1.f : 0.f);
+                        v1[k] = 4 + k < CIN ? x[p][4 + k] : (4 + k == CIN ? 1.f : 0.f);
+                    }
+                    rows_transpose4(v0, T[0]);
+                    rows_transpose4(v1, T[1]);
                 }
-                float po[2][CMID];
+                float P[4][CMID]; // partial outputs of this lane's 4 units per tile, pixel 16 g + lr
 #pragma unroll
-                for (int n = 0; n < 2; ++n) {
-                    const h8 bn = __builtin_bit_cast(h8, n ? b1u : b0u);
-                    f16x acc1 = {}, acc2 = {};
-                    acc1 = mfma32(a1h, bn, acc1);
-                    if (t1_full) acc1 = mfma32(a1l, bn, acc1);
-                    if (t2) {
-                        acc2 = mfma32(a2h, bn, acc2);
-                        if (t2_full) acc2 = mfma32(a2l, bn, acc2);
-                    }
+                for (int gh = 0; gh < 2; ++gh) {
+                    f2 P2[2][CMID];
 #pragma unroll
-                    for (int m = 0; m < CMID; ++m) po[n][m] = 0.f;
-                    // tile 1
+                    for (int gi = 0; gi < 2; ++gi)
 #pragma unroll
-                    for (int r = 0; r < 16; ++r) {
-                        const int u0 = (r & 3) + 8 * (r >> 2) + 4 * hh;
-                        float hv;
-                        int u;
-                        if (t1_full) { hv = acc1[r]; u = u0; }
-                        else { if (r >= 8) break; hv = acc1[r] + acc1[r + 8]; u = u0; }
-                        hv = fmaxf(hv, lo0);
-                        const float4 w = wl2(u);
-                        po[n][0] = fmaf(w.x, hv, po[n][0]);
-                        if constexpr (CMID > 1) po[n][1] = fmaf(w.y, hv, po[n][1]);
-                        if constexpr (CMID > 2) po[n][2] = fmaf(w.z, hv, po[n][2]);
-                        if constexpr (CMID > 3) po[n][3] = fmaf(w.w, hv, po[n][3]);
-                    }
-                    if (t2) {
+                        for (int m = 0; m < CMID; ++m) P2[gi][m] = f2(0.f);
 #pragma unroll
-                        for (int r = 0; r < 16; ++r) {
-                            const int u0 = 32 + (r & 3) + 8 * (r >> 2) + 4 * hh;
-                            float hv;
-                            if (t2_full) hv = acc2[r];
-                            else { if (r >= 8) break; hv = acc2[r] + acc2[r + 8]; }
-                            hv = fmaxf(hv, lo0);
-                            const float4 w = wl2(u0);
-                            po[n][0] = fmaf(w.x, hv, po[n][0]);
-                            if constexpr (CMID > 1) po[n][1] = fmaf(w.y, hv, po[n][1]);
-                            if constexpr (CMID > 2) po[n][2] = fmaf(w.z, hv, po[n][2]);
-                            if constexpr (CMID > 3) po[n][3] = fmaf(w.w, hv, po[n][3]);
+                    for (int mt = 0; mt < NT; ++mt) {
+                        v4f w[CMID]; // w1[m][16 mt + 4 lg + i], i = 0..3
+#pragma unroll
+                        for (int m = 0; m < CMID; ++m) w[m] = wb[(mt * 4 + lg) * CMID + m];
+#pragma unroll
+                        for (int gi = 0; gi < 2; ++gi) {
+                            const int g = 2 * gh + gi;
+                            v4f acc = mfma16(a1[mt][0], T[0][g], v4f{0.f, 0.f, 0.f, 0.f});
+                            acc = mfma16(a1[mt][1], T[1][g], acc);
+                            const f2 h01 = __builtin_elementwise_max(f2{acc[0], acc[1]}, lo0);
+                            const f2 h23 = __builtin_elementwise_max(f2{acc[2], acc[3]}, lo0);
+#pragma unroll
+                            for (int m = 0; m < CMID; ++m) {
+                                P2[gi][m] = __builtin_elementwise_fma(f2{w[m][0], w[m][1]}, h01, P2[gi][m]);
+                                P2[gi][m] = __builtin_elementwise_fma(f2{w[m][2], w[m][3]}, h23, P2[gi][m]);
+                            }
                         }
                     }
+#pragma unroll
+                    for (int gi = 0; gi < 2; ++gi)
+#pragma unroll
+                        for (int m = 0; m < CMID; ++m) P[2 * gh + gi][m] = P2[gi][m].x + P2[gi][m].y;
                 }
-                // the two halves of the wave hold complementary units of the same pixels:
-                // one swap brings both partial sums of this lane's own column together
-                const float lo1 = A.relu1 ? 0.f : -INFINITY;
+                // sum over the 4 lane rows (unit groups) and return to lane = column
 #pragma unroll
                 for (int m = 0; m < CMID; ++m) {
-                    const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(po[0][m]), __float_as_uint(po[1][m]),
-                                                                     false, false);
-                    o[p][m] = fmaxf(__uint_as_float(r[0]) + __uint_as_float(r[1]) + b1[m], lo1);
+                    const float v[4] = {P[0][m], P[1][m], P[2][m], P[3][m]};
+                    float t[4];
+                    rows_transpose4(v, t);
+                    o[p][m] = fmaxf(((t[0] + t[1]) + (t[2] + t[3])) + b1[m], lo1);
                 }
             }
         } else if (A.n_head == 2) {
@@ -883,12 +873,13 @@ void launch_fused(dim3 grid, hipStream_t s, const FusedArgs &fa, const LevelArgs
     }
 }
 
-// opt-in MFMA-head variant: the 7-grid decoders with upsampling fused (the common case) only
+// f32-MFMA head variant (ccmi_decode_args.head = CCMI_HEAD_MFMA): the 7-grid decoders with a
+// 48-wide head, upsampling fused and at least one 3x3 layer
 template <int CMID>
 bool launch_fused_mfma_head(dim3 grid, hipStream_t s, const FusedArgs &fa, const LevelArgs &u)
 {
-    if (fa.cin != 7 || !fa.head_mfma) return false;
-    hipLaunchKernelGGL((syn_fused_kernel<7, CMID, true, true>), grid, dim3(kFThreads), 0, s, fa, u);
+    if (!fa.head_mfma || fa.cin != 7 || fa.n_head != 2 || fa.hid != 48 || fa.n_sp < 1) return false;
+    hipLaunchKernelGGL((syn_fused_kernel<7, CMID, true, true, 48>), grid, dim3(kFThreads), 0, s, fa, u);
     return true;
 }
 
@@ -947,11 +938,6 @@ bool make_plan(const ccmi_syn_args *a, Plan *P)
         f.w1_off = w_off[1];
         f.b1_off = b_off[1];
         f.relu1 = L[1].relu;
-        // split-f16 MFMA first layer (c_in + bias in one 8-wide K slice, <= 64 hidden units):
-        // parity-green but measured slower than the VALU head in this latency-bound kernel
-        // (DESIGN.md section 5), so opt-in
-        static const bool mfma_head = getenv("CCMI_SYN_MFMA_HEAD") != nullptr;
-        f.head_mfma = mfma_head && a->c_in + 1 <= 8 && hid <= 64 && cmid <= 4;
     }
     f.n_sp = n_sp;
     for (int s = 0; s < n_sp; ++s) {
@@ -1079,6 +1065,8 @@ extern "C" int ccmi_decode_forward_f32(const ccmi_decode_args *a, void *stream)
     P.fa.out_stride = a->out_stride;
     P.fa.qmax = a->bitdepth > 0 ? (float)((1 << a->bitdepth) - 1) : 0.f;
     P.fa.yuv420 = a->yuv420;
+    if (a->head < CCMI_HEAD_DEFAULT || a->head > CCMI_HEAD_MFMA) return ccmi_set_error(CCMI_ERR_ARG, "decode: head %d", a->head);
+    P.fa.head_mfma = a->head == CCMI_HEAD_MFMA;
     const int halo = P.fa.n_sp;
     P.fa.tiles_x = ccmi_div_up(y.w, kRW - 2 * halo);
     dim3 grid(P.fa.tiles_x * ccmi_div_up(y.h, kRH - 2 * halo), y.batch);

@@ -1693,7 +1693,27 @@ struct AdamArgs {
     float lr_bc1, inv_sqrt_bc2, beta1, beta2, eps, clip;
     int N, latents_only;
     int64_t n, gstride, ls, ps, ms;
+    const float *bc; // optional [B][2] per-frame (lr / bc1, 1 / sqrt(bc2)) (per-frame Adam steps)
 };
+
+// per-frame bias corrections when frames carry their own Adam step (a frame whose optimizer
+// state was reloaded from its best record, train.py:226-236): computed in double like the
+// host path (torch.optim.Adam's bias_correction1/2 are Python floats); step <= 0 freezes
+// the frame (lr 0)
+__global__ void t_adam_bc(const int32_t *__restrict__ steps, double lr, double beta1, double beta2, int B,
+                          float *__restrict__ bc)
+{
+    const int b = blockIdx.x * blockDim.x + threadIdx.x;
+    if (b >= B) return;
+    const int t = steps[b];
+    if (t <= 0) {
+        bc[2 * b] = 0.f;
+        bc[2 * b + 1] = 1.f;
+        return;
+    }
+    bc[2 * b] = (float)(lr / (1.0 - pow(beta1, (double)t)));
+    bc[2 * b + 1] = (float)(1.0 / sqrt(1.0 - pow(beta2, (double)t)));
+}
 
 // torch.optim.Adam (_single_tensor_adam, no weight decay / amsgrad) after clip_grad_norm_
 __global__ void t_adam(const float *__restrict__ G, float *__restrict__ lat, float *__restrict__ th, float *__restrict__ m,
@@ -1710,9 +1730,10 @@ __global__ void t_adam(const float *__restrict__ G, float *__restrict__ lat, flo
     const float vv = A.beta2 * v[mi] + (1.f - A.beta2) * g * g;
     m[mi] = mm;
     v[mi] = vv;
-    const float denom = sqrtf(vv) * A.inv_sqrt_bc2 + A.eps;
+    const float lr_bc1 = A.bc ? A.bc[2 * b] : A.lr_bc1, inv_sqrt_bc2 = A.bc ? A.bc[2 * b + 1] : A.inv_sqrt_bc2;
+    const float denom = sqrtf(vv) * inv_sqrt_bc2 + A.eps;
     float *p = i < A.N ? lat + (int64_t)b * A.ls + i : th + (int64_t)b * A.ps + (i - A.N);
-    *p -= A.lr_bc1 * mm / denom;
+    *p -= lr_bc1 * mm / denom;
 }
 
 __global__ void t_finish(const float *__restrict__ acc4, float inv_total, float lam_px, float *__restrict__ out, int B)
@@ -1735,7 +1756,7 @@ struct Plan {
     int B, nblk_arm;
     // workspace offsets (bytes)
     size_t yq, dq, gq, kf, stacks, stacks_bytes, dense, z[kMaxSp + 1], graw, gbuf[2], gdense, gstack, tmpU, tmpG, G,
-        acc4, slots, total;
+        acc4, bc, slots, total;
     int64_t gstack_off[CCMI_MAX_GRIDS]; // per level k (1..L-2) inside gstack, elements per frame
     int64_t gstack_per, stack_per, tmp_per;
 };
@@ -1865,6 +1886,7 @@ int make_plan(const ccmi_train_args *a, Plan &pl)
     pl.tmpG = take(4 * B * tmax);
     pl.G = take(4 * B * ((size_t)g.N + g.P));
     pl.acc4 = take(4 * B * 4);
+    pl.bc = take(4 * B * 2);
     pl.slots = take(4 * B * kDwSlots * (size_t)(g.syn_off - g.up_off));
     pl.total = o;
     return CCMI_OK;
@@ -1993,7 +2015,7 @@ extern "C" int ccmi_train_step(const ccmi_train_args *a, void *stream)
     if (int rc = make_plan(a, pl)) return rc;
     if (!a->workspace || a->workspace_bytes < pl.total)
         return ccmi_set_error(CCMI_ERR_ARG, "train: workspace of %zu bytes needed", pl.total);
-    if (a->update && (!a->adam_m || !a->adam_v || a->step < 1))
+    if (a->update && (!a->adam_m || !a->adam_v || (a->step < 1 && !a->adam_steps)))
         return ccmi_set_error(CCMI_ERR_ARG, "train: Adam state and step >= 1 needed to update");
     if ((a->quantizer == CCMI_Q_SOFTROUND || a->quantizer == CCMI_Q_SOFTROUND_ALONE || a->quantizer == CCMI_Q_STE) &&
         !(a->temperature > 0.f))
@@ -2185,7 +2207,12 @@ extern "C" int ccmi_train_step(const ccmi_train_args *a, void *stream)
         const double bc1 = 1.0 - std::pow((double)a->beta1, a->step), bc2 = 1.0 - std::pow((double)a->beta2, a->step);
         AdamArgs A{(float)(a->lr / bc1), (float)(1.0 / std::sqrt(bc2)), a->beta1, a->beta2, a->eps, a->clip, g.N,
                    a->update == 2 ? 1 : 0, GS, GS,
-                   a->latent_stride, a->param_stride, (int64_t)a->latent_stride + a->param_stride};
+                   a->latent_stride, a->param_stride, (int64_t)a->latent_stride + a->param_stride, nullptr};
+        if (a->adam_steps) {
+            A.bc = F(pl.bc);
+            hipLaunchKernelGGL(t_adam_bc, dim3((unsigned)ccmi_div_up(B, 64)), dim3(64), 0, s, a->adam_steps, (double)a->lr,
+                               (double)a->beta1, (double)a->beta2, B, F(pl.bc));
+        }
         hipLaunchKernelGGL(t_adam, grid1(GS, B), dim3(kT), 0, s, G, a->latent, a->params, a->adam_m, a->adam_v, acc4, A);
     }
     CCMI_HIP_CHECK(hipGetLastError());

@@ -176,7 +176,12 @@ typedef struct ccmi_decode_args {
     int stages;             /* 0 = all; bit 0: upsampling pyramid down to level 1 (into
                                ups.workspace), bit 1: the fused full-resolution kernel --
                                lets a caller time the two apart */
+    int head;               /* synthesis 1x1 head arithmetic, CCMI_HEAD_*: both are fp32 (the
+                               MFMA form's products are exact f32 fmas, summed in another
+                               order); MFMA needs 7 inputs, 48 hidden units and >= 1 3x3 layer
+                               and falls back to VALU otherwise */
 } ccmi_decode_args;
+enum { CCMI_HEAD_DEFAULT = 0, CCMI_HEAD_VALU = 1, CCMI_HEAD_MFMA = 2 };
 int ccmi_decode_forward_f32(const ccmi_decode_args *args, void *stream);
 
 /* ------------------------------------------------------------------------- */
@@ -408,6 +413,9 @@ typedef struct ccmi_train_args {
                                the built-in MSE term (whose value then reads 0 in loss_out) */
     const float *grad_rate; /* optional [batch][N]: d loss / d rate per latent, used instead of
                                the built-in lmbda / (H W) */
+    const int32_t *adam_steps; /* optional device [batch]: each frame's own Adam step (overrides
+                               `step`; a frame whose optimizer state was reloaded from its best
+                               record, train.py:226-236); a step <= 0 leaves that frame unchanged */
 } ccmi_train_args;
 size_t ccmi_train_param_count(const ccmi_train_args *args);
 size_t ccmi_train_workspace_bytes(const ccmi_train_args *args);

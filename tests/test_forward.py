@@ -228,30 +228,35 @@ def test_hip_rejects_cpu_tensors(ccmi_lib):
         F.syn_forward(torch.zeros(2, 8, 8), mp.layers, F.pack_syn(mp.syn))
 
 
-def _fused(mps, lats, dev, bitdepth, yuv420):
+HEADS = (1, 2)  # ccmi.HEAD_VALU, ccmi.HEAD_MFMA: the fused kernel's two 1x1-head forms
+
+
+def _fused(mps, lats, dev, bitdepth, yuv420, head=0):
     from ccmi import forward as F
     mp0 = mps[0]
     lat = torch.stack([torch.cat([x.reshape(-1) for x in l]) for l in lats]).to(dev)
     ups_p = torch.stack([F.pack_ups(mp.ups_full(), mp.pre_full()) for mp in mps]).to(dev)
     syn_p = torch.stack([F.pack_syn(mp.syn) for mp in mps]).to(dev)
     return F.decode_forward(lat, mp0.sizes, ups_p, mp0.ups_k, len(mp0.ups_half), mp0.pre_k, len(mp0.pre_half),
-                            mp0.layers, syn_p, mp0.gain, True, bitdepth, yuv420)
+                            mp0.layers, syn_p, mp0.gain, True, bitdepth, yuv420, head)
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("head", HEADS)
 @pytest.mark.parametrize("path", GOLDEN, ids=[p.stem for p in GOLDEN])
-def test_fused_decode_matches_reference_golden(path, gpu, ccmi_lib):
+def test_fused_decode_matches_reference_golden(path, head, gpu, ccmi_lib):
     """ccmi_decode_forward_f32 (upsampling + synthesis + post in one kernel) against the
-    reference's synthesis output and decoded frames."""
+    reference's synthesis output and decoded frames, with either head form (the MFMA form
+    applies to the 48-wide 7-grid decoders and falls back to the VALU head otherwise)."""
     from ccmi import forward as F
     z = np.load(path)
     mp = fo.ModelParams.from_npz(z)
-    raw = _fused([mp], [_lat(z, mp)], gpu, 0, False)
+    raw = _fused([mp], [_lat(z, mp)], gpu, 0, False, head)
     np.testing.assert_allclose(raw[0].cpu().numpy(), z["syn"], rtol=0, atol=_tol(z["syn"]))
-    dec = _fused([mp], [_lat(z, mp)], gpu, 8, False)[0].cpu().numpy()
+    dec = _fused([mp], [_lat(z, mp)], gpu, 8, False, head)[0].cpu().numpy()
     assert np.mean(dec != z["dec"]) < 1e-3
     _ties_only(dec, z["syn"], _tol(z["syn"]))
-    d420 = F.split_420(_fused([mp], [_lat(z, mp)], gpu, 8, True)[0], mp.H, mp.W)
+    d420 = F.split_420(_fused([mp], [_lat(z, mp)], gpu, 8, True, head)[0], mp.H, mp.W)
     for k in "yuv":
         assert np.mean(d420[k].cpu().numpy() != z[f"dec420_{k}"]) < 1e-3
 
@@ -264,7 +269,8 @@ def test_fused_decode_matches_reference_golden(path, gpu, ccmi_lib):
     (45, 70, 7, "16-1-linear-relu|3-1-linear-none"),
     (64, 96, 8, "16-1-linear-relu|4-1-linear-none|4-3-residual-relu|4-3-residual-none|4-3-linear-none"),
 ])
-def test_fused_decode_matches_oracle_random(H, W, seed, layers, gpu, ccmi_lib):
+@pytest.mark.parametrize("head", HEADS)
+def test_fused_decode_matches_oracle_random(H, W, seed, layers, head, gpu, ccmi_lib):
     """Fused path vs the staged path's reference (oracle), across sizes whose windows clamp
     at every border, and head-only / single-layer-head / 4-channel synthesis stacks."""
     kw = {} if layers is None else {"layers": fo.parse_layers(layers)}
@@ -272,23 +278,24 @@ def test_fused_decode_matches_oracle_random(H, W, seed, layers, gpu, ccmi_lib):
     g = torch.Generator().manual_seed(seed)
     lat = [0.5 * torch.randn(h, w, generator=g) for h, w in mp.sizes]
     ref = fo.forward(mp, lat)
-    raw = _fused([mp], [lat], gpu, 0, False)
+    raw = _fused([mp], [lat], gpu, 0, False, head)
     np.testing.assert_allclose(raw[0].cpu().numpy(), ref["syn"].numpy(), atol=_tol(ref["syn"].numpy()))
     if mp.layers[-1][0] == 3:
         post = fo.post(ref["syn"], 8)
-        dec = _fused([mp], [lat], gpu, 8, False)[0].cpu().numpy()
+        dec = _fused([mp], [lat], gpu, 8, False, head)[0].cpu().numpy()
         assert np.mean(dec != post.numpy()) < 1e-3
         _ties_only(dec, ref["syn"].numpy(), _tol(ref["syn"].numpy()))
 
 
 @pytest.mark.gpu
-def test_fused_decode_batch_own_weights_and_two_grids(gpu, ccmi_lib):
+@pytest.mark.parametrize("head", HEADS)
+def test_fused_decode_batch_own_weights_and_two_grids(head, gpu, ccmi_lib):
     mps = [fo.ModelParams.random(96, 160, seed=20 + i) for i in range(3)]
     lats = []
     for i, mp in enumerate(mps):
         g = torch.Generator().manual_seed(200 + i)
         lats.append([0.5 * torch.randn(h, w, generator=g) for h, w in mp.sizes])
-    raw = _fused(mps, lats, gpu, 0, False)
+    raw = _fused(mps, lats, gpu, 0, False, head)
     for i, (mp, lat) in enumerate(zip(mps, lats)):
         ref = fo.forward(mp, lat)
         np.testing.assert_allclose(raw[i].cpu().numpy(), ref["syn"].numpy(), atol=_tol(ref["syn"].numpy()))

@@ -136,13 +136,16 @@ def encode(x: torch.Tensor, preset_cfg: PresetConfig, lmbda: float, seed: int, a
     cands = [FrameEncoder(coolchic_encoder_param=p, frame_type="I", frame_data_type="rgb", bitdepth=8)
              for _ in range(mgr.preset.warmup.phases[0].candidates)]
     fe = warmup(frame_encoder_manager=mgr, list_candidates=cands, frame=frame, device="cpu")
+    phase_its = [int(mgr.iterations_counter)]  # warm-up (every candidate's iterations)
     for ph in mgr.preset.all_phases:
+        before = int(mgr.iterations_counter)
         fe = train(frame_encoder=fe, frame=frame, frame_encoder_manager=mgr, start_lr=ph.lr,
                    end_lr=ph.end_lr if ph.end_lr is not None else 1e-5, cosine_scheduling_lr=ph.schedule_lr,
                    max_iterations=ph.max_itr, frequency_validation=ph.freq_valid, patience=ph.patience,
                    optimized_module=ph.optimized_module, quantizer_type=ph.quantizer_type,
                    quantizer_noise_type=ph.quantizer_noise_type, softround_temperature=ph.softround_temperature,
                    noise_parameter=ph.noise_parameter)
+        phase_its.append(int(mgr.iterations_counter) - before)
         if ph.quantize_model:
             if keep_before_quant is not None:
                 keep_before_quant["fe"] = copy.deepcopy(fe)
@@ -154,23 +157,29 @@ def encode(x: torch.Tensor, preset_cfg: PresetConfig, lmbda: float, seed: int, a
     dt = time.time() - t0
     return {"psnr_db": float(logs.psnr_db), "rate_bpp": float(logs.total_rate_bpp),
             "rate_latent_bpp": float(logs.rate_latent_bpp), "rate_nn_bpp": float(logs.rate_nn_bpp),
-            "loss": float(logs.loss), "iterations": int(mgr.iterations_counter), "seconds": dt,
+            "loss": float(logs.loss), "iterations": int(mgr.iterations_counter), "phase_iterations": phase_its,
+            "seconds": dt,
             "q_step": {k: {kk: float(vv) for kk, vv in v.items()} for k, v in
                        fe.coolchic_encoder.get_network_quantization_step().items()}}
 
 
-def run_rd(kind: str, out_path: Path):
+def run_rd(kind: str, out_path: Path, images=None, lambdas=None, seeds=None, scale: float = C3X_SCALE):
+    """kind: "debug" (debug preset) or "c3x" (c3x preset, every length x scale).  Runs
+    already in out_path are skipped, so an interrupted run resumes."""
     targets = load_targets()
     res = json.loads(out_path.read_text()) if out_path.exists() else {"runs": []}
     done = {(r["image"], r["preset"], r["lmbda"], r["seed"]) for r in res["runs"]}
-    seeds = SEEDS if kind == "debug" else [0]
-    cfg = preset("debug") if kind == "debug" else preset("c3x", C3X_SCALE)
+    seeds = seeds if seeds is not None else (SEEDS if kind == "debug" else [0])
+    cfg = preset("debug") if kind == "debug" else preset("c3x", scale)
+    tag = "debug" if kind == "debug" else ("c3x" if scale == 1.0 else f"c3x_x{scale}")
     for name, x in targets.items():
-        if kind != "debug" and name != "kodim15_192x128":
+        if images is not None and name not in images:
+            continue
+        if images is None and kind != "debug" and name != "kodim15_192x128":
             continue  # c3x on CPU: the small image only by default (~17 min per point at Kodak size)
-        for lm in LAMBDAS:
+        for lm in (lambdas or LAMBDAS):
             for s in seeds:
-                key = (name, kind if kind == "debug" else f"c3x_x{C3X_SCALE}", lm, s)
+                key = (name, tag, lm, s)
                 if key in done:
                     continue
                 r = encode(x, cfg, lm, s)
@@ -317,6 +326,13 @@ def gen_bd(out_path: Path):
 
 if __name__ == "__main__":
     what = sys.argv[1] if len(sys.argv) > 1 else "all"
+    if what == "one":
+        # one (image, preset scale, lambda, seed) point into its own file, so several can run
+        # side by side: python tools/gen_golden_rd.py one IMAGE SCALE LAMBDA SEED THREADS OUT
+        img, sc, lm, sd, th, out = sys.argv[2:8]
+        torch.set_num_threads(int(th))
+        run_rd("c3x", Path(out), images=[img], lambdas=[float(lm)], seeds=[int(sd)], scale=float(sc))
+        sys.exit(0)
     if what in ("bd", "all"):
         gen_bd(GOLD / "bd_reference.json")
     if what in ("debug", "all"):
