@@ -947,8 +947,13 @@ int launch_dec_arm(const ArmStreamDesc *d_streams, int n_streams, int max_w, int
     // the speculative kernel keeps one ring row fewer (its contexts reach row y-3 only):
     // 5 streams (waves) per CU instead of 4 at 720p
     const size_t lds_spec = sizeof(int32_t) * kRingS * pitch + ((size_t)max_blocks + 16) + sizeof(uint32_t) * 17 * 50 * 2;
-    // CCMI_ARM_NOSPEC=1 selects the one-latent-per-pass kernel (A/B measurements)
-    static const bool spec_off = getenv("CCMI_ARM_NOSPEC") != nullptr;
+    // the one-latent-per-pass kernel below stays for wider ARMs and is what a
+    // -DCCMI_DIAG_NOSPEC build runs for every stream (A/B measurements)
+#if defined(CCMI_DIAG_NOSPEC)
+    constexpr bool spec_off = true;
+#else
+    constexpr bool spec_off = false;
+#endif
     if (!spec_off && d <= 16 && lds_spec <= 160 * 1024) {
 #define CCMI_ARM_SPEC(DD, NN)                                                                                   \
         if (d == DD && nh == NN) {                                                                              \

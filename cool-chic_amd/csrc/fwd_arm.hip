@@ -208,146 +208,6 @@ __global__ __launch_bounds__(kThreads) void arm_fwd_kernel(
     }
 }
 
-// dim_arm = 16 on the matrix cores (the reference presets' ARM): the same math as
-// arm_fwd_kernel<16>, laid out like the training ARM (train.hip t_arm16).  A workgroup of
-// 4 waves is persistent over 4 x 64 tiles (the next tile's latents prefetched into
-// registers); a wave owns one tile row as 4 groups of 16 latents; each 16 x 16 hidden
-// layer is Z^T = W X^T on v_mfma_f32_16x16x4_f32 with the K order permuted so that the
-// accumulators are the next layer's operand, the weights held in 4 VGPRs per layer and
-// lane and loaded once per workgroup (no per-tile scalar weight loads); the output layer
-// is 4 partial products per lane summed over the latent's 4 lanes; the rate runs one
-// latent per lane.  Products are the same fp32 products, summed in another order.
-typedef float v4f __attribute__((ext_vector_type(4)));
-constexpr int kATY = 4, kALH = kATY + kHalo;
-
-template <int NH>
-__global__ __launch_bounds__(kThreads) void arm_fwd16_kernel(
-    const float *__restrict__ lat, int64_t lat_stride, ArmGeom g, float gain, int quantize,
-    const float *__restrict__ params, int64_t pstride, float *__restrict__ o_mu, float *__restrict__ o_scale,
-    float *__restrict__ o_log_scale, float *__restrict__ o_rate, int64_t ostride)
-{
-    constexpr int D = 16, LS = D * D + D, NL = NH > 0 ? NH : 1;
-    __shared__ float tile[kALH][kLW];
-    const int b = blockIdx.y, w = threadIdx.x >> 6, lane = threadIdx.x & 63, ln = lane & 15, lk = lane >> 4;
-    const cfloat_ptr p = (cfloat_ptr)(size_t)(params + (int64_t)b * pstride);
-
-    float WA[NL][4], BI[NL][4];
-#pragma unroll
-    for (int L = 0; L < NH; ++L)
-#pragma unroll
-        for (int s = 0; s < 4; ++s) {
-            WA[L][s] = p[L * LS + ln * D + 4 * lk + s]; // A = W[j = ln][i = 4 lk + s]
-            BI[L][s] = p[L * LS + D * D + 4 * lk + s];
-        }
-    const cfloat_ptr Wo = p + NH * LS;
-    float WO0[4], WO1[4];
-#pragma unroll
-    for (int r = 0; r < 4; ++r) {
-        WO0[r] = Wo[4 * lk + r];
-        WO1[r] = Wo[D + 4 * lk + r];
-    }
-    const float bo0 = Wo[2 * D], bo1 = Wo[2 * D + 1];
-    int coff[4];
-#pragma unroll
-    for (int s = 0; s < 4; ++s) {
-        int o[4];
-#pragma unroll
-        for (int q = 0; q < 4; ++q) {
-            int dy, dx;
-            ctx_offset<D>(4 * q + s, dy, dx);
-            o[q] = dy * kLW + dx;
-        }
-        coff[s] = lk == 0 ? o[0] : lk == 1 ? o[1] : lk == 2 ? o[2] : o[3];
-    }
-
-    auto tile_geo = [&](int t, int &l, int &y0, int &x0) {
-        l = 0;
-#pragma unroll
-        for (int k = 1; k < CCMI_MAX_GRIDS; ++k)
-            if (k < g.n && t >= g.tile_start[k]) l = k;
-        const int lt = t - g.tile_start[l];
-        y0 = (lt / g.tiles_x[l]) * kATY;
-        x0 = (lt % g.tiles_x[l]) * kTX;
-    };
-    constexpr int kSU = (kALH * kLW + kThreads - 1) / kThreads;
-    float pre[kSU];
-    auto load_tile = [&](int t) {
-        int l, y0, x0;
-        tile_geo(t, l, y0, x0);
-        const int H = g.h[l], W = g.w[l];
-        const float *src = lat + (int64_t)b * lat_stride + g.off[l];
-#pragma unroll
-        for (int u = 0; u < kSU; ++u) {
-            const int i = threadIdx.x + u * kThreads;
-            const int r = i / kLW, c = i - r * kLW;
-            const int y = y0 - kHalo + r, x = x0 - kHalo + c;
-            pre[u] = (i < kALH * kLW && y >= 0 && y < H && x >= 0 && x < W) ? src[y * W + x] : 0.f;
-        }
-    };
-    const int n_tiles = g.tile_start[g.n];
-    if ((int)blockIdx.x < n_tiles) load_tile(blockIdx.x);
-    for (int t = blockIdx.x; t < n_tiles; t += gridDim.x) {
-        int l, y0, x0;
-        tile_geo(t, l, y0, x0);
-        const int H = g.h[l], W = g.w[l];
-        __syncthreads(); // the previous tile's readers are done
-#pragma unroll
-        for (int u = 0; u < kSU; ++u) {
-            const int i = threadIdx.x + u * kThreads;
-            if (i < kALH * kLW) (&tile[0][0])[i] = quantize ? rintf(gain * pre[u]) : pre[u];
-        }
-        if (t + (int)gridDim.x < n_tiles) load_tile(t + gridDim.x);
-        __syncthreads();
-
-        const float *yrow = &tile[w + kHalo][kHalo + ln];
-        float mu = 0.f, lsv = 0.f;
-#pragma unroll
-        for (int gg = 0; gg < 4; ++gg) {
-            float X[4];
-#pragma unroll
-            for (int s = 0; s < 4; ++s) X[s] = yrow[16 * gg + coff[s]];
-#pragma unroll
-            for (int L = 0; L < NH; ++L) {
-                v4f acc = {0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-                for (int s = 0; s < 4; ++s) acc = __builtin_amdgcn_mfma_f32_16x16x4f32(WA[L][s], X[s], acc, 0, 0, 0);
-                // F.linear(x) + x, then ReLU (the bias added after the products, as arm_fwd_kernel)
-#pragma unroll
-                for (int r = 0; r < 4; ++r) X[r] = fmaxf((acc[r] + BI[L][r]) + X[r], 0.f);
-            }
-            float pm = 0.f, pl = 0.f;
-#pragma unroll
-            for (int r = 0; r < 4; ++r) {
-                pm = fmaf(WO0[r], X[r], pm);
-                pl = fmaf(WO1[r], X[r], pl);
-            }
-            pm += __shfl_xor(pm, 16);
-            pl += __shfl_xor(pl, 16);
-            pm += __shfl_xor(pm, 32);
-            pl += __shfl_xor(pl, 32);
-            if (gg == lk) {
-                mu = pm + bo0;
-                lsv = pl + bo1;
-            }
-        }
-        // rate etc., one latent per lane (tile column = lane)
-        const int y = y0 + w, x = x0 + lane;
-        if (y < H && x < W) {
-            const float sc = expf(fminf(fmaxf(lsv - 4.f, -4.6f), 5.0f));
-            const float q = tile[w + kHalo][lane + kHalo];
-            const int64_t idx = (int64_t)b * ostride + g.off[l] + y * W + x;
-            if (o_mu) o_mu[idx] = mu;
-            if (o_scale) o_scale[idx] = sc;
-            if (o_log_scale) o_log_scale[idx] = lsv;
-            if (o_rate) {
-                const float is = __builtin_amdgcn_rcpf(sc);
-                const float pr = fmaxf(laplace_cdf(q + 0.5f, mu, is) - laplace_cdf(q - 0.5f, mu, is), 1.52587890625e-05f);
-                o_rate[idx] = -log2f(pr);
-            }
-        }
-    }
-}
-
 template <int D>
 __global__ __launch_bounds__(kThreads) void arm_context_kernel(const float *__restrict__ grid, int H, int W,
                                                                float *__restrict__ out)
@@ -457,53 +317,16 @@ int ccmi_launch_arm_f32(const ccmi_arm_args *a, hipStream_t s)
     g.tile_start[a->n_grids] = tiles;
     if ((a->latent_stride != 0 && a->latent_stride < off) || a->out_stride < off)
         return ccmi_set_error(CCMI_ERR_ARG, "arm: stride smaller than the %d latents of a frame", off);
-    if (a->dim_arm == 16 && a->n_hidden >= 0 && a->n_hidden <= 3) {
-        // opt-in: measured 0.61 vs 0.54 ms per 32-frame 720p step against the VALU kernel
-        // (which already feeds each scalar weight to a packed pair of latents, and has no
-        // backward whose weight loads the MFMA form removes, unlike train.hip's t_arm16)
-        static const bool mfma = getenv("CCMI_ARM_MFMA") != nullptr;
-        if (mfma) {
-            // the MFMA kernel tiles 4 x 64 (persistent grid-stride over all tiles of all grids)
-            ArmGeom g4 = g;
-            int t4 = 0;
-            for (int l = 0; l < a->n_grids; ++l) {
-                g4.tile_start[l] = t4;
-                t4 += g4.tiles_x[l] * ccmi_div_up(a->h[l], kATY);
-            }
-            g4.tile_start[a->n_grids] = t4;
-            static int cus = [] {
-                int dev = 0, n = 0;
-                if (hipGetDevice(&dev) != hipSuccess ||
-                    hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
-                    n = 256;
-                return n > 0 ? n : 256;
-            }();
-            const int per_frame = std::max(1, std::min(t4, 8 * cus / std::max(1, a->batch)));
-            dim3 grid4((unsigned)per_frame, a->batch);
-#define CCMI_ARM16_LAUNCH(NN)                                                                                        \
-    hipLaunchKernelGGL(arm_fwd16_kernel<NN>, grid4, dim3(kThreads), 0, s, a->latent, a->latent_stride, g4, a->gain, \
-                       a->quantize, a->params, a->param_stride, a->mu, a->scale, a->log_scale, a->rate, a->out_stride)
-            switch (a->n_hidden) {
-            case 0: CCMI_ARM16_LAUNCH(0); break;
-            case 1: CCMI_ARM16_LAUNCH(1); break;
-            case 2: CCMI_ARM16_LAUNCH(2); break;
-            default: CCMI_ARM16_LAUNCH(3); break;
-            }
-#undef CCMI_ARM16_LAUNCH
-            CCMI_HIP_CHECK(hipGetLastError());
-            return CCMI_OK;
-        }
-    }
     dim3 grid(tiles, a->batch);
 #define CCMI_ARM_LAUNCH(DD)                                                                                     \
     hipLaunchKernelGGL(arm_fwd_kernel<DD>, grid, dim3(kThreads), 0, s, a->latent, a->latent_stride, g, a->gain, \
                        a->quantize, a->n_hidden, a->params, a->param_stride, a->mu, a->scale, a->log_scale,     \
                        a->rate, a->out_stride)
-    static const bool nh_rt = getenv("CCMI_ARM_NH_RUNTIME") != nullptr; // A/B switch
     switch (a->dim_arm) {
     case 8: CCMI_ARM_LAUNCH(8); break;
     case 16:
-        if (a->n_hidden == 2 && !nh_rt) {
+        // the presets' ARM (2 hidden layers): layer loop unrolled
+        if (a->n_hidden == 2) {
             hipLaunchKernelGGL((arm_fwd_kernel<16, 2>), grid, dim3(kThreads), 0, s, a->latent, a->latent_stride, g, a->gain,
                                a->quantize, a->n_hidden, a->params, a->param_stride, a->mu, a->scale, a->log_scale,
                                a->rate, a->out_stride);

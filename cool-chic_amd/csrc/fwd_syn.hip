@@ -855,12 +855,8 @@ template <int CMID, bool UPS>
 void launch_fused(dim3 grid, hipStream_t s, const FusedArgs &fa, const LevelArgs &u)
 {
     // the presets' 7-grid decoders with a 48-wide head (hop and its relatives): unrolled head
-    static const bool generic_head = getenv("CCMI_SYN_HEAD_LOOP") != nullptr; // A/B switch
-    if (fa.cin == 7 && fa.n_head == 2 && fa.hid == 48 && !generic_head) {
-        // CCMI_SYN_LDS_PAD (experiments only): extra dynamic LDS per workgroup, to measure how
-        // the kernel responds to fewer resident workgroups per CU
-        static const int pad = getenv("CCMI_SYN_LDS_PAD") ? atoi(getenv("CCMI_SYN_LDS_PAD")) : 0;
-        hipLaunchKernelGGL((syn_fused_kernel<7, CMID, UPS, false, 48>), grid, dim3(kFThreads), pad, s, fa, u);
+    if (fa.cin == 7 && fa.n_head == 2 && fa.hid == 48) {
+        hipLaunchKernelGGL((syn_fused_kernel<7, CMID, UPS, false, 48>), grid, dim3(kFThreads), 0, s, fa, u);
         return;
     }
     switch (fa.cin) {

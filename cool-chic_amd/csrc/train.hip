@@ -1111,7 +1111,8 @@ __global__ __launch_bounds__(kT) __attribute__((amdgpu_waves_per_eu(MODE == 2 ? 
 #else
 #define HEAD_MFMA(a, b, c) mfma4(a, b, c)
 #endif
-// PAIR (default; CCMI_HEAD_BWD_OLD=1 keeps the unit-at-a-time form for A/B): the per-pixel
+// PAIR (the instantiated form; PAIR = false is the round-1 unit-at-a-time form, measured
+// 397 vs 350-383 us per 8-frame iteration): the per-pixel
 // work runs over PAIRS of hidden units with packed FMAs -- records interleave the two units'
 // weights ({w0[j][i], w0[j+1][i]}, {b0[j], b0[j+1]}, {w1[k][j], w1[k][j+1]}), so every
 // packed operand is an aligned register pair -- and the output / g_x sums keep one partial
@@ -1898,9 +1899,9 @@ int launch_arm_d(int nh, dim3 grid, hipStream_t s, const float *yq, const Geo &g
                  float *rate_out)
 {
     if constexpr (D == 16) {
-        // the matrix-core ARM (t_arm16); CCMI_ARM_VALU=1 keeps the VALU kernel (A/B runs)
-        static const bool valu = getenv("CCMI_ARM_VALU") != nullptr;
-        if (!valu) {
+        // the matrix-core ARM (t_arm16): its MFMA chains replace the scalar weight loads of
+        // the VALU kernel's tile loop (606 -> 499 us per 8-frame iteration)
+        {
             switch (nh) {
             case 0: hipLaunchKernelGGL((t_arm16<0>), grid, dim3(kT), 0, s, yq, g, at, th, ps, lam_px, gq, gth, gstride, acc4, grate, rate_out); break;
             case 1: hipLaunchKernelGGL((t_arm16<1>), grid, dim3(kT), 0, s, yq, g, at, th, ps, lam_px, gq, gth, gstride, acc4, grate, rate_out); break;
@@ -1927,12 +1928,8 @@ void launch_head(bool bwd, dim3 grid, hipStream_t s, const float *dense, const f
     else {
         constexpr int kXP = CIN + 2 > 4 ? CIN + 2 : 4; // t_head_bwd's per-wave LDS rows
         const size_t lds = sizeof(float) * (kHeadT / 64) * 64 * (16 * ((g.hid + 15) / 16) + 1 + kXP);
-        static const bool old = getenv("CCMI_HEAD_BWD_OLD") != nullptr; // A/B switch
 #define CCMI_HB(N)                                                                                                     \
-    do {                                                                                                               \
-        auto *kfn = old ? t_head_bwd<CIN, N, false> : t_head_bwd<CIN, N, true>;                                        \
-        hipLaunchKernelGGL(kfn, grid, dim3(kHeadT), lds, s, dense, gz0, g, th, ps, z0_or_gdense, gth, gstride);         \
-    } while (0)
+    hipLaunchKernelGGL((t_head_bwd<CIN, N, true>), grid, dim3(kHeadT), lds, s, dense, gz0, g, th, ps, z0_or_gdense, gth, gstride)
         switch ((g.hid + 15) / 16) {
         case 1: CCMI_HB(1); break;
         case 2: CCMI_HB(2); break;
@@ -2106,16 +2103,15 @@ extern "C" int ccmi_train_step(const ccmi_train_args *a, void *stream)
     for (int i = g.n_sp - 1; i >= 0; --i) {
         float *gin = F(pl.gbuf[i & 1]);
         const int ntile = ccmi_div_up(g.W, kSX) * ccmi_div_up(g.H, kSY);
-        static const int sp_nb = getenv("CCMI_SP_NB") ? atoi(getenv("CCMI_SP_NB")) : 0; // experiments: WGs per frame
-        const unsigned nb = (unsigned)std::max(1, std::min(ntile, sp_nb > 0 ? sp_nb : 1024 / B));
+        // weight gradients: grid-stride over <= 1024 / B workgroups per frame (measured fastest
+        // against 32 .. 512 per frame)
+        const unsigned nb = (unsigned)std::max(1, std::min(ntile, 1024 / B));
         const float *outp = g.sp_relu[i] ? F(pl.z[i + 1]) : nullptr;
         {
             // input gradient: one tile per workgroup; weight gradients: grid-stride as before
             hipLaunchKernelGGL(t_sp_bwd<1>, dim3((unsigned)ntile, B), dim3(kT), 0, s, gcur, outp, F(pl.z[i]), g, a->params,
                                a->param_stride, g.sp_w[i], g.sp_b[i], g.sp_res[i], gin, Gth, GS);
-            static const int spw_nb = getenv("CCMI_SPW_NB") ? atoi(getenv("CCMI_SPW_NB")) : 0; // experiments
-            const unsigned nbw = spw_nb > 0 ? (unsigned)std::max(1, std::min(ntile, spw_nb)) : nb;
-            hipLaunchKernelGGL(t_sp_bwd<2>, dim3(nbw, B), dim3(kT), 0, s, gcur, outp, F(pl.z[i]), g, a->params,
+            hipLaunchKernelGGL(t_sp_bwd<2>, dim3(nb, B), dim3(kT), 0, s, gcur, outp, F(pl.z[i]), g, a->params,
                                a->param_stride, g.sp_w[i], g.sp_b[i], g.sp_res[i], gin, Gth, GS);
         }
         gcur = gin;
@@ -2123,8 +2119,7 @@ extern "C" int ccmi_train_step(const ccmi_train_args *a, void *stream)
     {
         // grid-stride over pixel chunks: about one resident wave of workgroups for the batch
         const int64_t nchunk = (npx + kHeadT - 1) / kHeadT;
-        static const int hb_nb = getenv("CCMI_HB_NB") ? atoi(getenv("CCMI_HB_NB")) : 0; // experiments: WGs per frame
-        const unsigned nb = (unsigned)std::max<int64_t>(1, std::min<int64_t>(nchunk, hb_nb > 0 ? hb_nb : 1024 / B));
+        const unsigned nb = (unsigned)std::max<int64_t>(1, std::min<int64_t>(nchunk, 1024 / B));
         head_dispatch(g.L, true, dim3(nb, B), s, dense, gcur, g, a->params, a->param_stride, gd, Gth, GS);
     }
 

@@ -1,5 +1,5 @@
 """Bit-exact decode leg of bench.py on its own: python tools/ab_decode.py [reps ...]
-(set CCMI_ARM_NOSPEC=1 to time the one-latent-per-pass ARM kernel)."""
+(a -DCCMI_DIAG_NOSPEC build times the one-latent-per-pass ARM kernel)."""
 import json
 import sys
 from pathlib import Path
