@@ -119,10 +119,13 @@ def ups_forward_i32(latent, sizes, kernels, ups_k: int, n_ups: int, pre_k: int, 
     w = (C.c_int * MAX_GRIDS)(*[s[1] for s in sizes])
     if latent.dtype != torch.int32 or latent.numel() < sum(a * b for a, b in sizes):
         raise ValueError("latent: int32 with sum(h * w) elements expected")
+    if kernels.dtype != torch.int32:
+        raise ValueError("kernels: int32 expected (weights_i32()[1])")
+    latent, kernels = latent.contiguous(), kernels.contiguous()  # held until after the launch
     out = torch.empty(n, sizes[0][0], sizes[0][1], dtype=torch.int32, device=latent.device)
     nws = L.ccmi_ups_workspace_bytes_i32(n, h, w)
     ws = torch.empty(max(nws, 4), dtype=torch.uint8, device=latent.device)
-    a = UpsI32Args(latent=latent.data_ptr(), n_grids=n, h=h, w=w, kernels=kernels.contiguous().data_ptr(), ups_k=ups_k,
+    a = UpsI32Args(latent=latent.data_ptr(), n_grids=n, h=h, w=w, kernels=kernels.data_ptr(), ups_k=ups_k,
                    n_ups=n_ups, pre_k=pre_k, n_pre=n_pre, out=out.data_ptr(), workspace=ws.data_ptr(), workspace_bytes=nws)
     check(L.ccmi_ups_forward_i32(C.byref(a), torch.cuda.current_stream(latent.device).cuda_stream))
     return out
@@ -139,9 +142,12 @@ def syn_forward_i32(x, layers, params):
     arr = (SynLayer * MAX_SYN_LAYERS)()
     for i, (n_out, ks, res, relu) in enumerate(layers):
         arr[i] = SynLayer(int(n_out), int(ks), int(res), int(relu))
+    if x.dtype != torch.int32 or params.dtype != torch.int32:
+        raise ValueError("syn_forward_i32: int32 input and params expected")
+    x, params = x.contiguous(), params.contiguous()  # held until after the launch
     out = torch.empty(layers[-1][0], hh, ww, dtype=torch.int32, device=x.device)
-    a = SynI32Args(in_=x.contiguous().data_ptr(), c_in=c, h=hh, w=ww, n_layers=len(layers), layers=arr,
-                   params=params.contiguous().data_ptr(), out=out.data_ptr(), workspace=None, workspace_bytes=0)
+    a = SynI32Args(in_=x.data_ptr(), c_in=c, h=hh, w=ww, n_layers=len(layers), layers=arr,
+                   params=params.data_ptr(), out=out.data_ptr(), workspace=None, workspace_bytes=0)
     nws = L.ccmi_syn_workspace_bytes_i32(C.byref(a))
     ws = None
     if nws:

@@ -6,7 +6,8 @@ Same constructor parameters, sub-modules and state_dict layout as the reference.
   upsampling pyramid                           -> ccmi_ups_forward_f32 (one launch / level),
   synthesis                                    -> ccmi_syn_forward_f32 (one fused launch).
 ``forward_batch`` decodes many independent encoders (each with its own weights) of the
-same size and architecture in one launch sequence.
+same size and architecture in one launch sequence; ``decoded_batch`` is the eval
+FrameEncoder.forward through the fused decode kernel (no dense stack, no raw output).
 """
 
 import math
@@ -170,16 +171,14 @@ def _check_same_arch(encs: Sequence[CoolChicEncoder]) -> None:
             raise ValueError("forward_batch: all encoders must share image size and architecture")
 
 
-@torch.no_grad()
-def forward_batch(encs: Sequence[CoolChicEncoder], AC_MAX_VAL: int = -1, flag_additional_outputs: bool = False):
-    """Eval forward of several independent CoolChicEncoders (own weights each) in one HIP launch
-    sequence.  Returns (raw_out [B, C, H, W], rate [B, N], additional_data)."""
+def _batch_inputs(encs: Sequence[CoolChicEncoder], AC_MAX_VAL: int):
+    """Flat latents [B, N] (AC_MAX_VAL-clamped integers when given), the per-frame packed
+    parameter blocks, and the ARM's outputs: the common front of both eval paths."""
     _check_same_arch(encs)
     e0 = encs[0]
     dev = e0.latent_grids[0].data.device
     if dev.type != "cuda":
         raise ValueError("CoolChicEncoder.forward runs on the GPU: move the module with .to('cuda')")
-    sizes = e0.grid_sizes
     gain = float(e0.encoder_gains)
     flat = torch.cat([e.flat_latent() for e in encs], dim=0).float().contiguous()
     quantize = True
@@ -189,10 +188,50 @@ def forward_batch(encs: Sequence[CoolChicEncoder], AC_MAX_VAL: int = -1, flag_ad
     arm_p = torch.stack([e.arm.packed_params() for e in encs]).to(dev)
     ups_p = torch.stack([e.upsampling.packed_params() for e in encs]).to(dev)
     syn_p = torch.stack([e.synthesis.packed_params() for e in encs]).to(dev)
+    return flat, quantize, gain, arm_p, ups_p, syn_p
+
+
+@torch.no_grad()
+def forward_batch(encs: Sequence[CoolChicEncoder], AC_MAX_VAL: int = -1, flag_additional_outputs: bool = False):
+    """Eval forward of several independent CoolChicEncoders (own weights each) in one HIP launch
+    sequence.  Returns (raw_out [B, C, H, W], rate [B, N], additional_data)."""
+    flat, quantize, gain, arm_p, ups_p, syn_p = _batch_inputs(encs, AC_MAX_VAL)
+    e0 = encs[0]
+    sizes = e0.grid_sizes
     want = ("mu", "scale", "log_scale", "rate") if flag_additional_outputs else ("rate",)
     a = _F.arm_forward(flat, sizes, arm_p, e0.param.dim_arm, e0.param.n_hidden_layers_arm, gain, quantize, want)
     dense = e0.upsampling.forward_flat(flat, sizes, gain, quantize, params=ups_p)
     raw = e0.synthesis.forward(dense, params=syn_p)
+    return raw, a["rate"], _additional(encs, flat, quantize, gain, a, flag_additional_outputs)
+
+
+@torch.no_grad()
+def decoded_batch(encs: Sequence[CoolChicEncoder], bitdepth: int, yuv420: bool, AC_MAX_VAL: int = -1,
+                  flag_additional_outputs: bool = False, head: int = 0):
+    """FrameEncoder.forward in eval mode (frame.py:153-183) for encoders whose architecture has
+    a fused decode kernel: the ARM + rate (ccmi_arm_forward_f32), then ccmi_decode_forward_f32
+    -- upsampling pyramid down to level 1, then ONE kernel for the last upsampling step,
+    the synthesis and the post-processing (round to the bitdepth grid, 420, clamp), so the
+    dense [L, H, W] stack and the raw synthesis output never reach HBM.  Returns (decoded
+    [B, 3, H, W] or the flat 420 planes [B, H W + 2 (H/2)(W/2)], rate [B, N], additional
+    data).  Raises CcmiError(ERR_UNSUPPORTED) for other architectures (forward_batch +
+    post-processing then)."""
+    flat, quantize, gain, arm_p, ups_p, syn_p = _batch_inputs(encs, AC_MAX_VAL)
+    e0 = encs[0]
+    p = e0.param
+    sizes = e0.grid_sizes
+    want = ("mu", "scale", "log_scale", "rate") if flag_additional_outputs else ("rate",)
+    a = _F.arm_forward(flat, sizes, arm_p, p.dim_arm, p.n_hidden_layers_arm, gain, quantize, want)
+    ups = e0.upsampling
+    out = _F.decode_forward(flat, sizes, ups_p, ups.ups_k_size, ups.n_ups_kernel, ups.ups_preconcat_k_size,
+                            ups.n_ups_preconcat_kernel, e0.synthesis.layer_desc, syn_p, gain, quantize, bitdepth,
+                            yuv420, head)
+    return out, a["rate"], _additional(encs, flat, quantize, gain, a, flag_additional_outputs)
+
+
+def _additional(encs, flat, quantize, gain, a, flag_additional_outputs) -> Dict[str, Any]:
+    """The per-grid detail dictionary of coolchic.py:426-479."""
+    sizes = encs[0].grid_sizes
     add: Dict[str, Any] = {}
     if flag_additional_outputs:
         if len(encs) > 1:
@@ -214,4 +253,4 @@ def forward_batch(encs: Sequence[CoolChicEncoder], AC_MAX_VAL: int = -1, flag_ad
             add["detailed_rate_bit"].append(a["rate"][:, sl].view(1, 1, h, w))
             add["detailed_centered_latent"].append(lat - mu)
             cnt += h * w
-    return raw, a["rate"], add
+    return add

@@ -1,8 +1,11 @@
 """FrameEncoder (reference: coolchic/enc/component/frame.py), intra frames.
 
 forward() = CoolChicEncoder.forward + the eval post-processing of frame.py:175-183
-(rounding to the output bitdepth, optional 444 -> 420 nearest, clamp), the latter in
-ccmi_post_f32.  Inter coding (warping, frame.py:165-170) is disabled in the reference
+(rounding to the output bitdepth, optional 444 -> 420 nearest, clamp).  In eval mode the
+whole decode tail is ccmi_decode_forward_f32 (coolchic.decoded_batch: one fused kernel
+for the last upsampling step, the synthesis and the post-processing); the staged
+ccmi_ups / ccmi_syn / ccmi_post path remains for architectures without a fused kernel
+and for train mode.  Inter coding (warping, frame.py:165-170) is disabled in the reference
 and not part of this hot path.
 """
 
@@ -12,8 +15,9 @@ from typing import Any, Dict, List, Optional, Union
 import torch
 from torch import Tensor, nn
 
+from ccmi import ERR_UNSUPPORTED, CcmiError
 from ccmi import forward as _F
-from coolchic.enc.component.coolchic import CoolChicEncoder, CoolChicEncoderParameter
+from coolchic.enc.component.coolchic import CoolChicEncoder, CoolChicEncoderParameter, decoded_batch
 
 
 @dataclass
@@ -39,6 +43,22 @@ class FrameEncoder(nn.Module):
                 quantizer_type: str = "softround", soft_round_temperature: Optional[float] = 0.3,
                 noise_parameter: Optional[float] = 1.0, AC_MAX_VAL: int = -1,
                 flag_additional_outputs: bool = False) -> FrameEncoderOutput:
+        if not self.training:
+            # eval: the raw synthesis output is not part of FrameEncoderOutput, so the decode
+            # tail runs as one fused kernel (pyramid, last upsampling step, synthesis and this
+            # post-processing); architectures without a fused kernel take the staged path
+            yuv420 = self.frame_data_type == "yuv420"
+            try:
+                out, rate, add = decoded_batch([self.coolchic_encoder], self.bitdepth, yuv420, AC_MAX_VAL,
+                                               flag_additional_outputs)
+            except CcmiError as e:
+                if e.code != ERR_UNSUPPORTED:
+                    raise
+            else:
+                if yuv420:
+                    H, W = self.coolchic_encoder.grid_sizes[0]
+                    out = {k: v.unsqueeze(1) for k, v in _F.split_420(out, H, W).items()}
+                return FrameEncoderOutput(out, rate, add if flag_additional_outputs else {})
         raw, rate, add = self.coolchic_encoder.forward(quantizer_noise_type, quantizer_type, soft_round_temperature,
                                                        noise_parameter, AC_MAX_VAL, flag_additional_outputs)
         return FrameEncoderOutput(self.post_process(raw), rate, add if flag_additional_outputs else {})

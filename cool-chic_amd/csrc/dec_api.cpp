@@ -110,6 +110,7 @@ extern "C" int ccmi_ups_forward_i32(const ccmi_ups_i32_args *a, void *stream)
 
 extern "C" size_t ccmi_syn_workspace_bytes_i32(const ccmi_syn_i32_args *a)
 {
+    if (!a) return 0;
     DecSynArgs y;
     ccmi_syn_i32_args t = *a;
     static int32_t dummy;

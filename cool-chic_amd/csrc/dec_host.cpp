@@ -360,7 +360,7 @@ int decode_many(const uint8_t *const *streams, const size_t *lens, int n, uint8_
     tot += align_up(tail_cap, 256);
 #if defined(CCMI_ARM_STAMPS)
     const size_t dbg_off = tot;
-    tot += align_up(8 * 8 * (size_t)n * CCMI_MAX_GRIDS, 256);
+    tot += align_up(16 * 8 * (size_t)n * CCMI_MAX_GRIDS, 256);
     size_t all_count = 0;
 #endif
 
@@ -423,7 +423,7 @@ int decode_many(const uint8_t *const *streams, const size_t *lens, int n, uint8_
             a.flags = 1;
             a.dbg = nullptr;
 #if defined(CCMI_ARM_STAMPS)
-            a.dbg = reinterpret_cast<uint64_t *>(dev + dbg_off) + 8 * (desc.size() + all_count++);
+            a.dbg = reinterpret_cast<uint64_t *>(dev + dbg_off) + 16 * (desc.size() + all_count++);
 #endif
             for (size_t k = 0; k < f.arm.size(); ++k) {
                 // biases sit between weight blocks; checking them too is conservative
@@ -575,15 +575,13 @@ int decode_many(const uint8_t *const *streams, const size_t *lens, int n, uint8_
         for (size_t k = 0; k < pl[i].lat_elems; ++k) lat_out[i][k] >>= kArmPrec;
 #if defined(CCMI_ARM_STAMPS)
     {
-        std::vector<uint64_t> dbg(8 * all.size());
+        std::vector<uint64_t> dbg(16 * all.size());
         CCMI_HIP_CHECK(hipMemcpy(dbg.data(), dev + dbg_off, dbg.size() * 8, hipMemcpyDeviceToHost));
         for (size_t j = 0; j < all.size(); ++j) {
-            const size_t k = (size_t)(reinterpret_cast<uint8_t *>(all[j].dbg) - (dev + dbg_off)) / 64;
-            fprintf(stderr, "STAMPS stream %zu (%dx%d): ctx %llu mlp %llu idx %llu cabac %llu coded %llu setup %llu loop %llu\n", k,
-                    all[j].h, all[j].w, (unsigned long long)dbg[8 * k], (unsigned long long)dbg[8 * k + 1],
-                    (unsigned long long)dbg[8 * k + 2], (unsigned long long)dbg[8 * k + 3],
-                    (unsigned long long)dbg[8 * k + 4], (unsigned long long)dbg[8 * k + 5],
-                    (unsigned long long)dbg[8 * k + 6]);
+            const size_t k = (size_t)(reinterpret_cast<uint8_t *>(all[j].dbg) - (dev + dbg_off)) / 128;
+            fprintf(stderr, "STAMPS stream %zu (%dx%d):", k, all[j].h, all[j].w);
+            for (int c = 0; c < 16; ++c) fprintf(stderr, " %llu", (unsigned long long)dbg[16 * k + c]);
+            fprintf(stderr, "\n");
         }
     }
 #endif

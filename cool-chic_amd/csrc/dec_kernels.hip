@@ -19,6 +19,7 @@
 //  dec_output       444 -> 420/444 8/10-bit or PPM payload (ccdecapi.cpp:59-240).
 #include <stdlib.h>
 
+#include <type_traits>
 #include <utility>
 
 #include "ccmi_cabac.h"
@@ -597,6 +598,434 @@ __global__ __launch_bounds__(64) void dec_arm_spec_kernel(const ArmStreamDesc *_
 #endif
 }
 
+// ------------------------------------------------------------------ latency-optimised ARM decode (d <= 16, >= 1 hidden layer)
+// dec_arm_spec_kernel's speculation (DPP row g = latent x + g, undecoded same-row latents
+// guessed 0), with the serial chain of a pass shortened:
+//  * the first hidden layer's above-row part (every context but the D_S = 3 same-row ones,
+//    plus the bias and the residual of the above-row neurons) is computed off the chain,
+//    64 latents at a time with lane = latent once the rows above are decoded, into an LDS
+//    ring of two 64-latent chunks; a pass adds the three same-row products to it.  Exact:
+//    the reference accumulates every product in int32 before its single rounding
+//    (arm_cpu.cpp:65-80), and int32 addition wraps identically in any order (-fwrapv);
+//  * the next pass's above-row sums are read for all four outcomes (x + 1 .. x + 4) before
+//    the CABAC of the current pass, so the chain never waits on LDS for them;
+//  * the CABAC bin uses a count-leading-zeros renormalisation and selects instead of
+//    the branchy lps_renorm ladder (same state transitions as TDecBinCABAC::decodeBin).
+constexpr int kDS = 3; // same-row contexts (0, -3), (0, -2), (0, -1): the last three context indices
+
+// Byte source of the latency kernel: the stream's words come through wave-uniform VECTOR
+// loads issued one word ahead (the scalar-load reader's fetch is counted in lgkmcnt with
+// the LDS reads, so every LDS wait of a pass also waited for it).  Word indices clamp to the
+// zero padding after the stream (>= 64 bytes, dec_host.cpp), which reads as zeros.
+struct DevBytesV {
+    typedef const __attribute__((address_space(1))) uint32_t *gptr; // global, not flat: vmcnt only
+    gptr p;
+    uint32_t lim, pos, wi, cur;
+    int32_t vnext; // word wi + 1, in a VGPR (possibly still in flight)
+    __device__ __forceinline__ int32_t fetch(uint32_t i) const
+    {
+        int vi = (int)(i < lim ? i : lim);
+        asm volatile("" : "+v"(vi)); // a vector load
+        return (int32_t)p[vi];
+    }
+    __device__ __forceinline__ void init(const uint32_t *base, uint32_t nbytes)
+    {
+        p = (gptr)(size_t)base;
+        lim = ((nbytes + 3u) >> 2) + 8u;
+        pos = 0;
+        wi = 0;
+        cur = (uint32_t)__builtin_amdgcn_readfirstlane(fetch(0));
+        vnext = fetch(1);
+    }
+    __device__ __forceinline__ uint32_t next()
+    {
+        const uint32_t b = (cur >> ((pos & 3u) * 8u)) & 0xFFu;
+        ++pos;
+        if ((pos & 3u) == 0) {
+            cur = (uint32_t)__builtin_amdgcn_readfirstlane(vnext);
+            ++wi;
+            vnext = fetch(wi + 1);
+        }
+        return b;
+    }
+};
+constexpr int kChunk = 64;
+
+// A static context's model state st (0..255) as the bin decode uses it: the MPS in bit 7,
+// the LPS-side state's top bits (st ^ 0xFF when the MPS is 1, then >> 2) in bits 0..4.
+__host__ __device__ constexpr uint32_t bin_code(uint32_t st)
+{
+    return (st & 0x80u) | ((((st >> 7) ? st ^ 0xFFu : st) & 0xFFu) >> 2);
+}
+
+// one bin of a static context given as bin_code(state) (TDecBinCABAC::decodeBin)
+__device__ __forceinline__ uint32_t bin_fast(Cabac<DevBytesV> &c, uint32_t code)
+{
+    const uint32_t mps = code >> 7;
+    const uint32_t lps = (((code & 0x1Fu) * (c.range >> 5)) >> 1) + 4;
+    const uint32_t rmps = c.range - lps;
+    const uint32_t scaled = rmps << 7;
+    // is_lps = value >= scaled, as an all-ones mask from the sign of scaled - 1 - value (both
+    // < 2^31): plain scalar arithmetic, where a bool select went through the VALU and back
+    const uint32_t m = (uint32_t)((int32_t)(scaled - 1u - c.value) >> 31);
+    // renormalisation: an LPS shifts its range lps in [4, 236] back to >= 256 (clz(lps) - 23 =
+    // Contexts.cpp's table); an MPS shifts once when the remaining range fell below 256
+    const uint32_t nb = ((uint32_t)(__builtin_clz(lps) - 23) & m) | (((rmps >> 8) ^ 1u) & ~m); // rmps < 512
+    c.value = (c.value - (scaled & m)) << nb;
+    c.range = ((lps & m) | (rmps & ~m)) << nb;
+    c.bits_needed += (int32_t)nb;
+    if (c.bits_needed >= 0) {
+        c.value += c.src.next() << c.bits_needed;
+        c.bits_needed -= 8;
+    }
+    return mps ^ (m & 1u);
+}
+
+template <int D, int NH>
+__global__ __launch_bounds__(64) void dec_arm_lat_kernel(const ArmStreamDesc *__restrict__ streams, int pitch)
+{
+    static_assert(D <= 16 && D > kDS && NH >= 1, "one neuron per lane of a DPP row, >= 1 hidden layer");
+    constexpr int DA = D - kDS; // above-row contexts
+#if defined(CCMI_ARM_STAMPS)
+    // [0] ARM pass (same-row products + MLP + output sums)  [1] index + table  [2] CABAC
+    // [3] ARM passes  [4] coded latents  [5] setup  [6] latent loop  [7] chunk precompute
+    // [8] block fills  [9] row copy-out  [10] blocks visited
+    uint64_t st_acc[16] = {};
+    const uint64_t t_begin = __builtin_amdgcn_s_memtime();
+#endif
+    extern __shared__ int32_t smem[];
+    uint32_t *ctab = reinterpret_cast<uint32_t *>(smem);               // 17 x 50 x 2
+    int32_t *w0s = smem + 17 * 50 * 2;                                  // [16][16] layer-0 weights, [16] biases
+    int32_t *pre = w0s + 16 * 16 + 16;                                  // [2][kChunk][16] above-row sums
+    int32_t *ring = pre + 2 * kChunk * 16;                              // kRingS x pitch
+    uint8_t *bmap = reinterpret_cast<uint8_t *>(ring + kRingS * pitch); // block sig/flat map
+
+    const ArmStreamDesc S = streams[blockIdx.x];
+    const int lane = threadIdx.x;
+    const int grp = lane >> 4, o = lane & 15;
+    const bool live = o < D;
+    const int h = S.h, w = S.w;
+    const bool w24 = (S.flags & 1) != 0;
+
+    // context table with every static-context index turned into its bin code (model state:
+    // Model::init + state(), then bin_code) once here instead of per bin
+    for (int i = lane; i < 17 * 50 * 2; i += 64) {
+        const uint32_t v = c_ctx.v[i];
+        uint32_t st = 0;
+        for (int k = 0; k < 4; ++k) {
+            Model m;
+            m.init((int)((v >> (8 * k)) & 0xFF));
+            st |= bin_code(m.state()) << (8 * k);
+        }
+        ctab[i] = (i & 1) ? (st & 0xFF) : st;
+    }
+    for (int i = lane; i < kRingS * pitch; i += 64) ring[i] = 0;
+    // layer 0 in LDS for the chunk precompute (broadcast reads: as scalar operands its 16 x 13
+    // above-row weights pushed the kernel's other wave-uniform state out to VGPR lanes)
+    for (int i = lane; i < 16 * 16 + 16; i += 64) {
+        const int r = i >> 4, cc = i & 15;
+        w0s[i] = i < 256 ? (r < D && cc < D ? S.weights[r * D + cc] : 0) : (cc < D ? S.weights[D * D + cc] : 0);
+    }
+
+    // layer 0: same-row weights of neuron o (its own residual folded into the matching one)
+    int32_t Ws[kDS];
+#pragma unroll
+    for (int j = 0; j < kDS; ++j) Ws[j] = live ? S.weights[o * D + DA + j] + (o == DA + j ? 256 : 0) : 0;
+    int32_t Wh[NH][16], Bh[NH];
+#pragma unroll
+    for (int l = 1; l < NH; ++l) {
+        const int32_t *base = S.weights + l * (D * D + D);
+#pragma unroll
+        for (int i = 0; i < 16; ++i) Wh[l][i] = (live && i < D) ? base[o * D + i] : 0;
+        Bh[l] = live ? base[D * D + o] : 0;
+    }
+    const int32_t *ob = S.weights + NH * (D * D + D);
+    const int32_t Wo0 = live ? ob[o] : 0, Wo1 = live ? ob[D + o] : 0;
+    const int32_t bo0 = __builtin_amdgcn_readfirstlane(ob[2 * D]);
+    const int32_t bo1 = __builtin_amdgcn_readfirstlane(ob[2 * D + 1]);
+
+    // ---- CABAC start + block significance / flat maps (BACContext::set_layer, cc-bac.h:24-130)
+    Cabac<DevBytesV> cab;
+    cab.src.init(S.bytes, S.nbytes);
+    cab.start();
+    const int updated = S.sig_blk < 0;
+    const int blk = S.sig_blk < 0 ? -S.sig_blk : S.sig_blk;
+    int shift = 0;
+    while ((1 << shift) < blk) ++shift;
+    const int mask = (1 << shift) - 1;
+    int nby = 1, nbx = 1;
+    if (blk > 0) {
+        nby = (h + blk - 1) >> shift;
+        nbx = (w + blk - 1) >> shift;
+    }
+    const int nblk = nby * nbx;
+    for (int i = lane; i < nblk; i += 64) bmap[i] = 1; // bit0 sig, bit1 flat
+    __syncthreads();
+    if (nblk > 1) {
+        if (cab.ep()) {
+            Model m;
+            m.init(65);
+            for (int i = 0; i < nblk; ++i) {
+                const uint32_t b = updated ? cab.bin_adaptive(m) : cab.ep();
+                if (lane == 0) bmap[i] = (uint8_t)b;
+            }
+        }
+        __syncthreads();
+        if (cab.ep()) {
+            Model m;
+            m.init(65);
+            for (int i = 0; i < nblk; ++i) {
+                const int sig = __builtin_amdgcn_readfirstlane((int)bmap[i]);
+                if (sig) {
+                    const uint32_t f = updated ? cab.bin_adaptive(m) : cab.ep();
+                    if (lane == 0) bmap[i] = (uint8_t)(sig | (f << 1));
+                }
+            }
+        }
+    }
+    __syncthreads();
+
+    // context offsets of the above-row contexts (rows y-3 .. y-1), for the chunk precompute
+    int big = 0;
+#if defined(CCMI_ARM_STAMPS)
+    st_acc[5] = __builtin_amdgcn_s_memtime() - t_begin;
+    const uint64_t t_loop = __builtin_amdgcn_s_memtime();
+#endif
+
+    for (int y = 0; y < h; ++y) {
+        int32_t *row = ring + (y % kRingS) * pitch + kPad;
+        const int32_t *up = ring + ((y + kRingS - 1) % kRingS) * pitch + kPad;
+        int32_t r1 = 0, r2 = 0, r3 = 0, r4 = 0; // decoded values at x-1 .. x-4 (this row)
+        const int brow = blk > 0 ? (y >> shift) * nbx : 0;
+        int have0 = -1, have1 = -1; // chunk held by pre slot 0 / 1
+        // above-row sums of chunk c (latents 64 c .. 64 c + 63), lane = latent; contexts of
+        // rows y-3 .. y-1 from the ring (their zero rows above the image, zero pad columns)
+        auto chunk = [&](int c) {
+#if defined(CCMI_ARM_STAMPS)
+            const uint64_t tc0 = __builtin_amdgcn_s_memtime();
+#endif
+            const int x = c * kChunk + lane;
+            const bool in = x < w; // lanes past the row end compute zeros nobody reads
+            int32_t ctx[DA];
+#pragma unroll
+            for (int i = 0; i < DA; ++i) {
+                int dy, dx;
+                ctx_dydx<D>(i, dy, dx);
+                ctx[i] = in ? ring[((y + dy + kRingS) % kRingS) * pitch + kPad + x + dx] : 0;
+            }
+            int32_t *dst = pre + ((c & 1) * kChunk + lane) * 16;
+            // the 24-bit form chosen once per chunk (a per-product select doubled the work)
+            auto sums = [&](auto F24) {
+                constexpr bool f24 = decltype(F24)::value;
+#pragma unroll
+                for (int n = 0; n < 16; n += 4) {
+                    int32_t acc[4];
+#pragma unroll
+                    for (int q = 0; q < 4; ++q) {
+                        const int nn = n + q;
+                        if (nn >= D) {
+                            acc[q] = 0;
+                            continue;
+                        }
+                        int32_t a = w0s[256 + nn] + (nn < DA ? ctx[nn < DA ? nn : 0] * 256 : 0); // bias + own residual
+                        const int4 *wr = reinterpret_cast<const int4 *>(w0s + 16 * nn);
+#pragma unroll
+                        for (int i4 = 0; i4 < (DA + 3) / 4; ++i4) {
+                            const int4 wv = wr[i4];
+                            const int32_t wk[4] = {wv.x, wv.y, wv.z, wv.w};
+#pragma unroll
+                            for (int k = 0; k < 4; ++k)
+                                if (4 * i4 + k < DA) a += imul<f24>(wk[k], ctx[4 * i4 + k]);
+                        }
+                        acc[q] = a;
+                    }
+                    *reinterpret_cast<int4 *>(dst + n) = int4{acc[0], acc[1], acc[2], acc[3]};
+                }
+            };
+            if (w24 && !big) sums(std::true_type{});
+            else sums(std::false_type{});
+            if (c & 1) have1 = c;
+            else have0 = c;
+            // other lanes read these sums next: order this wave's LDS stores before its loads
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+            __builtin_amdgcn_wave_barrier();
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+#if defined(CCMI_ARM_STAMPS)
+            __builtin_amdgcn_s_waitcnt(0);
+            st_acc[7] += __builtin_amdgcn_s_memtime() - tc0;
+#endif
+        };
+        auto push = [&](int32_t v, int x) {
+            r4 = r3;
+            r3 = r2;
+            r2 = r1;
+            r1 = v;
+            if (lane == 0) row[x] = v;
+        };
+        auto fill = [&](int x, int n, int kind /*0 zero, 1 = r1, 2 = up*/) {
+            const int32_t c1 = r1;
+            for (int i = lane; i < n; i += 64) row[x + i] = kind == 0 ? 0 : kind == 1 ? c1 : up[x + i];
+            if (kind == 2) {
+                __builtin_amdgcn_s_waitcnt(0);
+                __builtin_amdgcn_wave_barrier();
+                auto at = [&](int j) { return __builtin_amdgcn_readfirstlane(row[j]); };
+                r4 = n >= 4 ? at(x + n - 4) : n == 3 ? r1 : n == 2 ? r2 : r3;
+                r3 = n >= 3 ? at(x + n - 3) : n == 2 ? r1 : r2;
+                r2 = n >= 2 ? at(x + n - 2) : r1;
+                r1 = at(x + n - 1);
+            } else {
+                const int32_t v = kind == 0 ? 0 : c1;
+                r4 = n >= 4 ? v : n == 3 ? r1 : n == 2 ? r2 : r3;
+                r3 = n >= 3 ? v : n == 2 ? r1 : r2;
+                r2 = n >= 2 ? v : r1;
+                r1 = v;
+            }
+        };
+        int bm = 1, bend = 0;
+        // above-row sums of this lane's latent (x + grp) for the next pass, read ahead
+        int pf_x = -1;
+        int32_t pf_a = 0;
+        int up_base = 0;   // up_v lane i < 8: the latent above position up_base + i (read ahead)
+        int32_t up_v = 0;
+        for (int x = 0; x < w;) {
+            int L;
+            if (blk > 0) {
+                if (x >= bend) {
+                    bm = __builtin_amdgcn_readfirstlane((int)bmap[brow + (x >> shift)]);
+                    bend = min((x | mask) + 1, w);
+                }
+                if (!(bm & 1) || ((bm & 2) && ((y & mask) || (x & mask)))) {
+                    STAMP(tf0);
+                    fill(x, bend - x, !(bm & 1) ? 0 : (y & mask) ? 2 : 1);
+                    x = bend;
+                    STAMP(tf1);
+                    ACC(8, tf0, tf1);
+#if defined(CCMI_ARM_STAMPS)
+                    st_acc[10] += 1;
+#endif
+                    continue;
+                }
+                if (bm & 2) {
+                    L = 1; // the coded corner of a flat block
+                } else {
+                    L = min(kSpec, bend - x);
+                }
+            } else {
+                L = min(kSpec, w - x);
+            }
+            // the chunks this pass and the next pass's read-ahead use (latents x .. x + 7), from
+            // one call site: the chunk body is large, and a copy per use overflowed the
+            // instruction cache
+            {
+                const int c_hi = min(x + 2 * kSpec - 1, w - 1) >> 6;
+                for (int c = x >> 6; c <= c_hi; ++c)
+                    if ((c & 1 ? have1 : have0) != c) chunk(c);
+            }
+            if (x != pf_x) { // the read-ahead missed (a block boundary or a fill moved x)
+                const int xg = x + grp;
+                pf_a = pre[(((xg >> 6) & 1) * kChunk + (xg & 63)) * 16 + o];
+                up_base = x;
+                up_v = up[x + (lane & 7)];
+            }
+            // the guesses for the undecoded latents x .. x + 2 of the speculative rows: the
+            // latents directly above (hit 75-79 % on the coded blocks of the high-rate class-E
+            // streams, against 24-37 % for a zero guess, tools/latent_stats.py)
+            const int ub = x - up_base;
+            const int32_t g0 = __builtin_amdgcn_readlane(up_v, ub), g1 = __builtin_amdgcn_readlane(up_v, ub + 1),
+                          g2 = __builtin_amdgcn_readlane(up_v, ub + 2);
+            STAMP(t0);
+            // layer 0: above-row sums + the same-row products; lane (g, o) = latent x + g, whose
+            // neighbours at or right of x are the speculative zeros
+            const int32_t s1 = grp == 0 ? r1 : grp == 1 ? g0 : grp == 2 ? g1 : g2;
+            const int32_t s2 = grp == 0 ? r2 : grp == 1 ? r1 : grp == 2 ? g0 : g1;
+            const int32_t s3 = grp == 0 ? r3 : grp == 1 ? r2 : grp == 2 ? r1 : g0;
+            const bool f1 = w24 && !big;
+            int32_t acc = pf_a;
+            if (f1) acc += imul<true>(Ws[0], s3) + imul<true>(Ws[1], s2) + imul<true>(Ws[2], s1);
+            else acc += imul<false>(Ws[0], s3) + imul<false>(Ws[1], s2) + imul<false>(Ws[2], s1);
+            int32_t a = acc < 0 ? 0 : (acc + 128) >> 8;
+#pragma unroll
+            for (int l = 1; l < NH; ++l)
+                a = w24 ? arm_hidden_rows<D, true>(Wh[l], Bh[l], a) : arm_hidden_rows<D, false>(Wh[l], Bh[l], a);
+            const int32_t m_0 = row_sum16(w24 ? imul<true>(Wo0, a) : imul<false>(Wo0, a)) + bo0;
+            const int32_t m_1 = row_sum16(w24 ? imul<true>(Wo1, a) : imul<false>(Wo1, a)) + bo1;
+#if defined(CCMI_ARM_STAMPS)
+            __builtin_amdgcn_s_waitcnt(0);
+#endif
+            STAMP(t1);
+            // mu / scale -> context-table entry (lane 16 g + 15 holds row g's sums)
+            const int32_t mu = m_0 < 0 ? -((-m_0 + 128) >> 8) : (m_0 + 128) >> 8;
+            const int32_t ls = m_1 < 0 ? -((-m_1 + 128) >> 8) : (m_1 + 128) >> 8;
+            // get_val_mu_indicies (cc-contexts.h:20-48)
+            const int32_t mr = mu >= 0 ? ((mu + 128) >> 8) << 8 : -(((-mu + 128) >> 8) << 8);
+            int32_t mi = (mu - mr) * 16;
+            mi = (mi >= 0 ? (mi + 128) >> 8 : -((-mi + 128) >> 8)) + 8;
+            const int32_t lsp = ls + 256;
+            int32_t si = lsp < 0 ? 0 : (lsp * 5 + 128) >> 8;
+            si = si > 49 ? 49 : si;
+            const uint2 e = *reinterpret_cast<const uint2 *>(ctab + (uint32_t)(mi * 50 + si) * 2u);
+            // the next pass starts at x + nd, nd = 1 .. kSpec: its above-row sums for every nd
+            int32_t nxt[kSpec];
+#pragma unroll
+            for (int k = 1; k <= kSpec; ++k) {
+                const int xg = x + k + grp;
+                nxt[k - 1] = pre[(((xg >> 6) & 1) * kChunk + (xg & 63)) * 16 + o];
+            }
+            const int32_t up_nxt = up[x + (lane & 7)]; // lane i: above x + i; the next pass reads lanes nd .. nd + 2
+            const uint32_t pk = (uint32_t)(mr >> 8) << 8 | e.y; // mu rounded, sign-bin state
+            STAMP(t2);
+            // decode_single (cc-bac.h:192-231), in order, until the first non-zero latent
+            int nd = 0;
+#pragma unroll 1
+            for (int j = 0; j < L; ++j) {
+                const int src_lane = 16 * j + 15;
+                const uint32_t st = __builtin_amdgcn_readlane(e.x, src_lane);
+                const uint32_t pkj = __builtin_amdgcn_readlane(pk, src_lane);
+                int32_t val = 0;
+                if (bin_fast(cab, st & 0xFF)) {
+                    if (!bin_fast(cab, (st >> 8) & 0xFF)) val = 1;
+                    else if (!bin_fast(cab, (st >> 16) & 0xFF)) val = 2;
+                    else if (!bin_fast(cab, st >> 24)) val = 3;
+                    else val = cab.expgolomb(0) + 4;
+                    if (bin_fast(cab, pkj & 0xFF)) val = -val;
+                }
+                const int32_t q = ((int32_t)pkj >> 8) + val;
+                big |= (q >= 32768 || q <= -32768);
+                const int32_t v = (int32_t)((uint32_t)q << kArmPrec);
+                push(v, x + j);
+                ++nd;
+                // the next row assumed this latent equal to its guess
+                if (v != (j == 0 ? g0 : j == 1 ? g1 : g2)) break;
+            }
+            STAMP(t3);
+            ACC(0, t0, t1);
+            ACC(1, t1, t2);
+            ACC(2, t2, t3);
+#if defined(CCMI_ARM_STAMPS)
+            st_acc[3] += 1;
+            st_acc[4] += nd;
+#endif
+            x += nd;
+            pf_x = x;
+            pf_a = nd == 1 ? nxt[0] : nd == 2 ? nxt[1] : nd == 3 ? nxt[2] : nxt[3];
+            up_base = x - nd;
+            up_v = up_nxt;
+        }
+        STAMP(tr0);
+        __syncthreads();
+        int32_t *dst = S.out + (int64_t)y * w;
+        for (int x = lane; x < w; x += 64) dst[x] = row[x];
+        __syncthreads();
+        STAMP(tr1);
+        ACC(9, tr0, tr1);
+    }
+#if defined(CCMI_ARM_STAMPS)
+    st_acc[6] = __builtin_amdgcn_s_memtime() - t_loop;
+    if (lane == 0 && S.dbg)
+        for (int k = 0; k < 16; ++k) S.dbg[k] = st_acc[k];
+#endif
+}
+
 // ------------------------------------------------------------------ upsampling (integer)
 constexpr int kThreads = 256;
 constexpr int kTY = 16, kTX = 64;
@@ -954,6 +1383,19 @@ int launch_dec_arm(const ArmStreamDesc *d_streams, int n_streams, int max_w, int
 #else
     constexpr bool spec_off = false;
 #endif
+    // the latency-optimised kernel: + two 64-latent chunks of above-row sums in LDS
+    const size_t lds_lat = lds_spec + sizeof(int32_t) * (2 * kChunk * 16 + 16 * 16 + 16);
+    if (!spec_off && d <= 16 && d > kDS && nh >= 1 && lds_lat <= 160 * 1024) {
+#define CCMI_ARM_LAT(DD, NN)                                                                                    \
+        if (d == DD && nh == NN) {                                                                              \
+            hipLaunchKernelGGL((dec_arm_lat_kernel<DD, NN>), dim3(n_streams), dim3(64), lds_lat, s, d_streams, pitch); \
+            CCMI_HIP_CHECK(hipGetLastError());                                                                  \
+            return CCMI_OK;                                                                                     \
+        }
+        CCMI_ARM_LAT(8, 1) CCMI_ARM_LAT(8, 2) CCMI_ARM_LAT(8, 3) CCMI_ARM_LAT(8, 4)
+        CCMI_ARM_LAT(16, 1) CCMI_ARM_LAT(16, 2) CCMI_ARM_LAT(16, 3) CCMI_ARM_LAT(16, 4)
+#undef CCMI_ARM_LAT
+    }
     if (!spec_off && d <= 16 && lds_spec <= 160 * 1024) {
 #define CCMI_ARM_SPEC(DD, NN)                                                                                   \
         if (d == DD && nh == NN) {                                                                              \

@@ -1972,7 +1972,7 @@ extern "C" int ccmi_quantize_f32(const float *x, int64_t n, int quantizer, float
                                  float *y, float *dy, void *stream)
 {
     if (!x || !y || n < 0) return ccmi_set_error(CCMI_ERR_ARG, "quantize: null argument");
-    if (n > INT32_MAX) return ccmi_set_error(CCMI_ERR_ARG, "quantize: n > 2^31");
+    if (n > INT32_MAX - kT) return ccmi_set_error(CCMI_ERR_ARG, "quantize: n > 2^31 - %d", kT); // int thread indices
     if (quantizer < CCMI_Q_NONE || quantizer > CCMI_Q_TRUE_STE) return ccmi_set_error(CCMI_ERR_ARG, "quantize: type %d", quantizer);
     if ((quantizer == CCMI_Q_SOFTROUND || quantizer == CCMI_Q_SOFTROUND_ALONE || quantizer == CCMI_Q_STE) &&
         !(temperature > 0.f))
@@ -2086,6 +2086,11 @@ extern "C" int ccmi_train_step(const ccmi_train_args *a, void *stream)
         CCMI_HIP_CHECK(hipMemcpyAsync(a->raw_out, F(pl.z[g.n_sp]), sizeof(float) * 3 * npx * B, hipMemcpyDeviceToDevice, s));
     if (a->forward_only) {
         if (a->loss_out) {
+            // with a real target (target_stride > 0) the loss row holds the built-in MSE too;
+            // otherwise (autograd: the loss lives in torch) MSE reads 0 and loss = lmbda-rate
+            if (a->target && a->target_stride > 0)
+                hipLaunchKernelGGL(t_loss, dim3(std::min(grid1(npx, B).x, 256u), B), dim3(kT), 0, s, F(pl.z[g.n_sp]), g,
+                                   a->target, a->target_stride, a->yuv420, graw, acc4);
             const float total = a->yuv420 ? (float)(npx + 2 * (int64_t)(g.H / 2) * (g.W / 2)) : (float)(3 * npx);
             hipLaunchKernelGGL(t_finish, dim3(1), dim3(std::max(64, B)), 0, s, acc4, 1.f / total, lam_px, a->loss_out, B);
         }

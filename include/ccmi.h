@@ -400,7 +400,8 @@ typedef struct ccmi_train_args {
     uint64_t seed;          /* noise: counter-based RNG keyed by (seed, step, frame, index) */
     const float *noise_in;  /* optional [batch][latent_stride]: additive noise used as is */
     float *grad_out;        /* optional [batch][N + P]: raw gradients (before clipping) */
-    float *loss_out;        /* optional [batch][4]: loss, mse, rate_bits, grad_norm */
+    float *loss_out;        /* optional [batch][4]: loss, mse, rate_bits, grad_norm (forward_only:
+                               grad_norm 0; mse 0 unless a target is given, target_stride > 0) */
     int update;             /* 0: loss and gradients only; 1: Adam on everything; 2: Adam on the
                                latents only (optimized_module ["latent"]; the norm still covers all) */
     void *workspace;        /* ccmi_train_workspace_bytes() */

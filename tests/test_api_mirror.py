@@ -95,6 +95,60 @@ def test_frame_encoder_yuv420(gpu, ccmi_lib):
         assert np.mean(out.decoded_image[k][0, 0].cpu().numpy() != z[f"dec420_{k}"]) < 1e-3
 
 
+def _random_720p_frame_encoder(fmt, seed=0):
+    from coolchic.enc.component.coolchic import CoolChicEncoderParameter
+    from coolchic.enc.component.frame import FrameEncoder
+    p = CoolChicEncoderParameter(layers_synthesis=["48-1-linear-relu", "3-1-linear-none", "3-3-residual-relu",
+                                                   "3-3-residual-none"], n_ft_per_res=[1] * 7, dim_arm=16,
+                                 n_hidden_layers_arm=2)
+    p.set_image_size((720, 1280))
+    fe = FrameEncoder(p, frame_data_type=fmt).eval()
+    g = torch.Generator().manual_seed(seed)
+    with torch.no_grad():
+        for name, prm in fe.named_parameters():
+            if "upsampling" in name:
+                continue  # keep the bicubic / Dirac initial kernels
+            scale = 0.5 if "latent_grids" in name else 0.3 / max(1, prm[0].numel()) ** 0.5 if prm.dim() > 1 else 0.05
+            prm.copy_(scale * torch.randn(prm.shape, generator=g))
+            if "synthesis.layers.2.bias" in name:
+                prm.add_(0.5)  # outputs around mid-grey, so the clamp and the rounding both matter
+    return fe
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("fmt", ["rgb", "yuv420"])
+def test_frame_encoder_eval_runs_the_fused_kernel(fmt, gpu, ccmi_lib, monkeypatch):
+    """FrameEncoder.forward in eval mode (frame.py:153-183) goes through the fused decode
+    kernel (ccmi_decode_forward_f32, coolchic.decoded_batch) and equals the staged path
+    (CoolChicEncoder.forward's raw output + ccmi_post_f32) at 720p except on rounding ties:
+    a pixel may differ only where the staged raw value lies within the synthesis tolerance
+    (2e-5 (1 + max |raw|), x 255) of a k + 1/2 boundary of the 8-bit grid."""
+    import coolchic.enc.component.frame as FR
+    fe = _random_720p_frame_encoder(fmt).to(gpu)
+    calls = []
+    real = FR.decoded_batch
+    monkeypatch.setattr(FR, "decoded_batch", lambda *a, **k: calls.append(1) or real(*a, **k))
+    out = fe.forward()
+    assert calls, "eval forward did not take the fused path"
+    raw, rate_s, _ = fe.coolchic_encoder.forward()
+    ref = fe.post_process(raw)
+    assert torch.equal(out.rate, rate_s)
+    r = raw[0].double().cpu()
+    band = 255 * 2e-5 * (1 + float(r.abs().max()))
+    frac = (255 * r - torch.floor(255 * r) - 0.5).abs()
+    tie = frac < band
+    if fmt == "rgb":
+        pairs = [(out.decoded_image[0].cpu(), ref[0].cpu(), tie)]
+    else:
+        ties = {"y": tie[0:1], "u": tie[1:2, 0::2, 0::2], "v": tie[2:3, 0::2, 0::2]}
+        pairs = [(out.decoded_image[k][0].cpu(), ref[k][0].cpu(), ties[k]) for k in "yuv"]
+    for a, b, t in pairs:
+        diff = a != b
+        assert float(diff.float().mean()) < 1e-3
+        assert bool((~diff | t).all()), "a decoded pixel differs away from a rounding tie"
+        assert float((a - b).abs().max()) <= 1.0 / 255 + 1e-7
+
+
 @pytest.mark.gpu
 def test_cclib_shim_and_cli_decode(gpu, ccmi_lib, tmp_path):
     from CCLIB.ccdecapi_avx2 import cc_decode_avx2

@@ -101,3 +101,46 @@ def test_mirror_quantizer_matches_reference_formulas(gpu):
         yc.sum().backward()
         np.testing.assert_allclose(y.detach().cpu().numpy(), yc.detach().numpy(), rtol=1e-5, atol=1e-5, err_msg=qtype)
         np.testing.assert_allclose(xg.grad.cpu().numpy(), xc.grad.numpy(), rtol=1e-4, atol=1e-5, err_msg=qtype)
+
+
+@pytest.mark.parametrize("qtype,ntype,nparam", [("softround", "kumaraswamy", 2.0), ("softround", "gaussian", 0.25),
+                                               ("none", "kumaraswamy", 1.0)])
+def test_mirror_train_forward_with_noise_matches_oracle(qtype, ntype, nparam, gpu):
+    """The autograd bridge (ccmi.autograd.TrainForward behind the mirror CoolChicEncoder
+    forward in train mode) with real quantisation noise -- drawn by the mirror with the
+    reference's torch calls (quantizer.py:188-197) -- against the CPU oracle's train-mode
+    forward / backward (oracle/train_oracle.py, pinned to the reference goldens) given the
+    same noise tensor: loss and every parameter gradient.  Tolerances as test_train_gpu.py
+    (fp32, different summation order; latent grids: 0.1 % of entries may reach 4x, the
+    1 / P factor of the rate deep in the Laplace tails)."""
+    import train_oracle as to
+    from coolchic.enc.component.core.quantizer import draw_noise
+    from coolchic.enc.training.loss import loss_function
+    z = np.load(FILES[0])
+    fe, target, meta = _build(z, gpu)
+    enc = fe.coolchic_encoder
+    torch.manual_seed(11)
+    out = fe.forward(quantizer_noise_type=ntype, quantizer_type=qtype, soft_round_temperature=torch.tensor(0.3),
+                     noise_parameter=torch.tensor(nparam))
+    lo = loss_function(out.decoded_image, out.rate, target, lmbda=meta["lmbda"], rate_mlp_bit=0.0, compute_logs=False)
+    lo.loss.backward()
+    torch.manual_seed(11)  # the same draw again, for the oracle
+    noise = draw_noise(enc.flat_latent().detach() * enc.encoder_gains, ntype, torch.tensor(nparam))
+    assert noise is not None and float(noise.abs().max()) > 0
+    st, tgt, _ = to.from_golden(z)
+    L, _, _ = to.grads(st, tgt, qtype, 0.3, meta["lmbda"], meta["yuv420"], noise=noise[0].cpu())
+    assert abs(lo.loss.item() - L) <= 1e-5 * abs(L), (lo.loss.item(), L)
+    mine = dict(enc.named_parameters())
+    n_checked = 0
+    for name, p in zip(to.golden_param_names(meta), st.params()):
+        ref = p.grad.reshape(-1).numpy()
+        q = mine[name]
+        got = (q.grad if q.grad is not None else torch.zeros_like(q)).reshape(-1).cpu().numpy()
+        tol = 2e-3 * np.abs(ref) + 1e-7 + 2e-4 * np.abs(ref).max()
+        err = np.abs(got - ref)
+        if "latent_grids" in name:
+            assert np.mean(err > tol) <= 1e-3 and np.all(err <= 4 * tol), (name, int((err > tol).sum()))
+        else:
+            assert np.all(err <= tol), (name, float((err / tol).max()))
+        n_checked += 1
+    assert n_checked == len(list(st.params()))

@@ -64,11 +64,12 @@ def _adam_close(got, ref, lr, name, g0=None):
     next to the tensor's largest takes a step as sensitive to the float error of its gradient
     (bounded by the gradient test above: ~4e-5 of the tensor's largest at 128 x 192, the CPU
     restatement's own level) as the gradient is small.  Entries off by more than 2e-3 lr must
-    be such entries (|g0| < 5 % of the tensor's largest) or at most 2 % of the tensor."""
+    be such entries (|g0| < 5 % of the tensor's largest) or at most 2 % of the tensor; even
+    small-gradient entries may be at most 10 % of the tensor."""
     bad = np.abs(got - ref) > 1e-5 * np.abs(ref) + 2e-3 * lr
     if g0 is not None and bad.any():
         small = np.abs(g0) < 0.05 * np.abs(g0).max()
-        assert bad.mean() <= 0.02 or np.all(small[bad]), \
+        assert bad.mean() <= 0.02 or (np.all(small[bad]) and bad.mean() <= 0.1), \
             f"{name}: {int(bad.sum())} of {bad.size} entries off, {int((bad & ~small).sum())} with a large gradient"
     else:
         assert bad.mean() <= 0.02, f"{name}: {int(bad.sum())} of {bad.size} entries off"
@@ -153,6 +154,46 @@ def test_gpu_two_adam_steps_match_reference(f, gpu):
             _adam_close(flat[o:o + n], z[f"s{s}/{name}"].reshape(-1), meta["lr"], f"step {s} {name}",
                         z[f"g/{name}"].reshape(-1))
             o += n
+
+
+@pytest.mark.parametrize("f", [f for f in FILES if "g1/latent_grids.0.data" in np.load(f).files],
+                         ids=lambda f: f.stem)
+def test_gpu_two_adam_steps_at_128x192(f, gpu):
+    """Two clipped-Adam steps on the realistic-size golden.  Step 1 is compared for every
+    tensor.  Step 2 starts from OUR step-1 parameters, so it is compared only for the tensors
+    whose gradient there already matches the reference's step-1 gradient (g1): on the others
+    the trajectories split at a clamp / ReLU switch of a few latents (see the step-1 gradient
+    test above), which is not a kernel error."""
+    import train_oracle as to
+    z = np.load(f)
+    of, st, target, meta = _setup(z, gpu)
+    names = to.golden_param_names(meta)
+    sizes = [p.numel() for p in st.params()]
+    of.step(meta["quantizer_type"], "none", meta["temperature"], 0.0, meta["lmbda"], lr=meta["lr"], clip=0.1)
+    g = torch.zeros(1, of.N + of.P, device=gpu)
+    of.step(meta["quantizer_type"], "none", meta["temperature"], 0.0, meta["lmbda"], update=False, grad_out=g)
+    torch.cuda.synchronize()
+    flat1 = np.concatenate([of.latents[0].cpu().numpy(), of.params[0].cpu().numpy()])
+    g1 = g[0].cpu().numpy()
+    match, o = {}, 0
+    for name, n in zip(names, sizes):
+        _adam_close(flat1[o:o + n], z[f"s1/{name}"].reshape(-1), meta["lr"], f"step 1 {name}", z[f"g/{name}"].reshape(-1))
+        try:
+            _grad_close(g1[o:o + n], z[f"g1/{name}"].reshape(-1), name)
+            match[name] = True
+        except AssertionError:
+            match[name] = False
+        o += n
+    assert sum(match.values()) >= len(names) // 2, match
+    of.step(meta["quantizer_type"], "none", meta["temperature"], 0.0, meta["lmbda"], lr=meta["lr"], clip=0.1)
+    torch.cuda.synchronize()
+    flat2 = np.concatenate([of.latents[0].cpu().numpy(), of.params[0].cpu().numpy()])
+    o = 0
+    for name, n in zip(names, sizes):
+        if match[name]:
+            _adam_close(flat2[o:o + n], z[f"s2/{name}"].reshape(-1), meta["lr"], f"step 2 {name}",
+                        z[f"g1/{name}"].reshape(-1))
+        o += n
 
 
 @pytest.mark.parametrize("qtype,ntype", [("softround", "kumaraswamy"), ("softround", "gaussian"), ("none", "kumaraswamy"),
