@@ -612,6 +612,7 @@ __global__ __launch_bounds__(64) void dec_arm_spec_kernel(const ArmStreamDesc *_
 //  * the CABAC bin uses a count-leading-zeros renormalisation and selects instead of
 //    the branchy lps_renorm ladder (same state transitions as TDecBinCABAC::decodeBin).
 constexpr int kDS = 3; // same-row contexts (0, -3), (0, -2), (0, -1): the last three context indices
+constexpr int kChunk = 64;
 
 // Byte source of the latency kernel: the stream's words come through wave-uniform VECTOR
 // loads issued one word ahead (the scalar-load reader's fetch is counted in lgkmcnt with
@@ -649,7 +650,6 @@ struct DevBytesV {
         return b;
     }
 };
-constexpr int kChunk = 64;
 
 // A static context's model state st (0..255) as the bin decode uses it: the MPS in bit 7,
 // the LPS-side state's top bits (st ^ 0xFF when the MPS is 1, then >> 2) in bits 0..4.
@@ -690,7 +690,12 @@ __global__ __launch_bounds__(64) void dec_arm_lat_kernel(const ArmStreamDesc *__
     // [0] ARM pass (same-row products + MLP + output sums)  [1] index + table  [2] CABAC
     // [3] ARM passes  [4] coded latents  [5] setup  [6] latent loop  [7] chunk precompute
     // [8] block fills  [9] row copy-out  [10] blocks visited
-    uint64_t st_acc[16] = {};
+    // counters in a VGPR (lane k = counter k, 32-bit cycles): SGPR accumulators pushed the
+    // kernel's wave-uniform state out to VGPR lanes and distorted what they measured
+    uint32_t st_v = 0;
+#define LACC(k, d) st_v += (threadIdx.x == (k)) ? (uint32_t)(d) : 0u
+#undef ACC
+#define ACC(k, a, b) LACC(k, (b) - (a))
     const uint64_t t_begin = __builtin_amdgcn_s_memtime();
 #endif
     extern __shared__ int32_t smem[];
@@ -788,7 +793,7 @@ __global__ __launch_bounds__(64) void dec_arm_lat_kernel(const ArmStreamDesc *__
     // context offsets of the above-row contexts (rows y-3 .. y-1), for the chunk precompute
     int big = 0;
 #if defined(CCMI_ARM_STAMPS)
-    st_acc[5] = __builtin_amdgcn_s_memtime() - t_begin;
+    LACC(5, __builtin_amdgcn_s_memtime() - t_begin);
     const uint64_t t_loop = __builtin_amdgcn_s_memtime();
 #endif
 
@@ -852,7 +857,7 @@ __global__ __launch_bounds__(64) void dec_arm_lat_kernel(const ArmStreamDesc *__
             __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 #if defined(CCMI_ARM_STAMPS)
             __builtin_amdgcn_s_waitcnt(0);
-            st_acc[7] += __builtin_amdgcn_s_memtime() - tc0;
+            LACC(7, __builtin_amdgcn_s_memtime() - tc0);
 #endif
         };
         auto push = [&](int32_t v, int x) {
@@ -901,7 +906,7 @@ __global__ __launch_bounds__(64) void dec_arm_lat_kernel(const ArmStreamDesc *__
                     STAMP(tf1);
                     ACC(8, tf0, tf1);
 #if defined(CCMI_ARM_STAMPS)
-                    st_acc[10] += 1;
+                    LACC(10, 1);
 #endif
                     continue;
                 }
@@ -913,6 +918,7 @@ __global__ __launch_bounds__(64) void dec_arm_lat_kernel(const ArmStreamDesc *__
             } else {
                 L = min(kSpec, w - x);
             }
+            STAMP(tp);
             // the chunks this pass and the next pass's read-ahead use (latents x .. x + 7), from
             // one call site: the chunk body is large, and a copy per use overflowed the
             // instruction cache
@@ -998,18 +1004,21 @@ __global__ __launch_bounds__(64) void dec_arm_lat_kernel(const ArmStreamDesc *__
                 if (v != (j == 0 ? g0 : j == 1 ? g1 : g2)) break;
             }
             STAMP(t3);
+            ACC(12, tp, t0);
             ACC(0, t0, t1);
             ACC(1, t1, t2);
             ACC(2, t2, t3);
 #if defined(CCMI_ARM_STAMPS)
-            st_acc[3] += 1;
-            st_acc[4] += nd;
+            LACC(3, 1);
+            LACC(4, nd);
 #endif
             x += nd;
             pf_x = x;
             pf_a = nd == 1 ? nxt[0] : nd == 2 ? nxt[1] : nd == 3 ? nxt[2] : nxt[3];
             up_base = x - nd;
             up_v = up_nxt;
+            STAMP(t4);
+            ACC(11, t3, t4);
         }
         STAMP(tr0);
         __syncthreads();
@@ -1020,9 +1029,11 @@ __global__ __launch_bounds__(64) void dec_arm_lat_kernel(const ArmStreamDesc *__
         ACC(9, tr0, tr1);
     }
 #if defined(CCMI_ARM_STAMPS)
-    st_acc[6] = __builtin_amdgcn_s_memtime() - t_loop;
-    if (lane == 0 && S.dbg)
-        for (int k = 0; k < 16; ++k) S.dbg[k] = st_acc[k];
+    LACC(6, __builtin_amdgcn_s_memtime() - t_loop);
+    if (lane < 16 && S.dbg) S.dbg[lane] = st_v;
+#undef LACC
+#undef ACC
+#define ACC(k, a, b) st_acc[k] += (b) - (a)
 #endif
 }
 

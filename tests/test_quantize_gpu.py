@@ -47,3 +47,31 @@ def test_quantize_model_matches_reference_search(gpu):
             assert row[0, 2] - ref[:, 2].min() <= 2 * spread + 1e-12, (m, qm.q_step[m], chosen)
         else:
             assert tuple(qm.expgol[m]) == tuple(int(v) for v in z[f"expgol/{m}"]), m
+
+
+def test_train_and_eval_rate_forms_agree(gpu):
+    """The Laplace rate (arm.py:355-370, coolchic.py:419-424) exists in two fp32 forms: the
+    training step (train.hip arm_rate: expm1f and an IEEE division, as torch evaluates it) and
+    the eval forward that quantize_model / test() use (fwd_arm.hip laplace_cdf: v_exp_f32 - 1
+    and one v_rcp_f32 shared by both CDF terms, 5 % faster).  On the reference-trained model
+    of the quantize fixture, the two total rates (hard-rounded latents, the same network)
+    must agree within 2e-6 relative -- well inside the 1e-5 rate tolerance of the parity
+    tests and far below what moves a quantize_model choice (the loss-offset spread above is
+    1e-6 of the loss); the measured difference is printed."""
+    import forward_oracle as fo
+    from ccmi import quantize as Q
+    from ccmi import train as T
+    z = np.load(GOLDEN / "quantize_ref_kodim15_hop.npz")
+    meta = ast.literal_eval(str(z["meta"]))
+    mp = fo.ModelParams.from_npz(z)
+    arch = T.Arch(meta["H"], meta["W"], dim_arm=mp.dim_arm, n_hidden=mp.n_hidden, layers=tuple(mp.layers),
+                  n_grids=mp.n_grids, gain=mp.gain)
+    params = T.pack_params(mp.arm, mp.ups_half, mp.pre_half, mp.syn).to(gpu)
+    lat = torch.cat([torch.from_numpy(z[f"p/latent_grids.{i}.data"]).reshape(-1) for i in range(mp.n_grids)]).to(gpu)
+    tgt = torch.from_numpy(z["target"]).reshape(-1).float().to(gpu)
+    _, rate_eval = Q.evaluate(arch, lat, params, tgt, yuv420=False, bitdepth=8)
+    of = T.Overfitter(arch, lat[None], params[None], tgt[None], yuv420=False)
+    rate_train = float(of.validate(meta["lmbda"])[0, 2])
+    rel = abs(rate_eval - rate_train) / rate_train
+    print(f"\nrate: eval form {rate_eval:.4f} bits, train form {rate_train:.4f} bits, relative difference {rel:.3g}")
+    assert rel <= 2e-6, rel

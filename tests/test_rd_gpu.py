@@ -41,6 +41,9 @@ RATE_MARGIN = 0.15     # relative, on top of the reference's spread
 # 120-iteration curves are too noisy for a cubic fit (the reference's own seed 1 against its
 # seed 0 gives -66.6 % there, -0.45 % on kodim01 at 768 x 512).
 BD_WORSE, BD_BETTER = 10.0, 25.0
+# Kodak geometry (768 x 512, config 4's content): the band narrowed to +-5 % (measured: c3x
+# x0.1 +0.9 / +1.0 %, debug -0.65 %; profiles/r3_rd_gpu_summary.txt)
+BD_KODAK = 5.0
 
 pytestmark = pytest.mark.gpu
 
@@ -83,7 +86,8 @@ def _check(image, ours, ref, bd_band):
     lines.append(f"{image}: BD-rate GPU vs reference {bd:+.2f} %")
     print("\n" + "\n".join(lines))
     if bd_band:
-        assert -BD_BETTER <= bd <= BD_WORSE, lines[-1]
+        lo, hi = (-BD_KODAK, BD_KODAK) if image == "kodim01_768x512" else (-BD_BETTER, BD_WORSE)
+        assert lo <= bd <= hi, lines[-1]
     return bd
 
 
@@ -159,5 +163,7 @@ def test_c3x_preset_matches_reference_rd(image, gpu):
     bd = rd.bd_rate(R1, P1, R2, P2)
     lines.append(f"{image} c3x: BD-rate GPU vs reference {bd:+.2f} %")
     print("\n" + "\n".join(lines))
-    if image != "kodim15_192x128":
+    if image == "kodim01_768x512":
+        assert -BD_KODAK <= bd <= BD_KODAK, lines[-1]
+    elif image != "kodim15_192x128":
         assert -BD_BETTER <= bd <= BD_WORSE, lines[-1]
