@@ -1332,62 +1332,6 @@ struct UpLevel {
     int C, hs, ws, hd, wd, K, d_lo, d_hi, sidx; // sidx: kernel slot (step % n_ups)
 };
 
-// refine, horizontal pass: U[r][x] = sum_k w[k] X[r][x + k - P] (zero padding)
-__global__ void t_ref_u(const float *__restrict__ X, int64_t xs, int h, int w, const float *__restrict__ kf, int kstride,
-                        int koff, int Kp, float *__restrict__ U, int64_t us)
-{
-    const int b = blockIdx.y;
-    const int n = h * w, i = blockIdx.x * kT + threadIdx.x;
-    if (i >= n) return;
-    const int r = i / w, x = i - r * w, P = Kp / 2;
-    const float *wk = kf + (int64_t)b * kstride + koff, *src = X + (int64_t)b * xs + (int64_t)r * w;
-    float a = 0.f;
-    for (int k = 0; k < Kp; ++k) {
-        const int xx = x + k - P;
-        if (xx >= 0 && xx < w) a = fmaf(wk[k], src[xx], a);
-    }
-    U[(int64_t)b * us + i] = a;
-}
-
-// refine, vertical adjoint: GU[r][x] = sum_k w[k] GY[r - k + P][x]
-__global__ void t_ref_gu(const float *__restrict__ GY, int64_t gys, int h, int w, const float *__restrict__ kf,
-                         int kstride, int koff, int Kp, float *__restrict__ GU, int64_t us)
-{
-    const int b = blockIdx.y;
-    const int n = h * w, i = blockIdx.x * kT + threadIdx.x;
-    if (i >= n) return;
-    const int P = Kp / 2;
-    const float *wk = kf + (int64_t)b * kstride + koff;
-    const int r = i / w, x = i - r * w;
-    const float *gy = GY + (int64_t)b * gys;
-    float a = 0.f;
-    for (int k = 0; k < Kp; ++k) {
-        const int rr = r - k + P;
-        if (rr >= 0 && rr < h) a = fmaf(wk[k], gy[(int64_t)rr * w + x], a);
-    }
-    GU[(int64_t)b * us + i] = a;
-}
-
-// refine, horizontal adjoint + residual: GX += sum_k w[k] GU[r][m - k + P] + GY
-__global__ void t_ref_gx(const float *__restrict__ GU, int64_t us, const float *__restrict__ GY, int64_t gys, int h,
-                         int w, const float *__restrict__ kf, int kstride, int koff, int Kp, float *__restrict__ GX,
-                         int64_t gxs)
-{
-    const int b = blockIdx.y;
-    const int n = h * w, i = blockIdx.x * kT + threadIdx.x;
-    if (i >= n) return;
-    const int P = Kp / 2;
-    const float *wk = kf + (int64_t)b * kstride + koff;
-    const int r = i / w, m = i - r * w;
-    const float *gu = GU + (int64_t)b * us + (int64_t)r * w;
-    float a = GY[(int64_t)b * gys + i];
-    for (int k = 0; k < Kp; ++k) {
-        const int mm = m - k + P;
-        if (mm >= 0 && mm < w) a = fmaf(wk[k], gu[mm], a);
-    }
-    GX[(int64_t)b * gxs + i] += a;
-}
-
 // Sum of per-thread tap gradients over the workgroup, folded onto the symmetric half
 // kernel (upsampling.py:46-68): one atomic per half tap per workgroup.
 // Upsampling kernel gradients: each workgroup of a t_*_dw reduction adds its taps into one
@@ -1427,32 +1371,69 @@ __device__ __forceinline__ void reduce_taps(float (&dw)[K], float *__restrict__ 
     }
 }
 
-// refine kernel gradient over the level's pixels: vertical taps (GY x U) + horizontal taps (GU x X)
+// Refine backward of one pyramid level in ONE launch (formerly four
+// passes over the level through HBM temporaries): a 16 x 64 tile of the level
+// with its KP / 2 halo of X and GY staged in LDS; the horizontal pass U = X * w and the
+// vertical adjoint GU = GY (*) w of the tile are formed in LDS, then the latent gradient
+// GX += GY + horizontal adjoint of GU and the tap gradients (GY x U, GU x X) of the tile's
+// positions.  Per element the same fmaf chains in the same order as the former separate passes
+// (a zero-padded tap adds an exact 0).
 template <int KP>
-__global__ __launch_bounds__(kT) void t_ref_dw(const float *__restrict__ GY, int64_t gys, const float *__restrict__ U,
-                                               const float *__restrict__ GU, int64_t us, const float *__restrict__ X,
-                                               int64_t xs, int h, int w, float *__restrict__ gth, int64_t gstride,
-                                               int hoff)
+__global__ __launch_bounds__(kT) void t_ref_bwd(const float *__restrict__ GY, int64_t gys, const float *__restrict__ X,
+                                                int64_t xs, int h, int w, const float *__restrict__ kf, int kstride, int koff,
+                                                float *__restrict__ GX, int64_t gxs, float *__restrict__ slots,
+                                                int64_t gstride, int hoff, int tiles_x)
 {
-    constexpr int P = KP / 2;
-    const int b = blockIdx.y;
-    const int64_t n = (int64_t)h * w;
-    const float *gy = GY + (int64_t)b * gys, *u = U + (int64_t)b * us, *gu = GU + (int64_t)b * us;
-    const float *x = X + (int64_t)b * xs;
+    constexpr int P = KP / 2, TY = 16, TX = 64, SY = TY + 2 * P, SX = TX + 2 * P;
+    __shared__ float sx[SY][SX], sg[SY][SX], su[SY][TX], sgu[TY][SX];
+    const int b = blockIdx.y, tid = threadIdx.x;
+    const int ty0 = (blockIdx.x / tiles_x) * TY, tx0 = (blockIdx.x % tiles_x) * TX;
+    const float *wk = kf + (int64_t)b * kstride + koff;
+    float wv[KP];
+#pragma unroll
+    for (int k = 0; k < KP; ++k) wv[k] = wk[k];
+    const float *xb = X + (int64_t)b * xs, *gb = GY + (int64_t)b * gys;
+    for (int i = tid; i < SY * SX; i += kT) {
+        const int r = i / SX, c = i - r * SX, y = ty0 - P + r, x = tx0 - P + c;
+        const bool in = y >= 0 && y < h && x >= 0 && x < w;
+        sx[r][c] = in ? xb[(int64_t)y * w + x] : 0.f;
+        sg[r][c] = in ? gb[(int64_t)y * w + x] : 0.f;
+    }
+    __syncthreads();
+    for (int i = tid; i < SY * TX; i += kT) { // U rows ty0 - P .. ty0 + TY + P - 1
+        const int r = i / TX, c = i - r * TX;
+        float a = 0.f;
+#pragma unroll
+        for (int k = 0; k < KP; ++k) a = fmaf(wv[k], sx[r][c + k], a);
+        su[r][c] = a;
+    }
+    for (int i = tid; i < TY * SX; i += kT) { // GU cols tx0 - P .. tx0 + TX + P - 1
+        const int t = i / SX, c = i - t * SX;
+        float a = 0.f;
+#pragma unroll
+        for (int k = 0; k < KP; ++k) a = fmaf(wv[k], sg[t + 2 * P - k][c], a);
+        sgu[t][c] = a;
+    }
+    __syncthreads();
     float dw[KP];
 #pragma unroll
     for (int k = 0; k < KP; ++k) dw[k] = 0.f;
-    for (int64_t i = (int64_t)blockIdx.x * kT + threadIdx.x; i < n; i += (int64_t)gridDim.x * kT) {
-        const int r = (int)i / w, c = (int)i - r * w;
-        const float gv = gy[i], guv = gu[i];
+    float *gxb = GX + (int64_t)b * gxs;
+    for (int i = tid; i < TY * TX; i += kT) {
+        const int t = i / TX, c = i - t * TX, y = ty0 + t, x = tx0 + c;
+        if (y >= h || x >= w) continue;
+        const float gv = sg[t + P][c + P], guv = sgu[t][c + P];
+        float a = gv;
+#pragma unroll
+        for (int k = 0; k < KP; ++k) a = fmaf(wv[k], sgu[t][c - k + 2 * P], a);
+        gxb[(int64_t)y * w + x] += a;
 #pragma unroll
         for (int k = 0; k < KP; ++k) {
-            const int ru = r + k - P, cx = c + k - P;
-            if (ru >= 0 && ru < h) dw[k] = fmaf(gv, u[(int64_t)ru * w + c], dw[k]);
-            if (cx >= 0 && cx < w) dw[k] = fmaf(guv, x[(int64_t)r * w + cx], dw[k]);
+            dw[k] = fmaf(gv, su[t + k][c], dw[k]);
+            dw[k] = fmaf(guv, sx[t + P][c + k], dw[k]);
         }
     }
-    reduce_taps<KP>(dw, gth + ((int64_t)b * kDwSlots + blockIdx.x % kDwSlots) * gstride + hoff);
+    reduce_taps<KP>(dw, slots + ((int64_t)b * kDwSlots + blockIdx.x % kDwSlots) * gstride + hoff);
 }
 
 __device__ __forceinline__ int up_tap(int a, int d, int K) { return a + K / 2 - 1 - 2 * d; }
@@ -2142,20 +2123,22 @@ extern "C" int ccmi_train_step(const ccmi_train_args *a, void *stream)
             const int koff = g.n_ups * g.K + (step % g.n_pre) * g.Kp;
             const int hoff = g.pre_off + (step % g.n_pre) * g.hp;
             const int64_t n = (int64_t)hd * wd;
-            hipLaunchKernelGGL(t_ref_u, grid1(n, B), dim3(kT), 0, s, X, (int64_t)g.N, hd, wd, kf, g.kfull, koff, g.Kp, U,
-                               pl.tmp_per);
-            hipLaunchKernelGGL(t_ref_gu, grid1(n, B), dim3(kT), 0, s, GY, gys, hd, wd, kf, g.kfull, koff, g.Kp, GU,
-                               pl.tmp_per);
-            const dim3 gr(dw_blocks(n), B);
+            // one fused launch per level (tile 16 x 64)
+            const int tx = ccmi_div_up(wd, 64);
+            const dim3 gr((unsigned)(tx * ccmi_div_up(hd, 16)), B);
+            float *GXd = gq + g.off[k - 1];
+#define CCMI_REF_BWD(KK)                                                                                             \
+    hipLaunchKernelGGL(t_ref_bwd<KK>, gr, dim3(kT), 0, s, GY, gys, X, (int64_t)g.N, hd, wd, kf, g.kfull, koff, GXd,   \
+                       (int64_t)g.N, slots, (int64_t)nreg, hoff - g.up_off, tx)
             switch (g.Kp) {
-            case 1: hipLaunchKernelGGL(t_ref_dw<1>, gr, dim3(kT), 0, s, GY, gys, U, GU, pl.tmp_per, X, (int64_t)g.N, hd, wd, slots, (int64_t)nreg, hoff - g.up_off); break;
-            case 3: hipLaunchKernelGGL(t_ref_dw<3>, gr, dim3(kT), 0, s, GY, gys, U, GU, pl.tmp_per, X, (int64_t)g.N, hd, wd, slots, (int64_t)nreg, hoff - g.up_off); break;
-            case 5: hipLaunchKernelGGL(t_ref_dw<5>, gr, dim3(kT), 0, s, GY, gys, U, GU, pl.tmp_per, X, (int64_t)g.N, hd, wd, slots, (int64_t)nreg, hoff - g.up_off); break;
-            case 7: hipLaunchKernelGGL(t_ref_dw<7>, gr, dim3(kT), 0, s, GY, gys, U, GU, pl.tmp_per, X, (int64_t)g.N, hd, wd, slots, (int64_t)nreg, hoff - g.up_off); break;
-            default: hipLaunchKernelGGL(t_ref_dw<9>, gr, dim3(kT), 0, s, GY, gys, U, GU, pl.tmp_per, X, (int64_t)g.N, hd, wd, slots, (int64_t)nreg, hoff - g.up_off); break;
+            case 1: CCMI_REF_BWD(1); break;
+            case 3: CCMI_REF_BWD(3); break;
+            case 5: CCMI_REF_BWD(5); break;
+            case 7: CCMI_REF_BWD(7); break;
+            default: CCMI_REF_BWD(9); break;
             }
-            hipLaunchKernelGGL(t_ref_gx, grid1(n, B), dim3(kT), 0, s, GU, pl.tmp_per, GY, gys, hd, wd, kf, g.kfull, koff,
-                               g.Kp, gq + g.off[k - 1], (int64_t)g.N);
+#undef CCMI_REF_BWD
+            (void)n;
         }
         // transposed-conv upsampling of the source stack: channels 1..C
         {
