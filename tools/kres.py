@@ -16,16 +16,23 @@ with tempfile.TemporaryDirectory() as td:
     subprocess.run([str(LLVM / "llvm-objdump"), "--offloading", str(lib)], cwd=td, check=True, capture_output=True)
     text = "".join(subprocess.run([str(LLVM / "llvm-readelf"), "--notes", str(f)], capture_output=True, text=True).stdout
                    for f in sorted(Path(td).glob("libccmi.so.*gfx950")))
-rows, name = {}, None
+rows, rec = {}, None
+KEYS = ("vgpr_count", "agpr_count", "sgpr_count", "vgpr_spill_count", "sgpr_spill_count", "private_segment_fixed_size",
+        "group_segment_fixed_size")
 for line in text.splitlines():
-    m = re.match(r"\s+\.name:\s+(\S+)", line)
-    if m:
-        name = m.group(1)
-        rows[name] = {}
+    # one kernel record per "  - ." list item; its own keys sit at 4 spaces (the args' deeper)
+    m = re.match(r"^  - \.(\w+):\s*(\S*)", line) or re.match(r"^    \.(\w+):\s*(\S*)", line)
+    if not m:
         continue
-    m = re.match(r"\s+\.(vgpr_count|agpr_count|sgpr_count|vgpr_spill_count|sgpr_spill_count|private_segment_fixed_size|group_segment_fixed_size):\s+(\d+)", line)
-    if m and name:
-        rows[name][m.group(1)] = int(m.group(2))
+    if line.startswith("  - "):
+        rec = {}
+    if rec is None:
+        continue
+    key, val = m.groups()
+    if key == "name":
+        rows[val] = rec
+    elif key in KEYS:
+        rec[key] = int(val)
 dem = subprocess.run(["c++filt"], input="\n".join(rows), capture_output=True, text=True).stdout.split("\n")
 pats = sys.argv[1:]
 for (k, v), d in zip(rows.items(), dem):
