@@ -93,7 +93,7 @@ def test_bench_reference_comparison_and_proxies():
     recs = [{"image": n, "lmbda": lm, "psnr_db": rows[(n, lm)]["psnr_db"], "rate_bpp": rows[(n, lm)]["rate_bpp"]}
             for n in ("kodim01", "kodim07") for lm in lms]
     c = bench.compare_with_reference(recs, lms)
-    assert c["bd_rate_images"] == 2 and abs(c["bd_rate_vs_reference_pct_mean"]) < 1e-6
+    assert c["bd_rate_images"] == 2 and abs(c["bd_rate_vs_results_tsv_on_proxies_pct_mean"]) < 1e-6
     for v in c["per_lambda"].values():
         assert v["psnr_db_mean"] == v["reference_psnr_db_mean"] and v["images"] == 2
 
