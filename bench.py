@@ -321,10 +321,18 @@ def cpu_baseline(inp, budget_s=12.0, max_frames=64):
         fo.post(r["syn"], 8, True)
         frames += 1
     dt = time.perf_counter() - t0
-    return {"value": round(frames * H * W / dt / 1e6, 3), "unit": "Mpixel/s", "cores": torch.get_num_threads(),
-            "kind": "port",
-            "sample": f"{frames} synthetic 1280x720 hop frames, full float forward + 420 post "
-                      f"(oracle/forward_oracle.py, torch fp32 CPU, {torch.get_num_threads()} threads), {dt:.1f} s"}
+    value = frames * H * W / dt / 1e6
+    out = {"value": round(value, 3), "unit": "Mpixel/s", "cores": torch.get_num_threads(),
+           "kind": "port",
+           "sample": f"{frames} synthetic 1280x720 hop frames, full float forward + 420 post "
+                     f"(oracle/forward_oracle.py, torch fp32 CPU, {torch.get_num_threads()} threads), {dt:.1f} s"}
+    # the port timed against the reference's own eval forward on one host
+    # (tests/golden/cpu_calibration.json "forward_720p", tools/gen_golden_rd.py calib_forward)
+    cal = json.loads((ROOT / "tests" / "golden" / "cpu_calibration.json").read_text()).get("forward_720p")
+    if cal:
+        out["port_over_reference_time"] = round(cal["port_s_per_frame"] / cal["reference_s_per_frame"], 3)
+        out["reference_equivalent_value"] = round(value * out["port_over_reference_time"], 3)
+    return out
 
 
 def _reduce(counters: dict, dist, dev, op="sum"):

@@ -301,6 +301,49 @@ def gen_calib(out_path: Path):
     out_path.write_text(json.dumps(res, indent=1))
 
 
+def gen_calib_forward(out_path: Path, threads: int):
+    """Per-frame CPU time of the reference's eval forward (FrameEncoder.forward after
+    set_to_eval(), the call of test.py:402-411 under test()'s no_grad: quantize, ARM + rate,
+    upsampling, synthesis, 8-bit rounding, 444 -> 420) against oracle/forward_oracle.py's
+    forward + post (bench.py's cpu_baseline) on the same 1280x720 hop frame, same threads.
+    Merged into out_path under "forward_720p" (BASELINE.md §3.3 calibration)."""
+    sys.path.insert(0, str(ROOT / "oracle"))
+    import forward_oracle as fo
+    torch.set_num_threads(threads)
+    H, W = 720, 1280
+    p = CoolChicEncoderParameter(layers_synthesis=list(HOP["layers"]), n_ft_per_res=[1] * 7, dim_arm=16,
+                                 n_hidden_layers_arm=2)
+    p.set_image_size((H, W))
+    torch.manual_seed(0)
+    fe = FrameEncoder(coolchic_encoder_param=p, frame_type="I", frame_data_type="yuv420", bitdepth=8)
+    fe.set_to_eval()
+    ts = []
+    with torch.no_grad():
+        for _ in range(4):
+            t0 = time.perf_counter()
+            fe.forward(reference_frames=[], quantizer_noise_type="none", quantizer_type="hardround", AC_MAX_VAL=-1,
+                       flag_additional_outputs=True)
+            ts.append(time.perf_counter() - t0)
+    ref_s = float(np.median(ts[1:]))
+    mp = fo.ModelParams.random(H, W, seed=0)
+    g = torch.Generator().manual_seed(0)
+    lats = [0.5 * torch.randn(h, w, generator=g) for h, w in mp.sizes]
+    ts = []
+    for _ in range(4):
+        t0 = time.perf_counter()
+        r = fo.forward(mp, lats)
+        fo.post(r["syn"], 8, True)
+        ts.append(time.perf_counter() - t0)
+    port_s = float(np.median(ts[1:]))
+    res = json.loads(out_path.read_text()) if out_path.exists() else {}
+    res["forward_720p"] = {"threads": threads, "reference_s_per_frame": ref_s, "port_s_per_frame": port_s,
+                           "port_over_reference": port_s / ref_s,
+                           "what": "reference FrameEncoder.forward eval (hardround, yuv420 8-bit) vs "
+                                   "oracle/forward_oracle.py forward + post, one 1280x720 hop frame, median of 3"}
+    print(res["forward_720p"], flush=True)
+    out_path.write_text(json.dumps(res, indent=1))
+
+
 def gen_bd(out_path: Path):
     """Golden vectors for the BD-rate restatement: the reference's own BD_RATE / BD_PSNR
     (coolchic/utils/bjontegaard_metric.py) on seeded curve pairs, both integration modes."""
@@ -343,3 +386,5 @@ if __name__ == "__main__":
         run_rd("c3x", GOLD / "rd_reference_c3x.json")
     if what in ("calib", "all"):
         gen_calib(GOLD / "cpu_calibration.json")
+    if what == "calib_forward":  # python tools/gen_golden_rd.py calib_forward THREADS
+        gen_calib_forward(GOLD / "cpu_calibration.json", int(sys.argv[2]) if len(sys.argv) > 2 else 2)
