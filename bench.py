@@ -340,6 +340,41 @@ def _reduce(counters: dict, dist, dev, op="sum"):
     return D.reduce_counters(counters, op=op, device=dev) if dist else dict(counters)
 
 
+def bench_single_stream_decode(cls: str = "E", reps: int = 2):
+    """Path B latency, the drop-in case: ccmi_decode_file (cc_decode_cpu's replacement, file in
+    -> .yuv out: parse, upload, kernels, download, write) on each shipped class-`cls` stream,
+    ONE stream at a time, best of `reps` wall-clock runs, md5 checked against the reference
+    decoder's.  Compared with the reference decoder on one core (122.2 ms mean
+    over the 15 class-E streams, 284.3 over the class-B ones, ccdec --avx2)."""
+    import ctypes
+    import hashlib
+    import statistics
+    import tempfile
+    import ccmi
+    md5 = json.loads((ROOT / "tests/golden/ref_md5.json").read_text())
+    files = sorted((ROOT / "tests/golden/cool").glob(f"{cls}-*.cool"))
+    L = ccmi.lib()
+    ms, exact = [], True
+    with tempfile.TemporaryDirectory() as td:
+        out = Path(td) / "o.yuv"
+        assert L.ccmi_decode_file(str(files[0]).encode(), str(out).encode(), 0, 0, 0, 0) == 0, ccmi.last_error()
+        for f in files:
+            best = None
+            for _ in range(reps):
+                t0 = time.perf_counter()
+                rc = L.ccmi_decode_file(str(f).encode(), str(out).encode(), 0, 0, 0, 0)
+                dt = time.perf_counter() - t0
+                assert rc == 0, ccmi.last_error()
+                best = dt if best is None else min(best, dt)
+            ms.append(best * 1e3)
+            exact &= hashlib.md5(out.read_bytes()).hexdigest() == md5["jvet/" + f.name]["md5"]
+    ref = {"E": 122.2, "B": 284.3}[cls]
+    return {"metric": "ccmi_decode_file wall ms per stream, one stream at a time (best of %d)" % reps,
+            "streams": len(files), "mean_ms": round(statistics.mean(ms), 2), "max_ms": round(max(ms), 2),
+            "min_ms": round(min(ms), 2), "reference_1core_mean_ms": ref,
+            "speedup_vs_reference_1core": round(ref / statistics.mean(ms), 3), "bit_exact_vs_reference_md5": exact}
+
+
 def bench_bitexact_decode(reps: int, cls: str = "E", H=H, W=W, rank=0, world=1, dist=None, dev=None):
     """Path B: the bit-exact HIP decoder on the shipped JVET class-`cls` .cool streams
     (class E: 15 files at 1280x720; class B: 5 committed files at 1920x1080).  The job is
@@ -727,6 +762,8 @@ def main():
         dec = bench_bitexact_decode(args.decode_reps, rank=rank, world=world, dist=dist, dev=dev)
         if rank == 0 and world == 1 and not args.no_cpu_baseline:
             dec["cpu_baseline"] = cpu_decode_baseline()
+        if rank == 0:  # latency: one stream at a time through the drop-in entry point
+            dec["single_stream"] = bench_single_stream_decode("E")
         res["bitexact_decode"] = dec
         res["bitexact_encode"] = bench_bitexact_encode(rank=rank, world=world, dist=dist, dev=dev)
     if args.hd_decode_reps > 0:

@@ -945,31 +945,38 @@ __global__ __launch_bounds__(64) void dec_arm_lat_kernel(const ArmStreamDesc *__
             const int32_t s1 = grp == 0 ? r1 : grp == 1 ? g0 : grp == 2 ? g1 : g2;
             const int32_t s2 = grp == 0 ? r2 : grp == 1 ? r1 : grp == 2 ? g0 : g1;
             const int32_t s3 = grp == 0 ? r3 : grp == 1 ? r2 : grp == 2 ? r1 : g0;
-            const bool f1 = w24 && !big;
-            int32_t acc = pf_a;
-            if (f1) acc += imul<true>(Ws[0], s3) + imul<true>(Ws[1], s2) + imul<true>(Ws[2], s1);
-            else acc += imul<false>(Ws[0], s3) + imul<false>(Ws[1], s2) + imul<false>(Ws[2], s1);
-            int32_t a = acc < 0 ? 0 : (acc + 128) >> 8;
+            // the multiplies' form fixed per instantiation: with a runtime select per product
+            // the compiler folded both forms into the quarter-rate v_mul_lo_u32
+            auto mlp = [&](auto F1, auto W24) {
+                constexpr bool f1 = decltype(F1)::value, f24 = decltype(W24)::value;
+                const int32_t acc = pf_a + imul<f1>(Ws[0], s3) + imul<f1>(Ws[1], s2) + imul<f1>(Ws[2], s1);
+                int32_t a = acc < 0 ? 0 : (acc + 128) >> 8;
 #pragma unroll
-            for (int l = 1; l < NH; ++l)
-                a = w24 ? arm_hidden_rows<D, true>(Wh[l], Bh[l], a) : arm_hidden_rows<D, false>(Wh[l], Bh[l], a);
-            const int32_t m_0 = row_sum16(w24 ? imul<true>(Wo0, a) : imul<false>(Wo0, a)) + bo0;
-            const int32_t m_1 = row_sum16(w24 ? imul<true>(Wo1, a) : imul<false>(Wo1, a)) + bo1;
+                for (int l = 1; l < NH; ++l) a = arm_hidden_rows<D, f24>(Wh[l], Bh[l], a);
+                return int2{row_sum16(imul<f24>(Wo0, a)) + bo0, row_sum16(imul<f24>(Wo1, a)) + bo1};
+            };
+            int2 ms;
+            if (w24 && !big) ms = mlp(std::true_type{}, std::true_type{});
+            else if (w24) ms = mlp(std::false_type{}, std::true_type{});
+            else ms = mlp(std::false_type{}, std::false_type{});
 #if defined(CCMI_ARM_STAMPS)
             __builtin_amdgcn_s_waitcnt(0);
 #endif
             STAMP(t1);
-            // mu / scale -> context-table entry (lane 16 g + 15 holds row g's sums)
-            const int32_t mu = m_0 < 0 ? -((-m_0 + 128) >> 8) : (m_0 + 128) >> 8;
-            const int32_t ls = m_1 < 0 ? -((-m_1 + 128) >> 8) : (m_1 + 128) >> 8;
+            // mu / scale -> context-table entry (lane 16 g + 15 holds row g's sums).  The
+            // reference's symmetric rounding m < 0 ? -((-m + 128) >> 8) : (m + 128) >> 8 equals
+            // (m + 127 + [m >= 0]) >> 8 (arithmetic shift; |m| < 2^31 - 128): branch-free, where the
+            // ternary form compiled to exec-mask branches
+            auto rnd8 = [](int32_t m) { return (m + 128 + (m >> 31)) >> 8; };
+            const int32_t mu = rnd8(ms.x);
+            const int32_t ls = rnd8(ms.y);
             // get_val_mu_indicies (cc-contexts.h:20-48)
-            const int32_t mr = mu >= 0 ? ((mu + 128) >> 8) << 8 : -(((-mu + 128) >> 8) << 8);
-            int32_t mi = (mu - mr) * 16;
-            mi = (mi >= 0 ? (mi + 128) >> 8 : -((-mi + 128) >> 8)) + 8;
+            const int32_t mr = rnd8(mu) << 8;
+            const int32_t mi = rnd8((mu - mr) * 16) + 8; // in [0, 16]
+            // (lsp * 5 + 128) >> 8 is <= 0 for every lsp < 0, so one clamp covers both bounds
             const int32_t lsp = ls + 256;
-            int32_t si = lsp < 0 ? 0 : (lsp * 5 + 128) >> 8;
-            si = si > 49 ? 49 : si;
-            const uint2 e = *reinterpret_cast<const uint2 *>(ctab + (uint32_t)(mi * 50 + si) * 2u);
+            const int32_t si = min(max((lsp * 4 + lsp + 128) >> 8, 0), 49);
+            const uint2 e = *reinterpret_cast<const uint2 *>(ctab + (uint32_t)(__mul24(mi, 50) + si) * 2u);
             // the next pass starts at x + nd, nd = 1 .. kSpec: its above-row sums for every nd
             int32_t nxt[kSpec];
 #pragma unroll
@@ -978,7 +985,7 @@ __global__ __launch_bounds__(64) void dec_arm_lat_kernel(const ArmStreamDesc *__
                 nxt[k - 1] = pre[(((xg >> 6) & 1) * kChunk + (xg & 63)) * 16 + o];
             }
             const int32_t up_nxt = up[x + (lane & 7)]; // lane i: above x + i; the next pass reads lanes nd .. nd + 2
-            const uint32_t pk = (uint32_t)(mr >> 8) << 8 | e.y; // mu rounded, sign-bin state
+            const uint32_t pk = (uint32_t)mr | e.y; // mu rounded (a multiple of 256), sign-bin state
             STAMP(t2);
             // decode_single (cc-bac.h:192-231), in order, until the first non-zero latent
             int nd = 0;

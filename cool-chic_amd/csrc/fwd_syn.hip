@@ -204,10 +204,24 @@ __global__ __launch_bounds__(kFThreads) __attribute__((amdgpu_waves_per_eu(fused
     const float *in = A.in + (int64_t)b * A.in_stride;
     float *out = A.out + (int64_t)b * A.out_stride;
     const int64_t plane = (int64_t)A.H * A.W;
-    const int c = threadIdx.x & (kRW - 1);
-    const int rb = (threadIdx.x >> 6) * NR; // first window row of this thread
-    const int gx = ox + c;
-    const int cxg = clampi(gx, A.W - 1);
+    // lane-derived indices; re-derived after the head (below) so that they are not live
+    // across it: held there they were the kernel's 5 spilled VGPRs (scratch traffic
+    // in every wave)
+    int c = threadIdx.x & (kRW - 1);
+    int rb = (threadIdx.x >> 6) * NR; // first window row of this thread
+    int gx = ox + c;
+    int cxg = clampi(gx, A.W - 1);
+    int lx[3]; // 3x3 stage: window columns of the clamped horizontal neighbours
+    auto reidx = [&]() {
+        int t = threadIdx.x;
+        asm volatile("" : "+v"(t)); // an opaque copy: the compiler cannot reuse the old values
+        c = t & (kRW - 1);
+        rb = (t >> 6) * NR;
+        gx = ox + c;
+        cxg = clampi(gx, A.W - 1);
+#pragma unroll
+        for (int d = 0; d < 3; ++d) lx[d] = clampi(cxg + d - 1, A.W - 1) - ox;
+    };
 
     const float *lut8 = A.qmax == 255.f ? s_lut8 : nullptr;
     // per-frame tables in LDS: the 8-bit output quotients (own area, staged at once) and the
@@ -655,6 +669,7 @@ __global__ __launch_bounds__(kFThreads) __attribute__((amdgpu_waves_per_eu(fused
             }
         }
         FSTAMP(3);
+        reidx();
         if (halo == 0) {
 #pragma unroll
             for (int p = 0; p < NR; ++p) {
@@ -678,10 +693,8 @@ __global__ __launch_bounds__(kFThreads) __attribute__((amdgpu_waves_per_eu(fused
     // edge rows again one row further out (the only out-of-image rows an in-image output
     // reads).  So the vertical neighbours of window row r are simply rows r-1, r+1, and a
     // thread reads row pairs {r, r+1} straight into packed registers.  Columns are lanes:
-    // the horizontal neighbours use clamped columns lx[].
-    int lx[3];
-#pragma unroll
-    for (int d = 0; d < 3; ++d) lx[d] = clampi(cxg + d - 1, A.W - 1) - ox;
+    // the horizontal neighbours use clamped columns lx[].  Each layer and the store pass
+    // re-derive the lane indices (reidx) instead of holding them across the layers.
     // windows whose rows all lie strictly inside the image write no replicate rows
     const bool inner = oy > 0 && oy + kRH < A.H;
     // one 3x3 layer from buf(cur) into buf(cur ^ 1); the last one also lands in LDS (each
@@ -690,6 +703,7 @@ __global__ __launch_bounds__(kFThreads) __attribute__((amdgpu_waves_per_eu(fused
     auto layer = [&](auto LAST, int s, int cur) {
         constexpr bool last = decltype(LAST)::value;
         __syncthreads();
+        reidx();
         const cfloat_ptr wt = prm + A.sp[s].w_off;
         const cfloat_ptr bs = prm + A.sp[s].b_off;
         const f2 lo = f2(A.sp[s].relu ? 0.f : -INFINITY);
@@ -753,6 +767,7 @@ __global__ __launch_bounds__(kFThreads) __attribute__((amdgpu_waves_per_eu(fused
     // stores: this thread's own pixels of the last layer, back from LDS (program order, no
     // barrier), one branch-free loop per output format
     {
+        reidx();
         const int t = A.n_sp;
         const float *fin = &buf(cur)[0][0] + (rb + 1) * kRW + c;
         const bool col_ok = c >= t && c < kRW - t && gx < A.W;

@@ -24,9 +24,11 @@
 //   t_loss        train-mode output (420 nearest, clamp), MSE and its gradient
 //   t_sp_gpre / t_sp_bwd    3x3 layers backward (replicate-padding adjoint as a gather)
 //   t_head_bwd    1x1 head backward; weight gradients reduced through LDS
-//   t_ref_* / t_up_*        upsampling backward, one pyramid level at a time
+//   t_ref_bwd / t_up_bwd    upsampling backward, one launch each per pyramid level
 //   t_latgrad, t_sumsq, t_adam   dL/dy, global grad norm, clipped Adam update
 #include <stdlib.h>
+
+#include <cmath>
 
 #include "fwd_common.h"
 
@@ -104,10 +106,35 @@ struct SoftRound {
         const float fx = floorf(x), th = tanhf((x - fx - 0.5f) / t);
         return 0.5f * (1.f - th * th) / t * inv;
     }
+    // f(x) and df(x) from one tanh (the same expressions as f / df)
+    __device__ void fdf(float x, float &y, float &d) const
+    {
+        const float fx = floorf(x), th = tanhf((x - fx - 0.5f) / t);
+        y = fx + 0.5f * th * inv + 0.5f;
+        d = 0.5f * (1.f - th * th) / t * inv;
+    }
 };
 
-__global__ void t_quant(const float *__restrict__ lat, int64_t ls, int N, float gain, int qt, int nz, float temp,
-                        float nprm, uint64_t seed, int step, const float *__restrict__ noise_in, float *__restrict__ yq,
+// Quantiser constants, uniform over the launch (computed once on the host): softround
+// temperature and 1 / tanh(1 / 2t); kumaraswamy a, 1 / a and 1 / b (quantizer.py:60-102)
+struct QuantArgs {
+    float temp, inv, ka_inv, kb_inv, nprm;
+};
+
+QuantArgs quant_args(float temp, float nprm)
+{
+    QuantArgs q{temp, 0.f, 0.f, 0.f, nprm};
+    if (temp > 0.f) q.inv = 1.f / std::tanh(1.f / (2.f * temp));
+    if (nprm > 0.f) {
+        const float a = nprm, b = (std::exp2(a) * (a - 1.f) + 1.f) / a;
+        q.ka_inv = 1.f / a;
+        q.kb_inv = 1.f / b;
+    }
+    return q;
+}
+
+__global__ void t_quant(const float *__restrict__ lat, int64_t ls, int N, float gain, int qt, int nz, QuantArgs Q,
+                        uint64_t seed, int step, const float *__restrict__ noise_in, float *__restrict__ yq,
                         float *__restrict__ dq, float *__restrict__ gq)
 {
     const int b = blockIdx.y, i = blockIdx.x * kT + threadIdx.x;
@@ -120,23 +147,26 @@ __global__ void t_quant(const float *__restrict__ lat, int64_t ls, int N, float 
     } else if (nz != CCMI_NOISE_NONE) {
         const uint64_t r = mix64(seed ^ mix64(((uint64_t)step << 40) ^ ((uint64_t)b << 32) ^ (uint64_t)i));
         const float u1 = unif(r);
-        if (nz == CCMI_NOISE_KUMARASWAMY) { // generate_kumaraswamy_noise (quantizer.py:60-102)
-            const float a = nprm, bb = (exp2f(a) * (a - 1.f) + 1.f) / a;
-            n = powf(1.f - powf(1.f - u1, 1.f / bb), 1.f / a) - 0.5f;
+        if (nz == CCMI_NOISE_KUMARASWAMY) { // generate_kumaraswamy_noise: (1 - (1 - u)^(1/b))^(1/a) - 1/2
+            // powers through v_log_f32 / v_exp_f32 (u1 in (0, 1): both bases in (0, 1]); the
+            // draw only has to follow the distribution, parity tests pass their noise in
+            const float p = exp2f(__log2f(1.f - u1) * Q.kb_inv);
+            n = exp2f(__log2f(1.f - p) * Q.ka_inv) - 0.5f;
         } else { // gaussian: Box-Muller
             const float u2 = unif(mix64(r + 0x632BE59BD9B4E019ull));
-            n = sqrtf(-2.f * logf(u1)) * cospif(2.f * u2) * nprm;
+            n = sqrtf(-2.f * logf(u1)) * cospif(2.f * u2) * Q.nprm;
         }
     }
-    SoftRound s{temp, 1.f / tanhf(1.f / (2.f * temp))};
+    const SoftRound s{Q.temp, Q.inv};
     float y, d;
     switch (qt) {
     case CCMI_Q_NONE: y = x + n; d = 1.f; break;
-    case CCMI_Q_SOFTROUND_ALONE: y = s.f(x); d = s.df(x); break;
+    case CCMI_Q_SOFTROUND_ALONE: s.fdf(x, y, d); break;
     case CCMI_Q_SOFTROUND: {
-        const float u = s.f(x) + n;
-        y = s.f(u);
-        d = s.df(u) * s.df(x);
+        float fx, dx, du;
+        s.fdf(x, fx, dx);
+        s.fdf(fx + n, y, du);
+        d = du * dx;
         break;
     }
     case CCMI_Q_STE: y = rintf(x); d = s.df(x); break;
@@ -1393,11 +1423,25 @@ __global__ __launch_bounds__(kT) void t_ref_bwd(const float *__restrict__ GY, in
 #pragma unroll
     for (int k = 0; k < KP; ++k) wv[k] = wk[k];
     const float *xb = X + (int64_t)b * xs, *gb = GY + (int64_t)b * gys;
-    for (int i = tid; i < SY * SX; i += kT) {
-        const int r = i / SX, c = i - r * SX, y = ty0 - P + r, x = tx0 - P + c;
-        const bool in = y >= 0 && y < h && x >= 0 && x < w;
-        sx[r][c] = in ? xb[(int64_t)y * w + x] : 0.f;
-        sg[r][c] = in ? gb[(int64_t)y * w + x] : 0.f;
+    {
+        // every load of a thread in flight before its LDS stores
+        constexpr int NL = (SY * SX + kT - 1) / kT;
+        float vx[NL], vg[NL];
+#pragma unroll
+        for (int k = 0; k < NL; ++k) {
+            const int i = tid + k * kT, r = i / SX, c = i - r * SX, y = ty0 - P + r, x = tx0 - P + c;
+            const bool in = i < SY * SX && y >= 0 && y < h && x >= 0 && x < w;
+            vx[k] = in ? xb[(int64_t)y * w + x] : 0.f;
+            vg[k] = in ? gb[(int64_t)y * w + x] : 0.f;
+        }
+#pragma unroll
+        for (int k = 0; k < NL; ++k) {
+            const int i = tid + k * kT;
+            if (i < SY * SX) {
+                (&sx[0][0])[i] = vx[k];
+                (&sg[0][0])[i] = vg[k];
+            }
+        }
     }
     __syncthreads();
     for (int i = tid; i < SY * TX; i += kT) { // U rows ty0 - P .. ty0 + TY + P - 1
@@ -1515,94 +1559,6 @@ __global__ void t_up_gs(const float *__restrict__ GU, int64_t us, UpLevel A, con
 // upsample kernel gradient: vertical taps over destination row pairs (c, j, xd),
 // horizontal taps over destination column pairs (c, r, j); taps are compile-time per
 // parity: destination 2j + a, source offset d -> tap a + K/2 - 1 - 2d.
-// Compile-time-tap forms of the two upsampling adjoints for the reference's 8-tap kernel:
-// interior rows / columns (every source tap inside the stack, no clamping) take a fixed
-// unrolled sum in the generic kernel's summation order (d ascending, then parity), the
-// borders fall back to the generic loops -- same results, no runtime tap loops.
-template <int K>
-__global__ void t_up_gu_k(const float *__restrict__ GY, int64_t gys, UpLevel A, const float *__restrict__ kf, int kstride,
-                          int koff, float *__restrict__ GU, int64_t us)
-{
-    constexpr int K2 = K / 2, DLO = -((K2 + 1) / 2), DHI = K2 / 2;
-    const int b = blockIdx.y;
-    const int n = A.C * A.hs * A.wd, i = blockIdx.x * kT + threadIdx.x;
-    if (i >= n) return;
-    const int cr = i / A.wd, xd = i - cr * A.wd;
-    const int c = cr / A.hs, r = cr - c * A.hs;
-    const float *wk = kf + (int64_t)b * kstride + koff;
-    float w[K];
-#pragma unroll
-    for (int t = 0; t < K; ++t) w[t] = wk[t];
-    const float *gy = GY + (int64_t)b * gys + (int64_t)(c + 1) * A.hd * A.wd + xd;
-    const int nj = (A.hd + 1) >> 1;
-    float acc = 0.f;
-    if (r >= 1 && r <= A.hs - 2 && r - DHI >= 0 && r - DLO <= nj - 1 && 2 * (r - DLO) + 1 < A.hd) {
-#pragma unroll
-        for (int d = DLO; d <= DHI; ++d)
-#pragma unroll
-            for (int a = 0; a < 2; ++a) {
-                const int t = a + K2 - 1 - 2 * d;
-                if (t >= 0 && t < K) acc = fmaf(w[t], gy[(int64_t)(2 * (r - d) + a) * A.wd], acc);
-            }
-    } else {
-        for (int d = DLO; d <= DHI; ++d) {
-            int jlo = r == 0 ? 0 : r - d, jhi = r == A.hs - 1 ? nj - 1 : r - d;
-            jlo = max(jlo, 0);
-            jhi = min(jhi, nj - 1);
-            for (int j = jlo; j <= jhi; ++j) {
-                if (clampi(j + d, A.hs - 1) != r) continue;
-                for (int a = 0; a < 2; ++a) {
-                    const int yd = 2 * j + a, t = up_tap(a, d, K);
-                    if (yd < A.hd && t >= 0 && t < K) acc = fmaf(w[t], gy[(int64_t)yd * A.wd], acc);
-                }
-            }
-        }
-    }
-    GU[(int64_t)b * us + i] = acc;
-}
-
-template <int K>
-__global__ void t_up_gs_k(const float *__restrict__ GU, int64_t us, UpLevel A, const float *__restrict__ kf, int kstride,
-                          int koff, float *__restrict__ GS, int64_t gss, int accumulate)
-{
-    constexpr int K2 = K / 2, DLO = -((K2 + 1) / 2), DHI = K2 / 2;
-    const int b = blockIdx.y;
-    const int n = A.C * A.hs * A.ws, i = blockIdx.x * kT + threadIdx.x;
-    if (i >= n) return;
-    const int cr = i / A.ws, m = i - cr * A.ws;
-    const float *wk = kf + (int64_t)b * kstride + koff;
-    float w[K];
-#pragma unroll
-    for (int t = 0; t < K; ++t) w[t] = wk[t];
-    const float *gu = GU + (int64_t)b * us + cr * A.wd;
-    const int nj = (A.wd + 1) >> 1;
-    float acc = 0.f;
-    if (m >= 1 && m <= A.ws - 2 && m - DHI >= 0 && m - DLO <= nj - 1 && 2 * (m - DLO) + 1 < A.wd) {
-#pragma unroll
-        for (int d = DLO; d <= DHI; ++d)
-#pragma unroll
-            for (int a = 0; a < 2; ++a) {
-                const int t = a + K2 - 1 - 2 * d;
-                if (t >= 0 && t < K) acc = fmaf(w[t], gu[2 * (m - d) + a], acc);
-            }
-    } else {
-        for (int d = DLO; d <= DHI; ++d) {
-            int jlo = m == 0 ? 0 : m - d, jhi = m == A.ws - 1 ? nj - 1 : m - d;
-            jlo = max(jlo, 0);
-            jhi = min(jhi, nj - 1);
-            for (int j = jlo; j <= jhi; ++j) {
-                if (clampi(j + d, A.ws - 1) != m) continue;
-                for (int a = 0; a < 2; ++a) {
-                    const int xd = 2 * j + a, t = up_tap(a, d, K);
-                    if (xd < A.wd && t >= 0 && t < K) acc = fmaf(w[t], gu[xd], acc);
-                }
-            }
-        }
-    }
-    float *o = GS + (int64_t)b * gss + i;
-    *o = accumulate ? *o + acc : acc;
-}
-
 template <int K>
 __global__ __launch_bounds__(kT) void t_up_dw(const float *__restrict__ GY, int64_t gys, const float *__restrict__ U,
                                               const float *__restrict__ GU, int64_t us, const float *__restrict__ S,
@@ -1648,6 +1604,173 @@ __global__ __launch_bounds__(kT) void t_up_dw(const float *__restrict__ GY, int6
         }
     }
     reduce_taps<K>(dw, gth + ((int64_t)b * kDwSlots + blockIdx.x % kDwSlots) * gstride + hoff);
+}
+
+// Upsampling backward of one pyramid step in ONE launch (formerly t_up_u, t_up_gu, t_up_dw
+// and t_up_gs with compile-time taps, with the [C][hs][wd] temporaries U and GU through HBM).  A workgroup owns
+// source rows [r0, r0 + TR) x destination columns [x0, x0 + TX) of one channel.  It stages
+// in LDS the clamped source rows r0 + DLO .. r0 + TR - 1 + DHI (columns m0 + DLO .. m0 + TM - 1
+// + DHI, m0 = x0 / 2) and the destination-gradient rows 2 (r0 - DHI) .. 2 (r0 + TR - 1 - DLO) + 1
+// with 2 DHI halo columns on each side (zero outside the level), forms
+//   U  = horizontal pass of S        rows r0 + DLO .. r0 + TR - 1 + DHI, the tile's columns;
+//   GU = vertical adjoint of GY      rows r0 .. r0 + TR - 1, the tile's columns + halo;
+// and emits GS (horizontal adjoint of GU) for its TM source columns and the tap-gradient
+// partial sums (GY x U, GU x S) of its destination positions.  Border rows / columns take
+// the generic clamped-gather loops of t_up_gu / t_up_gs over the staged tiles.
+template <int K>
+__global__ __launch_bounds__(kT) void t_up_bwd(const float *__restrict__ GY, int64_t gys, const float *__restrict__ S,
+                                               int64_t ss, UpLevel A, const float *__restrict__ kf, int kstride, int koff,
+                                               float *__restrict__ GS, int64_t gss, int accumulate,
+                                               float *__restrict__ slots, int64_t gstride, int hoff, int tiles_x,
+                                               int tiles_y)
+{
+    constexpr int K2 = K / 2, DLO = -((K2 + 1) / 2), DHI = K2 / 2, DW = DHI - DLO;
+    constexpr int TR = 16, TX = 64, TM = TX / 2;
+    constexpr int SR = TR + DW, SC = TM + DW; // staged source tile
+    constexpr int GR = 2 * (TR + DW), GC = TX + 2 * DW; // staged GY tile (GU has GC columns too)
+    __shared__ float s_s[SR][SC], s_u[SR][TX], s_gy[GR][GC], s_gu[TR][GC];
+    const int b = blockIdx.y, tid = threadIdx.x;
+    const int tile = blockIdx.x % (tiles_x * tiles_y), c = blockIdx.x / (tiles_x * tiles_y);
+    const int r0 = (tile / tiles_x) * TR, x0 = (tile % tiles_x) * TX, m0 = x0 / 2;
+    const int gy0 = 2 * (r0 - DHI), gx0 = x0 - 2 * DHI; // GY / GU tile origin
+    const int hs = A.hs, ws = A.ws, hd = A.hd, wd = A.wd;
+    const int njy = (hd + 1) >> 1, njx = (wd + 1) >> 1;
+    float w[K];
+    {
+        const float *wk = kf + (int64_t)b * kstride + koff;
+#pragma unroll
+        for (int t = 0; t < K; ++t) w[t] = wk[t];
+    }
+    const float *sb = S + (int64_t)b * ss + (int64_t)c * hs * ws;
+    const float *gb = GY + (int64_t)b * gys + (int64_t)(c + 1) * hd * wd; // channel c + 1 of the dest stack
+    // staging: every load of a thread issued before its LDS stores (a load-store pair per
+    // loop iteration paid one memory latency per element)
+    {
+        constexpr int NS = (SR * SC + kT - 1) / kT, NG = (GR * GC + kT - 1) / kT;
+        float vs[NS], vg[NG];
+#pragma unroll
+        for (int k = 0; k < NS; ++k) {
+            const int i = tid + k * kT, r = i / SC, q = i - r * SC;
+            vs[k] = i < SR * SC ? sb[(int64_t)clampi(r0 + DLO + r, hs - 1) * ws + clampi(m0 + DLO + q, ws - 1)] : 0.f;
+        }
+#pragma unroll
+        for (int k = 0; k < NG; ++k) {
+            const int i = tid + k * kT, r = i / GC, q = i - r * GC, y = gy0 + r, x = gx0 + q;
+            vg[k] = (i < GR * GC && y >= 0 && y < hd && x >= 0 && x < wd) ? gb[(int64_t)y * wd + x] : 0.f;
+        }
+#pragma unroll
+        for (int k = 0; k < NS; ++k) {
+            const int i = tid + k * kT;
+            if (i < SR * SC) (&s_s[0][0])[i] = vs[k];
+        }
+#pragma unroll
+        for (int k = 0; k < NG; ++k) {
+            const int i = tid + k * kT;
+            if (i < GR * GC) (&s_gy[0][0])[i] = vg[k];
+        }
+    }
+    __syncthreads();
+    // U: destination column x0 + q reads source columns m0 + (q >> 1) + d
+    for (int i = tid; i < SR * TX; i += kT) {
+        const int r = i / TX, q = i - r * TX, a = q & 1;
+        float acc = 0.f;
+#pragma unroll
+        for (int d = DLO; d <= DHI; ++d) {
+            const int t = a + K2 - 1 - 2 * d;
+            if (t >= 0 && t < K) acc = fmaf(w[t], s_s[r][(q >> 1) + d - DLO], acc);
+        }
+        s_u[r][q] = acc;
+    }
+    // GU at source row r0 + tr, destination column gx0 + q
+    for (int i = tid; i < TR * GC; i += kT) {
+        const int tr = i / GC, q = i - tr * GC, r = r0 + tr, x = gx0 + q;
+        float acc = 0.f;
+        if (r < hs && x >= 0 && x < wd) {
+            if (r >= 1 && r <= hs - 2 && r - DHI >= 0 && r - DLO <= njy - 1 && 2 * (r - DLO) + 1 < hd) {
+#pragma unroll
+                for (int d = DLO; d <= DHI; ++d)
+#pragma unroll
+                    for (int a = 0; a < 2; ++a) {
+                        const int t = a + K2 - 1 - 2 * d;
+                        if (t >= 0 && t < K) acc = fmaf(w[t], s_gy[2 * (tr - d + DHI) + a][q], acc);
+                    }
+            } else {
+                for (int d = DLO; d <= DHI; ++d) {
+                    int jlo = r == 0 ? 0 : r - d, jhi = r == hs - 1 ? njy - 1 : r - d;
+                    jlo = max(jlo, 0);
+                    jhi = min(jhi, njy - 1);
+                    for (int j = jlo; j <= jhi; ++j) {
+                        if (clampi(j + d, hs - 1) != r) continue;
+                        for (int a = 0; a < 2; ++a) {
+                            const int yd = 2 * j + a, t = up_tap(a, d, K);
+                            if (yd < hd && t >= 0 && t < K) acc = fmaf(w[t], s_gy[yd - gy0][q], acc);
+                        }
+                    }
+                }
+            }
+        }
+        s_gu[tr][q] = acc;
+    }
+    __syncthreads();
+    // GS at source row r0 + tr, column m0 + mm
+    float *gsb = GS + (int64_t)b * gss + (int64_t)c * hs * ws;
+    for (int i = tid; i < TR * TM; i += kT) {
+        const int tr = i / TM, mm = i - tr * TM, r = r0 + tr, m = m0 + mm;
+        if (r >= hs || m >= ws) continue;
+        float acc = 0.f;
+        if (m >= 1 && m <= ws - 2 && m - DHI >= 0 && m - DLO <= njx - 1 && 2 * (m - DLO) + 1 < wd) {
+#pragma unroll
+            for (int d = DLO; d <= DHI; ++d)
+#pragma unroll
+                for (int a = 0; a < 2; ++a) {
+                    const int t = a + K2 - 1 - 2 * d;
+                    if (t >= 0 && t < K) acc = fmaf(w[t], s_gu[tr][2 * (mm - d + DHI) + a], acc);
+                }
+        } else {
+            for (int d = DLO; d <= DHI; ++d) {
+                int jlo = m == 0 ? 0 : m - d, jhi = m == ws - 1 ? njx - 1 : m - d;
+                jlo = max(jlo, 0);
+                jhi = min(jhi, njx - 1);
+                for (int j = jlo; j <= jhi; ++j) {
+                    if (clampi(j + d, ws - 1) != m) continue;
+                    for (int a = 0; a < 2; ++a) {
+                        const int xd = 2 * j + a, t = up_tap(a, d, K);
+                        if (xd < wd && t >= 0 && t < K) acc = fmaf(w[t], s_gu[tr][xd - gx0], acc);
+                    }
+                }
+            }
+        }
+        float *o = gsb + (int64_t)r * ws + m;
+        *o = accumulate ? *o + acc : acc;
+    }
+    // tap gradients: vertical use (GY x U at the tile's destination rows), horizontal use
+    // (GU x S at the tile's source rows)
+    float dw[K];
+#pragma unroll
+    for (int k = 0; k < K; ++k) dw[k] = 0.f;
+    for (int i = tid; i < 2 * TR * TX; i += kT) {
+        const int ty = i / TX, q = i - ty * TX;
+        if (2 * r0 + ty >= hd || x0 + q >= wd) continue;
+        const float g = s_gy[ty + 2 * DHI][q + 2 * DHI];
+        const int a = ty & 1;
+#pragma unroll
+        for (int d = DLO; d <= DHI; ++d) {
+            const int t = a + K2 - 1 - 2 * d;
+            if (t >= 0 && t < K) dw[t] = fmaf(g, s_u[(ty >> 1) + d - DLO][q], dw[t]);
+        }
+    }
+    for (int i = tid; i < TR * TX; i += kT) {
+        const int tr = i / TX, q = i - tr * TX;
+        if (r0 + tr >= hs || x0 + q >= wd) continue;
+        const float g = s_gu[tr][q + 2 * DHI];
+        const int a = q & 1;
+#pragma unroll
+        for (int d = DLO; d <= DHI; ++d) {
+            const int t = a + K2 - 1 - 2 * d;
+            if (t >= 0 && t < K) dw[t] = fmaf(g, s_s[tr - DLO][(q >> 1) + d - DLO], dw[t]);
+        }
+    }
+    reduce_taps<K>(dw, slots + ((int64_t)b * kDwSlots + blockIdx.x % kDwSlots) * gstride + hoff);
 }
 
 // ------------------------------------------------------------------ latents, norm, Adam
@@ -1961,7 +2084,8 @@ extern "C" int ccmi_quantize_f32(const float *x, int64_t n, int quantizer, float
     if (n == 0) return CCMI_OK;
     // noise comes as a tensor (or none): the counter-based generator is not used here
     hipLaunchKernelGGL(t_quant, grid1(n, 1), dim3(kT), 0, static_cast<hipStream_t>(stream), x, (int64_t)n, (int)n, 1.f,
-                       quantizer, (int)CCMI_NOISE_NONE, temperature, 1.f, (uint64_t)0, 0, noise, y, dy, (float *)nullptr);
+                       quantizer, (int)CCMI_NOISE_NONE, quant_args(temperature, 1.f), (uint64_t)0, 0, noise, y, dy,
+                       (float *)nullptr);
     CCMI_HIP_CHECK(hipGetLastError());
     return CCMI_OK;
 }
@@ -2022,7 +2146,8 @@ extern "C" int ccmi_train_step(const ccmi_train_args *a, void *stream)
     // ---- forward
     hipLaunchKernelGGL(t_expand, grid1(g.kfull, B), dim3(kT), 0, s, a->params, a->param_stride, g, kf);
     hipLaunchKernelGGL(t_quant, grid1(g.N, B), dim3(kT), 0, s, a->latent, a->latent_stride, g.N, a->gain, a->quantizer,
-                       a->noise, a->temperature, a->noise_param, (uint64_t)a->seed, a->step, a->noise_in, yq, dq, gq);
+                       a->noise, quant_args(a->temperature, a->noise_param), (uint64_t)a->seed, a->step, a->noise_in, yq,
+                       dq, gq);
     {
         // persistent over the latent tiles: about one resident wave of workgroups for the batch
         dim3 grid((unsigned)std::max(1, std::min(pl.nblk_arm, 2048 / B)), B);
@@ -2154,26 +2279,27 @@ extern "C" int ccmi_train_step(const ccmi_train_args *a, void *stream)
             }
             const int koff = A.sidx * g.K;
             const int hoff = g.up_off + A.sidx * g.hu;
+            float *GSd = (k == g.L - 1) ? gq + g.off[k] : gst + pl.gstack_off[k];
+            const int64_t gss = (k == g.L - 1) ? (int64_t)g.N : pl.gstack_per;
+            if (g.K == 8 && A.d_lo == -2 && A.d_hi == 2) {
+                // the whole step in one launch (16 source rows x 64 destination columns per tile)
+                const int tx = ccmi_div_up(wd, 64), ty = ccmi_div_up(A.hs, 16);
+                hipLaunchKernelGGL(t_up_bwd<8>, dim3((unsigned)(tx * ty * C), B), dim3(kT), 0, s, GY, gys, S, ss, A, kf,
+                                   g.kfull, koff, GSd, gss, k == g.L - 1 ? 1 : 0, slots, (int64_t)nreg, hoff - g.up_off, tx,
+                                   ty);
+                continue;
+            }
             const int64_t nu = (int64_t)C * A.hs * wd;
             hipLaunchKernelGGL(t_up_u, grid1(nu, B), dim3(kT), 0, s, S, ss, A, kf, g.kfull, koff, U, pl.tmp_per);
-            if (g.K == 8 && A.d_lo == -2 && A.d_hi == 2)
-                hipLaunchKernelGGL(t_up_gu_k<8>, grid1(nu, B), dim3(kT), 0, s, GY, gys, A, kf, g.kfull, koff, GU, pl.tmp_per);
-            else
-                hipLaunchKernelGGL(t_up_gu, grid1(nu, B), dim3(kT), 0, s, GY, gys, A, kf, g.kfull, koff, GU, pl.tmp_per);
+            hipLaunchKernelGGL(t_up_gu, grid1(nu, B), dim3(kT), 0, s, GY, gys, A, kf, g.kfull, koff, GU, pl.tmp_per);
             const dim3 gr(dw_blocks((int64_t)C * hd * wd, 8), B); // measured: 8 items per thread beat 1 here
             switch (g.K) {
             case 4: hipLaunchKernelGGL(t_up_dw<4>, gr, dim3(kT), 0, s, GY, gys, U, GU, pl.tmp_per, S, ss, A, slots, (int64_t)nreg, hoff - g.up_off); break;
             case 6: hipLaunchKernelGGL(t_up_dw<6>, gr, dim3(kT), 0, s, GY, gys, U, GU, pl.tmp_per, S, ss, A, slots, (int64_t)nreg, hoff - g.up_off); break;
             default: hipLaunchKernelGGL(t_up_dw<8>, gr, dim3(kT), 0, s, GY, gys, U, GU, pl.tmp_per, S, ss, A, slots, (int64_t)nreg, hoff - g.up_off); break;
             }
-            float *GSd = (k == g.L - 1) ? gq + g.off[k] : gst + pl.gstack_off[k];
-            const int64_t gss = (k == g.L - 1) ? (int64_t)g.N : pl.gstack_per;
-            if (g.K == 8 && A.d_lo == -2 && A.d_hi == 2)
-                hipLaunchKernelGGL(t_up_gs_k<8>, grid1((int64_t)C * A.hs * A.ws, B), dim3(kT), 0, s, GU, pl.tmp_per, A, kf,
-                                   g.kfull, koff, GSd, gss, k == g.L - 1 ? 1 : 0);
-            else
-                hipLaunchKernelGGL(t_up_gs, grid1((int64_t)C * A.hs * A.ws, B), dim3(kT), 0, s, GU, pl.tmp_per, A, kf,
-                                   g.kfull, koff, GSd, gss, k == g.L - 1 ? 1 : 0);
+            hipLaunchKernelGGL(t_up_gs, grid1((int64_t)C * A.hs * A.ws, B), dim3(kT), 0, s, GU, pl.tmp_per, A, kf, g.kfull,
+                               koff, GSd, gss, k == g.L - 1 ? 1 : 0);
         }
     }
     CCMI_HIP_CHECK(hipGetLastError());

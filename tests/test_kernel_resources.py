@@ -17,11 +17,13 @@ LLVM = Path("/opt/rocm/lib/llvm/bin")
 
 # demangled-name prefix -> (max VGPRs, max VGPR spills, scratch bytes allowed)
 BUDGET = {
-    # path A fused decode, 7 grids: three workgroups per CU need <= 80 VGPRs (6 waves / SIMD);
-    # the allocator spills a few values across the channel-group phases (measured: 3 resident
-    # workgroups 0.79 ms vs 2 resident 0.85 ms per 32 frames, tools/occ_probe.sh)
-    "syn_fused_kernel<7, 3, true, false, 0>": (80, 8, 40),   # any head width
-    "syn_fused_kernel<7, 3, true, false, 48>": (80, 8, 40),  # headline (hop): unrolled head
+    # path A fused decode, 7 grids: three workgroups per CU need <= 80 VGPRs (6 waves / SIMD)
+    # (measured: 3 resident workgroups 0.79 ms vs 2 resident 0.85 ms per 32 frames,
+    # tools/occ_probe.sh); no spills since the lane indices are re-derived after the head and
+    # per 3x3 layer (round 2 held them across: 5 spilled VGPRs, ~190 MB of scratch writes
+    # per 32-frame launch)
+    "syn_fused_kernel<7, 3, true, false, 0>": (80, 0, 0),   # any head width
+    "syn_fused_kernel<7, 3, true, false, 48>": (80, 0, 0),  # headline (hop): unrolled head
     "syn_fused_kernel<7, 4, true, false, 0>": (128, 0, 0),   # 4-channel tail: 2 workgroups
     "arm_fwd_kernel<16, 2>": (128, 0, 0),                   # path A ARM + rate (hop: 2 hidden layers)
     "arm_fwd_kernel<16, -1>": (128, 0, 0),                  # any hidden-layer count
