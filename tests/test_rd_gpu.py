@@ -167,3 +167,45 @@ def test_c3x_preset_matches_reference_rd(image, gpu):
         assert -BD_KODAK <= bd <= BD_KODAK, lines[-1]
     elif image != "kodim15_192x128":
         assert -BD_BETTER <= bd <= BD_WORSE, lines[-1]
+
+
+# The FULL c3x schedule (preset_cfg/c3x.yaml unscaled: warm-up 5 x 400 + 2 x 400 candidate
+# iterations, phases 10,000 + 1,500 + 1,000 with patience; BASELINE config 4's operating
+# point) on the Kodak-geometry target at lambda 1e-3: the reference encoder ran it twice here
+# (seeds 0 and 1, tools/gen_golden_rd.py one kodim01_768x512 1.0 0.001 SEED ...; ~3.8 h each
+# on 3 CPU threads), the GPU runs GPU_SEEDS.  Bar: the GPU's median PSNR within the
+# reference's seed spread + 0.3 dB of the reference mean, its mean rate within the spread + 10 %,
+# and the same iteration counts (patience stopping, train.py:226-240) within 2 %.
+FULL_PSNR_MARGIN_DB = 0.3
+FULL_RATE_MARGIN = 0.10
+
+
+@pytest.mark.skipif(not (GOLDEN / "rd_reference_c3x_full.json").exists(), reason="full-schedule reference fixture absent")
+def test_c3x_full_schedule_matches_reference(gpu):
+    from ccmi import io, rd, train
+    ref = json.loads((GOLDEN / "rd_reference_c3x_full.json").read_text())["runs"]
+    image, lm = "kodim01_768x512", 0.001
+    ref = [r for r in ref if r["image"] == image and r["lmbda"] == lm and r["preset"] == "c3x"]
+    assert len(ref) >= 2, "two reference seeds"
+    x = _targets()[image]
+    H, W = x.shape[-2:]
+    arch = train.Arch(H, W, dim_arm=16, n_hidden=2, layers=HOP)
+    tgt = io.to_target(x, "rgb").to(gpu)
+    recs = rd.encode_points(tgt, H, W, (lm,), arch, yuv420=False, seeds=GPU_SEEDS, preset="c3x", scale=1.0,
+                            name=image)
+    out = ROOT / "gpurun_out"
+    out.mkdir(exist_ok=True)
+    (out / "rd_gpu_c3x_full.json").write_text(json.dumps({image: [r.as_dict() for r in recs]}, indent=1))
+    rp, rr, ri = [r["psnr_db"] for r in ref], [r["rate_bpp"] for r in ref], [r["iterations"] for r in ref]
+    op = float(np.median([r.psnr_db for r in recs]))
+    orr = float(np.mean([r.rate_bpp for r in recs]))
+    its = int(np.median([r.iterations for r in recs]))
+    tol_p = FULL_PSNR_MARGIN_DB + (max(rp) - min(rp))
+    tol_r = FULL_RATE_MARGIN + (max(rr) - min(rr)) / np.mean(rr)
+    line = (f"{image} c3x full lambda {lm}: PSNR ref {np.mean(rp):.3f} ({min(rp):.3f}..{max(rp):.3f}) gpu median "
+            f"{op:.3f} (tol {tol_p:.2f}); rate ref {np.mean(rr):.4f} gpu {orr:.4f} (tol {tol_r:.2f}); iterations "
+            f"ref {ri} gpu median {its} (min {min(r.iterations for r in recs)}, max {max(r.iterations for r in recs)})")
+    print("\n" + line)
+    assert abs(op - np.mean(rp)) <= tol_p, line
+    assert abs(orr / np.mean(rr) - 1) <= tol_r, line
+    assert abs(its - np.mean(ri)) <= 0.02 * np.mean(ri), line

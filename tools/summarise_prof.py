@@ -71,8 +71,7 @@ def main(src: str, tag: str, frames: int = 8):
     global FUSED
     stats_csv = find(src, "trace", "kernel_stats.csv")
     shutil.copy(stats_csv, prof / f"{tag}_kernel_stats.csv")
-    FUSED = any("syn_fused_kernel" in r["Name"] and ("Lb1E" in r["Name"] or "true>" in r["Name"])
-                for r in csv.DictReader(stats_csv.open()))
+    FUSED = any(stage_of(r["Name"]) == "decode_fused" for r in csv.DictReader(stats_csv.open()))
     fetch = per_step_counter(find(src, ("pmc_fetch", "pmc_size"), "counter_collection.csv"), "FETCH_SIZE")
     write = per_step_counter(find(src, "pmc_write", "counter_collection.csv"), "WRITE_SIZE")
     stats = {r["Name"]: r for r in csv.DictReader(stats_csv.open())}
