@@ -24,8 +24,8 @@
 //   t_loss        train-mode output (420 nearest, clamp), MSE and its gradient
 //   t_sp_gpre / t_sp_bwd    3x3 layers backward (replicate-padding adjoint as a gather)
 //   t_head_bwd    1x1 head backward; weight gradients reduced through LDS
-//   t_ref_bwd / t_up_bwd    upsampling backward, one launch each per pyramid level
-//   t_latgrad, t_sumsq, t_adam   dL/dy, global grad norm, clipped Adam update
+//   t_lvl_bwd     upsampling backward, one launch per pyramid level (refine + transposed conv)
+//   t_latgrad_sumsq, t_adam      dL/dy + global grad norm, clipped Adam update
 #include <stdlib.h>
 
 #include <cmath>
@@ -1408,16 +1408,40 @@ __device__ __forceinline__ void reduce_taps(float (&dw)[K], float *__restrict__ 
 // GX += GY + horizontal adjoint of GU and the tap gradients (GY x U, GU x X) of the tile's
 // positions.  Per element the same fmaf chains in the same order as the former separate passes
 // (a zero-padded tap adds an exact 0).
+struct RefBwd {
+    const float *GY;
+    int64_t gys;
+    const float *X;
+    int64_t xs;
+    int h, w;
+    const float *kf;
+    int kstride, koff;
+    float *GX;
+    int64_t gxs;
+    float *slots;
+    int64_t gstride;
+    int hoff, tiles_x;
+};
 template <int KP>
-__global__ __launch_bounds__(kT) void t_ref_bwd(const float *__restrict__ GY, int64_t gys, const float *__restrict__ X,
-                                                int64_t xs, int h, int w, const float *__restrict__ kf, int kstride, int koff,
-                                                float *__restrict__ GX, int64_t gxs, float *__restrict__ slots,
-                                                int64_t gstride, int hoff, int tiles_x)
+constexpr int ref_bwd_lds()
+{
+    return 2 * (16 + KP / 2 * 2) * (64 + KP / 2 * 2) + (16 + KP / 2 * 2) * 64 + 16 * (64 + KP / 2 * 2);
+}
+// tile bx of the level (blockIdx.x of its own launch, or of the combined t_lvl_bwd)
+template <int KP>
+__device__ __forceinline__ void ref_bwd_tile(float *pool, int bx, const RefBwd &R)
 {
     constexpr int P = KP / 2, TY = 16, TX = 64, SY = TY + 2 * P, SX = TX + 2 * P;
-    __shared__ float sx[SY][SX], sg[SY][SX], su[SY][TX], sgu[TY][SX];
+    float(*sx)[SX] = reinterpret_cast<float(*)[SX]>(pool);
+    float(*sg)[SX] = reinterpret_cast<float(*)[SX]>(pool + SY * SX);
+    float(*su)[TX] = reinterpret_cast<float(*)[TX]>(pool + 2 * SY * SX);
+    float(*sgu)[SX] = reinterpret_cast<float(*)[SX]>(pool + 2 * SY * SX + SY * TX);
+    const float *GY = R.GY, *X = R.X, *kf = R.kf;
+    const int64_t gys = R.gys, xs = R.xs, gxs = R.gxs, gstride = R.gstride;
+    const int h = R.h, w = R.w, kstride = R.kstride, koff = R.koff, hoff = R.hoff, tiles_x = R.tiles_x;
+    float *GX = R.GX, *slots = R.slots;
     const int b = blockIdx.y, tid = threadIdx.x;
-    const int ty0 = (blockIdx.x / tiles_x) * TY, tx0 = (blockIdx.x % tiles_x) * TX;
+    const int ty0 = (bx / tiles_x) * TY, tx0 = (bx % tiles_x) * TX;
     const float *wk = kf + (int64_t)b * kstride + koff;
     float wv[KP];
 #pragma unroll
@@ -1477,7 +1501,14 @@ __global__ __launch_bounds__(kT) void t_ref_bwd(const float *__restrict__ GY, in
             dw[k] = fmaf(guv, sx[t + P][c + k], dw[k]);
         }
     }
-    reduce_taps<KP>(dw, slots + ((int64_t)b * kDwSlots + blockIdx.x % kDwSlots) * gstride + hoff);
+    reduce_taps<KP>(dw, slots + ((int64_t)b * kDwSlots + bx % kDwSlots) * gstride + hoff);
+}
+
+template <int KP>
+__global__ __launch_bounds__(kT) void t_ref_bwd(RefBwd R)
+{
+    __shared__ __attribute__((aligned(16))) float pool[ref_bwd_lds<KP>()];
+    ref_bwd_tile<KP>(pool, blockIdx.x, R);
 }
 
 __device__ __forceinline__ int up_tap(int a, int d, int K) { return a + K / 2 - 1 - 2 * d; }
@@ -1617,20 +1648,46 @@ __global__ __launch_bounds__(kT) void t_up_dw(const float *__restrict__ GY, int6
 // and emits GS (horizontal adjoint of GU) for its TM source columns and the tap-gradient
 // partial sums (GY x U, GU x S) of its destination positions.  Border rows / columns take
 // the generic clamped-gather loops of t_up_gu / t_up_gs over the staged tiles.
+struct UpBwd {
+    const float *GY;
+    int64_t gys;
+    const float *S;
+    int64_t ss;
+    UpLevel A;
+    const float *kf;
+    int kstride, koff;
+    float *GS;
+    int64_t gss;
+    int accumulate;
+    float *slots;
+    int64_t gstride;
+    int hoff, tiles_x, tiles_y;
+};
 template <int K>
-__global__ __launch_bounds__(kT) void t_up_bwd(const float *__restrict__ GY, int64_t gys, const float *__restrict__ S,
-                                               int64_t ss, UpLevel A, const float *__restrict__ kf, int kstride, int koff,
-                                               float *__restrict__ GS, int64_t gss, int accumulate,
-                                               float *__restrict__ slots, int64_t gstride, int hoff, int tiles_x,
-                                               int tiles_y)
+constexpr int up_bwd_lds()
+{
+    constexpr int K2 = K / 2, DW = K2 / 2 + (K2 + 1) / 2, TR = 16, TX = 64, TM = TX / 2;
+    return (TR + DW) * (TM + DW) + (TR + DW) * TX + 2 * (TR + DW) * (TX + 2 * DW) + TR * (TX + 2 * DW);
+}
+template <int K>
+__device__ __forceinline__ void up_bwd_tile(float *pool, int bx, const UpBwd &Q)
 {
     constexpr int K2 = K / 2, DLO = -((K2 + 1) / 2), DHI = K2 / 2, DW = DHI - DLO;
     constexpr int TR = 16, TX = 64, TM = TX / 2;
     constexpr int SR = TR + DW, SC = TM + DW; // staged source tile
     constexpr int GR = 2 * (TR + DW), GC = TX + 2 * DW; // staged GY tile (GU has GC columns too)
-    __shared__ float s_s[SR][SC], s_u[SR][TX], s_gy[GR][GC], s_gu[TR][GC];
+    float(*s_s)[SC] = reinterpret_cast<float(*)[SC]>(pool);
+    float(*s_u)[TX] = reinterpret_cast<float(*)[TX]>(pool + SR * SC);
+    float(*s_gy)[GC] = reinterpret_cast<float(*)[GC]>(pool + SR * SC + SR * TX);
+    float(*s_gu)[GC] = reinterpret_cast<float(*)[GC]>(pool + SR * SC + SR * TX + GR * GC);
+    const float *GY = Q.GY, *S = Q.S, *kf = Q.kf;
+    const int64_t gys = Q.gys, ss = Q.ss, gss = Q.gss, gstride = Q.gstride;
+    const UpLevel A = Q.A;
+    const int kstride = Q.kstride, koff = Q.koff, accumulate = Q.accumulate, hoff = Q.hoff;
+    const int tiles_x = Q.tiles_x, tiles_y = Q.tiles_y;
+    float *GS = Q.GS, *slots = Q.slots;
     const int b = blockIdx.y, tid = threadIdx.x;
-    const int tile = blockIdx.x % (tiles_x * tiles_y), c = blockIdx.x / (tiles_x * tiles_y);
+    const int tile = bx % (tiles_x * tiles_y), c = bx / (tiles_x * tiles_y);
     const int r0 = (tile / tiles_x) * TR, x0 = (tile % tiles_x) * TX, m0 = x0 / 2;
     const int gy0 = 2 * (r0 - DHI), gx0 = x0 - 2 * DHI; // GY / GU tile origin
     const int hs = A.hs, ws = A.ws, hd = A.hd, wd = A.wd;
@@ -1770,24 +1827,49 @@ __global__ __launch_bounds__(kT) void t_up_bwd(const float *__restrict__ GY, int
             if (t >= 0 && t < K) dw[t] = fmaf(g, s_s[tr - DLO][(q >> 1) + d - DLO], dw[t]);
         }
     }
-    reduce_taps<K>(dw, slots + ((int64_t)b * kDwSlots + blockIdx.x % kDwSlots) * gstride + hoff);
+    reduce_taps<K>(dw, slots + ((int64_t)b * kDwSlots + bx % kDwSlots) * gstride + hoff);
+}
+
+// One pyramid step of the upsampling backward in ONE launch: workgroups [0, nref) are tiles
+// of the refine backward (latent k-1, channel 0 of the destination gradient), the rest tiles of
+// the transposed-conv backward (channels 1..C): the two read disjoint inputs and write
+// disjoint outputs, so they run side by side (the coarse levels are a few workgroups each and
+// were latency-bound as two launches)
+template <int KP, int K>
+__global__ __launch_bounds__(kT) void t_lvl_bwd(RefBwd R, UpBwd Q, int nref)
+{
+    constexpr int n = ref_bwd_lds<KP>() > up_bwd_lds<K>() ? ref_bwd_lds<KP>() : up_bwd_lds<K>();
+    __shared__ __attribute__((aligned(16))) float pool[n];
+    if ((int)blockIdx.x < nref) ref_bwd_tile<KP>(pool, blockIdx.x, R);
+    else up_bwd_tile<K>(pool, blockIdx.x - nref, Q);
 }
 
 // ------------------------------------------------------------------ latents, norm, Adam
-__global__ void t_latgrad(const float *__restrict__ gq, const float *__restrict__ dq, int N, float *__restrict__ G,
-                          int64_t gstride)
+__global__ void t_zero_rows(float *__restrict__ p, int64_t n, int64_t stride)
 {
-    const int b = blockIdx.y, i = blockIdx.x * kT + threadIdx.x;
-    if (i < N) G[(int64_t)b * gstride + i] = gq[(int64_t)b * N + i] * dq[(int64_t)b * N + i];
+    const int64_t i = (int64_t)blockIdx.x * kT + threadIdx.x;
+    if (i < n) p[(int64_t)blockIdx.y * stride + i] = 0.f;
 }
 
-__global__ __launch_bounds__(kT) void t_sumsq(const float *__restrict__ G, int64_t n, int64_t gstride, float *__restrict__ acc4)
+// dL/dy of the latents (G[0, N) = dL/dyhat * dyhat/dy) and the squared norm of the whole
+// gradient row (latents + parameters, clip_grad_norm_) in one pass
+__global__ __launch_bounds__(kT) void t_latgrad_sumsq(const float *__restrict__ gq, const float *__restrict__ dq, int N,
+                                                      float *__restrict__ G, int64_t n, int64_t gstride,
+                                                      float *__restrict__ acc4)
 {
     __shared__ float s_red[8];
     const int b = blockIdx.y;
+    float *g = G + (int64_t)b * gstride;
+    const float *gqb = gq + (int64_t)b * N, *dqb = dq + (int64_t)b * N;
     float s = 0.f;
     for (int64_t i = (int64_t)blockIdx.x * kT + threadIdx.x; i < n; i += (int64_t)gridDim.x * kT) {
-        const float v = G[(int64_t)b * gstride + i];
+        float v;
+        if (i < N) {
+            v = gqb[i] * dqb[i];
+            g[i] = v;
+        } else {
+            v = g[i];
+        }
         s = fmaf(v, v, s);
     }
     s = block_sum(s, s_red);
@@ -2141,7 +2223,9 @@ extern "C" int ccmi_train_step(const ccmi_train_args *a, void *stream)
     CCMI_HIP_CHECK(hipMemsetAsync(acc4, 0, pl.total - pl.acc4, s));
     float *slots = F(pl.slots);
     const int nreg = g.syn_off - g.up_off; // upsampling kernels' parameters (half kernels)
-    CCMI_HIP_CHECK(hipMemsetAsync(G, 0, sizeof(float) * GS * B, s));
+    // the parameter part of every gradient row (its latent part is written whole by
+    // t_latgrad_sumsq)
+    hipLaunchKernelGGL(t_zero_rows, grid1(g.P, B), dim3(kT), 0, s, G + g.N, (int64_t)g.P, GS);
 
     // ---- forward
     hipLaunchKernelGGL(t_expand, grid1(g.kfull, B), dim3(kT), 0, s, a->params, a->param_stride, g, kf);
@@ -2242,29 +2326,11 @@ extern "C" int ccmi_train_step(const ccmi_train_args *a, void *stream)
         const int C = g.L - k;
         const float *GY = (k - 1 == 0) ? gd : gst + pl.gstack_off[k - 1];
         const int64_t gys = (k - 1 == 0) ? (int64_t)g.L * npx : pl.gstack_per;
-        // refine of y_hat(k-1): channel 0 of the destination stack
-        {
-            const float *X = yq + g.off[k - 1];
-            const int koff = g.n_ups * g.K + (step % g.n_pre) * g.Kp;
-            const int hoff = g.pre_off + (step % g.n_pre) * g.hp;
-            const int64_t n = (int64_t)hd * wd;
-            // one fused launch per level (tile 16 x 64)
-            const int tx = ccmi_div_up(wd, 64);
-            const dim3 gr((unsigned)(tx * ccmi_div_up(hd, 16)), B);
-            float *GXd = gq + g.off[k - 1];
-#define CCMI_REF_BWD(KK)                                                                                             \
-    hipLaunchKernelGGL(t_ref_bwd<KK>, gr, dim3(kT), 0, s, GY, gys, X, (int64_t)g.N, hd, wd, kf, g.kfull, koff, GXd,   \
-                       (int64_t)g.N, slots, (int64_t)nreg, hoff - g.up_off, tx)
-            switch (g.Kp) {
-            case 1: CCMI_REF_BWD(1); break;
-            case 3: CCMI_REF_BWD(3); break;
-            case 5: CCMI_REF_BWD(5); break;
-            case 7: CCMI_REF_BWD(7); break;
-            default: CCMI_REF_BWD(9); break;
-            }
-#undef CCMI_REF_BWD
-            (void)n;
-        }
+        // refine of y_hat(k-1): channel 0 of the destination stack (tiles 16 x 64)
+        const int rtx = ccmi_div_up(wd, 64), nref = rtx * ccmi_div_up(hd, 16);
+        const RefBwd R{GY, gys, yq + g.off[k - 1], (int64_t)g.N, hd, wd, kf, g.kfull,
+                       g.n_ups * g.K + (step % g.n_pre) * g.Kp, gq + g.off[k - 1], (int64_t)g.N, slots, (int64_t)nreg,
+                       g.pre_off + (step % g.n_pre) * g.hp - g.up_off, rtx};
         // transposed-conv upsampling of the source stack: channels 1..C
         {
             UpLevel A{C, g.h[k], g.w[k], hd, wd, g.K, -((K2 + 1) / 2), K2 / 2, step % g.n_ups};
@@ -2282,12 +2348,27 @@ extern "C" int ccmi_train_step(const ccmi_train_args *a, void *stream)
             float *GSd = (k == g.L - 1) ? gq + g.off[k] : gst + pl.gstack_off[k];
             const int64_t gss = (k == g.L - 1) ? (int64_t)g.N : pl.gstack_per;
             if (g.K == 8 && A.d_lo == -2 && A.d_hi == 2) {
-                // the whole step in one launch (16 source rows x 64 destination columns per tile)
+                // the whole step, refine and transposed conv, in one launch (t_lvl_bwd)
                 const int tx = ccmi_div_up(wd, 64), ty = ccmi_div_up(A.hs, 16);
-                hipLaunchKernelGGL(t_up_bwd<8>, dim3((unsigned)(tx * ty * C), B), dim3(kT), 0, s, GY, gys, S, ss, A, kf,
-                                   g.kfull, koff, GSd, gss, k == g.L - 1 ? 1 : 0, slots, (int64_t)nreg, hoff - g.up_off, tx,
-                                   ty);
+                const UpBwd Q{GY, gys, S, ss, A, kf, g.kfull, koff, GSd, gss, k == g.L - 1 ? 1 : 0, slots, (int64_t)nreg,
+                              hoff - g.up_off, tx, ty};
+                const dim3 grid((unsigned)(nref + tx * ty * C), B);
+                switch (g.Kp) {
+                case 1: hipLaunchKernelGGL((t_lvl_bwd<1, 8>), grid, dim3(kT), 0, s, R, Q, nref); break;
+                case 3: hipLaunchKernelGGL((t_lvl_bwd<3, 8>), grid, dim3(kT), 0, s, R, Q, nref); break;
+                case 5: hipLaunchKernelGGL((t_lvl_bwd<5, 8>), grid, dim3(kT), 0, s, R, Q, nref); break;
+                case 7: hipLaunchKernelGGL((t_lvl_bwd<7, 8>), grid, dim3(kT), 0, s, R, Q, nref); break;
+                default: hipLaunchKernelGGL((t_lvl_bwd<9, 8>), grid, dim3(kT), 0, s, R, Q, nref); break;
+                }
                 continue;
+            }
+            const dim3 rgr((unsigned)nref, B);
+            switch (g.Kp) {
+            case 1: hipLaunchKernelGGL(t_ref_bwd<1>, rgr, dim3(kT), 0, s, R); break;
+            case 3: hipLaunchKernelGGL(t_ref_bwd<3>, rgr, dim3(kT), 0, s, R); break;
+            case 5: hipLaunchKernelGGL(t_ref_bwd<5>, rgr, dim3(kT), 0, s, R); break;
+            case 7: hipLaunchKernelGGL(t_ref_bwd<7>, rgr, dim3(kT), 0, s, R); break;
+            default: hipLaunchKernelGGL(t_ref_bwd<9>, rgr, dim3(kT), 0, s, R); break;
             }
             const int64_t nu = (int64_t)C * A.hs * wd;
             hipLaunchKernelGGL(t_up_u, grid1(nu, B), dim3(kT), 0, s, S, ss, A, kf, g.kfull, koff, U, pl.tmp_per);
@@ -2307,9 +2388,9 @@ extern "C" int ccmi_train_step(const ccmi_train_args *a, void *stream)
     hipLaunchKernelGGL(t_dw_fold, dim3((unsigned)ccmi_div_up(nreg, 64), B), dim3(64), 0, s, slots, nreg, Gth, GS, g.up_off);
 
     // ---- latent gradients, norm, Adam
-    hipLaunchKernelGGL(t_latgrad, grid1(g.N, B), dim3(kT), 0, s, gq, dq, g.N, G, GS);
-    hipLaunchKernelGGL(t_sumsq, dim3((unsigned)std::min<int64_t>(ccmi_div_up((int)std::min<int64_t>(GS, 1 << 30), kT), 64), B),
-                       dim3(kT), 0, s, G, GS, GS, acc4);
+    // about eight workgroups per CU over the batch, 4+ elements per thread
+    const unsigned nls = (unsigned)std::max<int64_t>(1, std::min<int64_t>(ccmi_div_up(GS, 4 * kT), std::max(1, 2048 / B)));
+    hipLaunchKernelGGL(t_latgrad_sumsq, dim3(nls, B), dim3(kT), 0, s, gq, dq, g.N, G, GS, GS, acc4);
     const float total = a->yuv420 ? (float)(npx + 2 * (int64_t)(g.H / 2) * (g.W / 2)) : (float)(3 * npx);
     if (a->loss_out) hipLaunchKernelGGL(t_finish, dim3(1), dim3(std::max(64, B)), 0, s, acc4, 1.f / total, lam_px, a->loss_out, B);
     if (a->update) {
