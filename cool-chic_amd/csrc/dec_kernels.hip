@@ -658,27 +658,46 @@ __host__ __device__ constexpr uint32_t bin_code(uint32_t st)
     return (st & 0x80u) | ((((st >> 7) ? st ^ 0xFFu : st) & 0xFFu) >> 2);
 }
 
-// one bin of a static context given as bin_code(state) (TDecBinCABAC::decodeBin)
+// one bin of a static context given as bin_code(state) (TDecBinCABAC::decodeBin): the state
+// update as one SALU sequence with a single compare whose SCC drives four selects (the
+// compiled C form rebuilt the decision as a 64-bit lane mask ANDed with exec per select:
+// ~30 instead of 19 instructions on the serial chain).  LPS iff value >= (range - lps) << 7;
+// the renormalisation shift is clz(lps) - 23 after an LPS (Contexts.cpp's table for lps in
+// [4, 236]) and 1 after an MPS that left the range below 256.
 __device__ __forceinline__ uint32_t bin_fast(Cabac<DevBytesV> &c, uint32_t code)
 {
-    const uint32_t mps = code >> 7;
-    const uint32_t lps = (((code & 0x1Fu) * (c.range >> 5)) >> 1) + 4;
-    const uint32_t rmps = c.range - lps;
-    const uint32_t scaled = rmps << 7;
-    // is_lps = value >= scaled, as an all-ones mask from the sign of scaled - 1 - value (both
-    // < 2^31): plain scalar arithmetic, where a bool select went through the VALU and back
-    const uint32_t m = (uint32_t)((int32_t)(scaled - 1u - c.value) >> 31);
-    // renormalisation: an LPS shifts its range lps in [4, 236] back to >= 256 (clz(lps) - 23 =
-    // Contexts.cpp's table); an MPS shifts once when the remaining range fell below 256
-    const uint32_t nb = ((uint32_t)(__builtin_clz(lps) - 23) & m) | (((rmps >> 8) ^ 1u) & ~m); // rmps < 512
-    c.value = (c.value - (scaled & m)) << nb;
-    c.range = ((lps & m) | (rmps & ~m)) << nb;
+    uint32_t range = c.range, value = c.value, nb, lp, t0, t1, lps, rm, sc, nl, nm;
+    asm("s_and_b32 %[t0], %[code], 31\n\t"
+        "s_lshr_b32 %[t1], %[range], 5\n\t"
+        "s_mul_i32 %[t0], %[t0], %[t1]\n\t"
+        "s_lshr_b32 %[t0], %[t0], 1\n\t"
+        "s_add_u32 %[lps], %[t0], 4\n\t"
+        "s_sub_u32 %[rm], %[range], %[lps]\n\t"
+        "s_lshl_b32 %[sc], %[rm], 7\n\t"
+        "s_flbit_i32_b32 %[nl], %[lps]\n\t"
+        "s_sub_u32 %[nl], %[nl], 23\n\t"
+        "s_lshr_b32 %[nm], %[rm], 8\n\t"
+        "s_xor_b32 %[nm], %[nm], 1\n\t"
+        "s_cmp_ge_u32 %[value], %[sc]\n\t"
+        "s_cselect_b32 %[range], %[lps], %[rm]\n\t"
+        "s_cselect_b32 %[nb], %[nl], %[nm]\n\t"
+        "s_cselect_b32 %[sc], %[sc], 0\n\t"
+        "s_cselect_b32 %[lp], 1, 0\n\t"
+        "s_sub_u32 %[value], %[value], %[sc]\n\t"
+        "s_lshl_b32 %[value], %[value], %[nb]\n\t"
+        "s_lshl_b32 %[range], %[range], %[nb]"
+        : [range] "+s"(range), [value] "+s"(value), [nb] "=&s"(nb), [lp] "=&s"(lp), [t0] "=&s"(t0), [t1] "=&s"(t1),
+          [lps] "=&s"(lps), [rm] "=&s"(rm), [sc] "=&s"(sc), [nl] "=&s"(nl), [nm] "=&s"(nm)
+        : [code] "s"(code)
+        : "scc");
+    c.range = range;
+    c.value = value;
     c.bits_needed += (int32_t)nb;
     if (c.bits_needed >= 0) {
         c.value += c.src.next() << c.bits_needed;
         c.bits_needed -= 8;
     }
-    return mps ^ (m & 1u);
+    return (code >> 7) ^ lp;
 }
 
 template <int D, int NH>
