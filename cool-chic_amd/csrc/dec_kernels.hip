@@ -810,7 +810,9 @@ __global__ __launch_bounds__(64) void dec_arm_lat_kernel(const ArmStreamDesc *__
     __syncthreads();
 
     // context offsets of the above-row contexts (rows y-3 .. y-1), for the chunk precompute
-    int big = 0;
+    // sticky 24-bit guard: the largest (q + 32767) as unsigned, >= 65535 once a decoded latent
+    // has |q| >= 32768 (an s_max per latent; the bool form went through a VGPR and back)
+    uint32_t qspan = 0;
 #if defined(CCMI_ARM_STAMPS)
     LACC(5, __builtin_amdgcn_s_memtime() - t_begin);
     const uint64_t t_loop = __builtin_amdgcn_s_memtime();
@@ -866,7 +868,7 @@ __global__ __launch_bounds__(64) void dec_arm_lat_kernel(const ArmStreamDesc *__
                     *reinterpret_cast<int4 *>(dst + n) = int4{acc[0], acc[1], acc[2], acc[3]};
                 }
             };
-            if (w24 && !big) sums(std::true_type{});
+            if (w24 && qspan < 65535u) sums(std::true_type{});
             else sums(std::false_type{});
             if (c & 1) have1 = c;
             else have0 = c;
@@ -975,7 +977,7 @@ __global__ __launch_bounds__(64) void dec_arm_lat_kernel(const ArmStreamDesc *__
                 return int2{row_sum16(imul<f24>(Wo0, a)) + bo0, row_sum16(imul<f24>(Wo1, a)) + bo1};
             };
             int2 ms;
-            if (w24 && !big) ms = mlp(std::true_type{}, std::true_type{});
+            if (w24 && qspan < 65535u) ms = mlp(std::true_type{}, std::true_type{});
             else if (w24) ms = mlp(std::false_type{}, std::true_type{});
             else ms = mlp(std::false_type{}, std::false_type{});
 #if defined(CCMI_ARM_STAMPS)
@@ -1007,9 +1009,11 @@ __global__ __launch_bounds__(64) void dec_arm_lat_kernel(const ArmStreamDesc *__
             const uint32_t pk = (uint32_t)mr | e.y; // mu rounded (a multiple of 256), sign-bin state
             STAMP(t2);
             // decode_single (cc-bac.h:192-231), in order, until the first non-zero latent
+            // unrolled: constant lanes for the readlanes and a constant guess per latent
             int nd = 0;
-#pragma unroll 1
-            for (int j = 0; j < L; ++j) {
+#pragma unroll
+            for (int j = 0; j < kSpec; ++j) {
+                if (j >= L) break;
                 const int src_lane = 16 * j + 15;
                 const uint32_t st = __builtin_amdgcn_readlane(e.x, src_lane);
                 const uint32_t pkj = __builtin_amdgcn_readlane(pk, src_lane);
@@ -1022,7 +1026,7 @@ __global__ __launch_bounds__(64) void dec_arm_lat_kernel(const ArmStreamDesc *__
                     if (bin_fast(cab, pkj & 0xFF)) val = -val;
                 }
                 const int32_t q = ((int32_t)pkj >> 8) + val;
-                big |= (q >= 32768 || q <= -32768);
+                qspan = max(qspan, (uint32_t)(q + 32767));
                 const int32_t v = (int32_t)((uint32_t)q << kArmPrec);
                 push(v, x + j);
                 ++nd;
