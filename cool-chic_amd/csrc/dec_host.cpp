@@ -283,6 +283,28 @@ struct EventSet {
     }
 };
 
+// every synthesis weight (not the biases) of every branch fits 24 signed bits: the fused
+// integer synthesis then multiplies with v_mul_i32_i24 (DecSynArgs::f24)
+bool syn_weights_fit24(const FrameHost &f)
+{
+    const size_t per_branch = f.syn.size() / (size_t)std::max(1, f.n_branches);
+    for (int b = 0; b < f.n_branches; ++b) {
+        size_t q = per_branch * (size_t)b;
+        int c = f.n_layers;
+        for (const SynLayerDesc &L : f.layers) {
+            const size_t nw = (size_t)L.n_out * c * L.ks * L.ks;
+            if (q + nw > f.syn.size()) return false;
+            for (size_t i = 0; i < nw; ++i) {
+                const int32_t v = f.syn[q + i];
+                if (v < -(1 << 23) || v >= (1 << 23)) return false;
+            }
+            q += nw + (size_t)L.n_out;
+            c = L.n_out;
+        }
+    }
+    return true;
+}
+
 // ws / ws_bytes: caller-owned device workspace (NULL: one hipMalloc per call); need: when
 // not NULL, only the workspace size is computed (streams parsed, nothing launched).
 int decode_many(const uint8_t *const *streams, const size_t *lens, int n, uint8_t *const *outs, const size_t *caps,
@@ -494,6 +516,7 @@ int decode_many(const uint8_t *const *streams, const size_t *lens, int n, uint8_
         sa.params = reinterpret_cast<const int32_t *>(dev + p.syn_off);
         sa.out = reinterpret_cast<int32_t *>(dev + p.synout_off);
         sa.workspace = reinterpret_cast<int32_t *>(dev + p.synws_off);
+        sa.f24 = syn_weights_fit24(f) ? 1 : 0;
         t.bitdepth = of[i].bitdepth;
         t.kind = of[i].kind;
         t.dst = dev + p.out_off;

@@ -84,6 +84,11 @@ struct DecSynArgs {
     const int32_t *params; // per layer W then b (one branch)
     int32_t *out;
     int32_t *workspace;    // generic path ping-pong, 2 * maxc * h * w
+    // every weight fits 24 signed bits (host-checked): the fused kernel multiplies with
+    // v_mul_i32_i24 (full rate) instead of v_mul_lo_u32 (quarter rate).  The activations
+    // always fit: each is an int32 shifted right by UPS_/SYN_ precision 12 (|v| <= 2^19), and
+    // a 24x24-bit product's low 32 bits equal the int32 product's.
+    int f24 = 0;
 };
 size_t dec_syn_workspace_elems(const DecSynArgs &a);
 int launch_dec_syn(const DecSynArgs &a, hipStream_t s);

@@ -1190,27 +1190,32 @@ struct DecSynFused {
     int res[kMaxSp], relu[kMaxSp];
     int32_t *out;
     int tiles_x;
+    int f24; // DecSynArgs::f24
 };
 
-template <int CIN, int CMID>
+template <int CIN, int CMID, bool F24>
 __device__ __forceinline__ void syn_fused_body(const DecSynFused &A, int32_t (*s_buf)[CMID][kRegion]);
 
 template <int CIN, int CMID>
 __global__ __launch_bounds__(kThreads) void dec_syn_fused(DecSynFused A)
 {
-    __shared__ int32_t s_buf[2][CMID][kRegion];
-    syn_fused_body<CIN, CMID>(A, s_buf);
+    __shared__ __attribute__((aligned(16))) int32_t s_buf[2][CMID][kRegion];
+    if (A.f24) syn_fused_body<CIN, CMID, true>(A, s_buf);
+    else syn_fused_body<CIN, CMID, false>(A, s_buf);
 }
 
 template <int CIN, int CMID>
 __global__ __launch_bounds__(kThreads) void dec_syn_fused_batch(const DecSynFused *__restrict__ As)
 {
-    __shared__ int32_t s_buf[2][CMID][kRegion];
-    const DecSynFused A = As[blockIdx.y];
-    syn_fused_body<CIN, CMID>(A, s_buf);
+    __shared__ __attribute__((aligned(16))) int32_t s_buf[2][CMID][kRegion];
+    // by reference: the frame's argument record is read with scalar loads where it is used (a
+    // by-value copy with runtime-indexed layer arrays lived in scratch, 160 bytes per lane)
+    const DecSynFused &A = As[blockIdx.y];
+    if (A.f24) syn_fused_body<CIN, CMID, true>(A, s_buf);
+    else syn_fused_body<CIN, CMID, false>(A, s_buf);
 }
 
-template <int CIN, int CMID>
+template <int CIN, int CMID, bool F24>
 __device__ __forceinline__ void syn_fused_body(const DecSynFused &A, int32_t (*s_buf)[CMID][kRegion])
 {
     const int halo = A.n_sp;
@@ -1221,22 +1226,26 @@ __device__ __forceinline__ void syn_fused_body(const DecSynFused &A, int32_t (*s
     const int c = threadIdx.x & (kRW - 1), r0 = threadIdx.x >> 6;
     const int gx = ox + c, cxg = clampi(gx, A.W - 1);
 
-    for (int r = r0; r < kRH; r += 4) {
-        const int64_t pix = (int64_t)clampi(oy + r, A.H - 1) * A.W + cxg;
-        int32_t x[CIN];
-#pragma unroll
-        for (int k = 0; k < CIN; ++k) x[k] = A.in[k * plane + pix];
-        int32_t o[CMID];
-#pragma unroll
-        for (int m = 0; m < CMID; ++m) o[m] = A.b1[m];
-        for (int j = 0; j < A.hid; ++j) {
-            int32_t acc = A.b0[j];
-#pragma unroll
-            for (int k = 0; k < CIN; ++k) acc += x[k] * A.w0[j * CIN + k];
-            acc = acc < 0 ? 0 : acc >> kSynPrec;
-#pragma unroll
-            for (int m = 0; m < CMID; ++m) o[m] += acc * A.w1[m * A.hid + j];
+    // the head's weight records (w0[j][0..CIN), b0[j], w1[0..CMID)[j]; 12 ints) in the second
+    // ping-pong buffer, which the first 3x3 layer writes only after its barrier: read back as
+    // three broadcast ds_read_b128 per hidden unit, issued ahead of use (scalar weight loads
+    // per unit made every unit wait for its own s_load round trip)
+    static_assert(CIN + 1 + CMID <= 12, "head record");
+    int32_t *s_rec = &s_buf[1][0][0];
+    const int hid = A.hid;
+    const bool recs = hid * 12 <= CMID * kRegion;
+    if (recs) {
+        for (int i = threadIdx.x; i < hid * 12; i += kThreads) {
+            const int j = i / 12, f = i - j * 12;
+            int32_t v = 0;
+            if (f < CIN) v = A.w0[j * CIN + f];
+            else if (f == CIN) v = A.b0[j];
+            else if (f < CIN + 1 + CMID) v = A.w1[(f - CIN - 1) * hid + j];
+            s_rec[i] = v;
         }
+        __syncthreads();
+    }
+    auto store_head = [&](int r, const int32_t (&o)[CMID]) {
         const int gy = oy + r;
 #pragma unroll
         for (int m = 0; m < CMID; ++m) {
@@ -1246,6 +1255,58 @@ __device__ __forceinline__ void syn_fused_body(const DecSynFused &A, int32_t (*s
             } else {
                 s_buf[0][m][r * kRW + c] = v;
             }
+        }
+    };
+    if (recs) {
+        // two rows (r, r + 4) per pass over the records
+        typedef int i4v __attribute__((ext_vector_type(4)));
+        typedef const __attribute__((address_space(3))) i4v *lds_i4;
+        lds_i4 rb = (lds_i4)s_rec;
+        for (int r = r0; r < kRH; r += 8) {
+            int32_t x[2][CIN], o[2][CMID];
+#pragma unroll
+            for (int p = 0; p < 2; ++p) {
+                const int64_t pix = (int64_t)clampi(oy + r + 4 * p, A.H - 1) * A.W + cxg;
+#pragma unroll
+                for (int k = 0; k < CIN; ++k) x[p][k] = A.in[k * plane + pix];
+#pragma unroll
+                for (int m = 0; m < CMID; ++m) o[p][m] = A.b1[m];
+            }
+#pragma unroll 2
+            for (int j = 0; j < hid; ++j) {
+                const i4v q0 = rb[3 * j], q1 = rb[3 * j + 1], q2 = rb[3 * j + 2];
+                const int32_t w[12] = {q0.x, q0.y, q0.z, q0.w, q1.x, q1.y, q1.z, q1.w, q2.x, q2.y, q2.z, q2.w};
+#pragma unroll
+                for (int p = 0; p < 2; ++p) {
+                    int32_t acc = w[CIN];
+#pragma unroll
+                    for (int k = 0; k < CIN; ++k) acc += imul<F24>(x[p][k], w[k]);
+                    acc = acc < 0 ? 0 : acc >> kSynPrec;
+#pragma unroll
+                    for (int m = 0; m < CMID; ++m) o[p][m] += imul<F24>(acc, w[CIN + 1 + m]);
+                }
+            }
+            store_head(r, o[0]);
+            store_head(r + 4, o[1]);
+        }
+    } else {
+        for (int r = r0; r < kRH; r += 4) {
+            const int64_t pix = (int64_t)clampi(oy + r, A.H - 1) * A.W + cxg;
+            int32_t x[CIN];
+#pragma unroll
+            for (int k = 0; k < CIN; ++k) x[k] = A.in[k * plane + pix];
+            int32_t o[CMID];
+#pragma unroll
+            for (int m = 0; m < CMID; ++m) o[m] = A.b1[m];
+            for (int j = 0; j < hid; ++j) {
+                int32_t acc = A.b0[j];
+#pragma unroll
+                for (int k = 0; k < CIN; ++k) acc += imul<F24>(x[k], A.w0[j * CIN + k]);
+                acc = acc < 0 ? 0 : acc >> kSynPrec;
+#pragma unroll
+                for (int m = 0; m < CMID; ++m) o[m] += imul<F24>(acc, A.w1[m * hid + j]);
+            }
+            store_head(r, o);
         }
     }
     if (halo == 0) return;
@@ -1283,7 +1344,7 @@ __device__ __forceinline__ void syn_fused_body(const DecSynFused &A, int32_t (*s
 #pragma unroll
                     for (int dy = 0; dy < 3; ++dy)
 #pragma unroll
-                        for (int dx = 0; dx < 3; ++dx) acc += nb[k][dy][dx] * wt[((m * CMID + k) * 3 + dy) * 3 + dx];
+                        for (int dx = 0; dx < 3; ++dx) acc += imul<F24>(nb[k][dy][dx], wt[((m * CMID + k) * 3 + dy) * 3 + dx]);
                 const int32_t v = acc < 0 ? (A.relu[s] ? 0 : -((-acc) >> kSynPrec)) : acc >> kSynPrec;
                 if (last)
                     A.out[m * plane + (int64_t)gy * A.W + gx] = v;
@@ -1588,6 +1649,7 @@ int launch_dec_syn(const DecSynArgs &a, hipStream_t s)
             F.relu[i] = a.layers[2 + i].relu;
         }
         F.out = a.out;
+        F.f24 = a.f24;
         const int halo = F.n_sp;
         F.tiles_x = ccmi_div_up(a.w, kRW - 2 * halo);
         dim3 grid(F.tiles_x * ccmi_div_up(a.h, kRH - 2 * halo));
@@ -1681,6 +1743,7 @@ static DecSynFused make_syn_fused(const DecSynArgs &a)
         F.relu[i] = a.layers[2 + i].relu;
     }
     F.out = a.out;
+    F.f24 = a.f24;
     F.tiles_x = ccmi_div_up(a.w, kRW - 2 * F.n_sp);
     return F;
 }

@@ -26,5 +26,9 @@ for reps in [int(x) for x in (sys.argv[1:] or ["1", "4"])]:
     outs = decode.decode_batch(batch)
     dt = time.perf_counter() - t0
     ok = all(hashlib.md5(o).hexdigest() == MD5["jvet/" + f.name]["md5"] for f, o in zip(files * reps, outs))
+    tm = decode.last_timing()
+    kern = (tm["arm_cabac"] + tm["ups_syn_out"]) / 1e3
     print(json.dumps({"frames": len(batch), "seconds": round(dt, 4), "fps": round(len(batch) / dt, 2),
-                      "mpix_s": round(len(batch) * 1280 * 720 / dt / 1e6, 2), "bit_exact": ok}), flush=True)
+                      "mpix_s": round(len(batch) * 1280 * 720 / dt / 1e6, 2),
+                      "mpix_s_kernels": round(len(batch) * 1280 * 720 / kern / 1e6, 2),
+                      "stage_ms": {k: round(v, 2) for k, v in tm.items()}, "bit_exact": ok}), flush=True)
