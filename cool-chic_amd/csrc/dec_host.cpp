@@ -417,9 +417,31 @@ int decode_many(const uint8_t *const *streams, const size_t *lens, int n, uint8_
     ev.rec(0, s);
     CCMI_HIP_CHECK(hipMemcpyAsync(dev, host.data(), cst, hipMemcpyHostToDevice, s));
 
-    // ---- ARM + CABAC: every non-empty latent layer of every frame, one launch per (d, nh)
+    // ---- frames in K chunks by decode cost (coded bytes of their latent layers), cheapest
+    // first.  Each chunk's ARM launch and decoder tail run on a stream of their own, so the
+    // tails of the early chunks overlap the long ARM chains of the later ones: a batch's ARM
+    // stage is the slowest layer-0 chain, and most CUs sit idle once the short streams are done.
+    // K = 2: the caller's stream and one more (GPU_MAX_HW_QUEUES is 4 per process; streams
+    // beyond the hardware queues share one and serialise)
+#ifndef CCMI_DEC_CHUNKS
+#define CCMI_DEC_CHUNKS 2
+#endif
+    const int K = n >= 64 ? CCMI_DEC_CHUNKS : 1;
+    std::vector<int> chunk_of(n, 0);
+    if (K > 1) {
+        std::vector<int> order(n);
+        std::vector<size_t> cost(n, 0);
+        for (int i = 0; i < n; ++i) {
+            order[i] = i;
+            for (int l = 0; l < fr[i].n_layers; ++l) cost[i] += fr[i].lat_n[l];
+        }
+        std::stable_sort(order.begin(), order.end(), [&](int a, int b) { return cost[a] < cost[b]; });
+        for (int r = 0; r < n; ++r) chunk_of[order[r]] = (int)((int64_t)r * K / n);
+    }
+
+    // ---- ARM + CABAC: every non-empty latent layer of every frame, one launch per (chunk, d, nh)
     std::vector<ArmStreamDesc> desc;
-    struct Key { int d, nh; };
+    struct Key { int chunk, d, nh; };
     std::vector<std::pair<Key, std::vector<ArmStreamDesc>>> groups;
     int max_w = 0, max_blocks = 1;
     for (int i = 0; i < n; ++i) {
@@ -459,17 +481,19 @@ int decode_many(const uint8_t *const *streams, const size_t *lens, int n, uint8_
                 while ((1 << sh) < blk) ++sh;
                 max_blocks = std::max(max_blocks, ((a.h + blk - 1) >> sh) * ((a.w + blk - 1) >> sh));
             }
-            auto it = std::find_if(groups.begin(), groups.end(),
-                                   [&](auto &g) { return g.first.d == a.d && g.first.nh == a.nh; });
+            auto it = std::find_if(groups.begin(), groups.end(), [&](auto &g) {
+                return g.first.chunk == chunk_of[i] && g.first.d == a.d && g.first.nh == a.nh;
+            });
             if (it == groups.end()) {
-                groups.push_back({Key{a.d, a.nh}, {}});
+                groups.push_back({Key{chunk_of[i], a.d, a.nh}, {}});
                 it = groups.end() - 1;
             }
             it->second.push_back(a);
         }
     }
-    size_t dpos = 0;
+
     std::vector<ArmStreamDesc> all;
+    std::stable_sort(groups.begin(), groups.end(), [](const auto &x, const auto &y) { return x.first.chunk < y.first.chunk; });
     for (auto &g : groups) {
         // longest streams first: they bound the launch
         std::stable_sort(g.second.begin(), g.second.end(),
@@ -528,7 +552,7 @@ int decode_many(const uint8_t *const *streams, const size_t *lens, int n, uint8_
     for (int i = 0; i < n; ++i) {
         if (fr[i].n_branches != 1 || !dec_tail_batchable(tail[i])) continue;
         auto it = std::find_if(tgroups.begin(), tgroups.end(), [&](const std::vector<int> &g) {
-            return g.size() < 65535 && dec_tail_same_group(tail[g[0]], tail[i]);
+            return g.size() < 65535 && chunk_of[g[0]] == chunk_of[i] && dec_tail_same_group(tail[g[0]], tail[i]);
         });
         if (it == tgroups.end()) {
             tgroups.emplace_back();
@@ -549,40 +573,75 @@ int decode_many(const uint8_t *const *streams, const size_t *lens, int n, uint8_
     }
     if (tpos) CCMI_HIP_CHECK(hipMemcpyAsync(dev + tail_off, tab.data(), tpos, hipMemcpyHostToDevice, s));
     ev.rec(1, s);
-    if (!all.empty()) {
+    // one chunk's ARM launches, then its decoder tail (batched groups, then the rest per frame)
+    auto launch_chunk = [&](int c, hipStream_t cs, hipEvent_t arm_done) -> int {
+        size_t dp = 0;
         for (auto &g : groups) {
-            const ArmStreamDesc *dd = reinterpret_cast<const ArmStreamDesc *>(dev + desc_off) + dpos;
-            if (int rc = launch_dec_arm(dd, (int)g.second.size(), max_w, max_blocks, g.first.d, g.first.nh, s)) return rc;
-            dpos += g.second.size();
-        }
-    }
-
-    ev.rec(2, s);
-    // ---- upsampling, synthesis (+ blend), output bytes: batched groups, then the rest per frame
-    for (size_t g = 0; g < tgroups.size(); ++g)
-        if (int rc = launch_dec_tail_batch(tail[tgroups[g][0]], (int)tgroups[g].size(), dev + tail_off + tg_off[g], s))
-            return rc;
-    for (int i = 0; i < n; ++i) {
-        if (batched[i]) continue;
-        FrameHost &f = fr[i];
-        DevPlan &p = pl[i];
-        if (int rc = launch_dec_ups(tail[i].ups, s)) return rc;
-
-        const int nout = f.layers.back().n_out;
-        const int64_t plane = (int64_t)f.h * f.w;
-        size_t per_branch = f.syn.size() / f.n_branches;
-        int32_t *synout = reinterpret_cast<int32_t *>(dev + p.synout_off);
-        for (int b = 0; b < f.n_branches; ++b) {
-            DecSynArgs sa = tail[i].syn;
-            sa.params += per_branch * b;
-            sa.out = synout + (size_t)b * nout * plane;
-            if (int rc = launch_dec_syn(sa, s)) return rc;
-            if (b >= 1) // run_syn (cc-frame-decoder.cpp:1044-1149): blends on 3 planes
-                if (int rc = launch_dec_blend(synout, synout + (size_t)b * nout * plane, 3 * plane,
-                                              f.blend[0], f.blend[b], b == 1, s))
+            if (g.first.chunk == c) {
+                const ArmStreamDesc *dd = reinterpret_cast<const ArmStreamDesc *>(dev + desc_off) + dp;
+                if (int rc = launch_dec_arm(dd, (int)g.second.size(), max_w, max_blocks, g.first.d, g.first.nh, cs))
                     return rc;
+            }
+            dp += g.second.size();
         }
-        if (int rc = launch_dec_output(synout, f.h, f.w, of[i].bitdepth, of[i].kind, dev + p.out_off, s)) return rc;
+        if (arm_done) CCMI_HIP_CHECK(hipEventRecord(arm_done, cs));
+        for (size_t g = 0; g < tgroups.size(); ++g)
+            if (chunk_of[tgroups[g][0]] == c)
+                if (int rc = launch_dec_tail_batch(tail[tgroups[g][0]], (int)tgroups[g].size(), dev + tail_off + tg_off[g], cs))
+                    return rc;
+        for (int i = 0; i < n; ++i) {
+            if (batched[i] || chunk_of[i] != c) continue;
+            FrameHost &f = fr[i];
+            DevPlan &p = pl[i];
+            if (int rc = launch_dec_ups(tail[i].ups, cs)) return rc;
+
+            const int nout = f.layers.back().n_out;
+            const int64_t plane = (int64_t)f.h * f.w;
+            size_t per_branch = f.syn.size() / f.n_branches;
+            int32_t *synout = reinterpret_cast<int32_t *>(dev + p.synout_off);
+            for (int b = 0; b < f.n_branches; ++b) {
+                DecSynArgs sa = tail[i].syn;
+                sa.params += per_branch * b;
+                sa.out = synout + (size_t)b * nout * plane;
+                if (int rc = launch_dec_syn(sa, cs)) return rc;
+                if (b >= 1) // run_syn (cc-frame-decoder.cpp:1044-1149): blends on 3 planes
+                    if (int rc = launch_dec_blend(synout, synout + (size_t)b * nout * plane, 3 * plane,
+                                                  f.blend[0], f.blend[b], b == 1, cs))
+                        return rc;
+            }
+            if (int rc = launch_dec_output(synout, f.h, f.w, of[i].bitdepth, of[i].kind, dev + p.out_off, cs)) return rc;
+        }
+        return CCMI_OK;
+    };
+    // K > 1: streams forked from s after the uploads and joined back before the downloads
+    struct Fork {
+        std::vector<hipStream_t> st; // st[0] = the caller's stream (not destroyed)
+        std::vector<hipEvent_t> ev;  // [0] fork; per chunk c: [1 + 3c] start, [2 + 3c] ARM done, [3 + 3c] done
+        ~Fork()
+        {
+            for (size_t k = 1; k < st.size(); ++k)
+                if (st[k]) (void)hipStreamDestroy(st[k]);
+            for (auto x : ev)
+                if (x) (void)hipEventDestroy(x);
+        }
+    } fk;
+    if (K == 1) {
+        if (int rc = launch_chunk(0, s, ev.ok ? ev.e[2] : nullptr)) return rc;
+    } else {
+        fk.st.assign(K, nullptr);
+        fk.st[0] = s;
+        fk.ev.assign(1 + 3 * K, nullptr);
+        for (int c = 1; c < K; ++c) CCMI_HIP_CHECK(hipStreamCreateWithFlags(&fk.st[c], hipStreamNonBlocking));
+        for (auto &x : fk.ev) CCMI_HIP_CHECK(hipEventCreate(&x));
+        CCMI_HIP_CHECK(hipEventRecord(fk.ev[0], s));
+        for (int c = K - 1; c >= 0; --c) { // the most expensive chunk first
+            hipStream_t cs = fk.st[c];
+            if (c > 0) CCMI_HIP_CHECK(hipStreamWaitEvent(cs, fk.ev[0], 0));
+            CCMI_HIP_CHECK(hipEventRecord(fk.ev[1 + 3 * c], cs));
+            if (int rc = launch_chunk(c, cs, fk.ev[2 + 3 * c])) return rc;
+            CCMI_HIP_CHECK(hipEventRecord(fk.ev[3 + 3 * c], cs));
+        }
+        for (int c = 1; c < K; ++c) CCMI_HIP_CHECK(hipStreamWaitEvent(s, fk.ev[3 + 3 * c], 0));
     }
     ev.rec(3, s);
     for (int i = 0; i < n && outs; ++i) {
@@ -608,8 +667,22 @@ int decode_many(const uint8_t *const *streams, const size_t *lens, int n, uint8_
         }
     }
 #endif
-    if (ev.ok)
+    if (ev.ok) {
         for (int k = 0; k < 4; ++k) (void)hipEventElapsedTime(&g_last_ms[k], ev.e[k], ev.e[k + 1]);
+        if (K > 1) {
+            // overlapped stages: ARM = the longest chunk's ARM (its start to its ARM end, events
+            // of one stream), tail = the rest of the kernel span
+            float span = 0.f, arm = 0.f;
+            (void)hipEventElapsedTime(&span, ev.e[1], ev.e[3]);
+            for (int c = 0; c < K; ++c) {
+                float t = 0.f;
+                if (hipEventElapsedTime(&t, fk.ev[1 + 3 * c], fk.ev[2 + 3 * c]) == hipSuccess) arm = std::max(arm, t);
+            }
+            g_last_ms[1] = arm;
+            g_last_ms[2] = span - arm;
+            (void)hipGetLastError(); // a timing query that failed must not surface in the next call
+        }
+    }
     return CCMI_OK;
 }
 
