@@ -116,8 +116,9 @@ def test_debug_preset_matches_reference_rd(image, gpu):
 
 
 # c3x preset (preset_cfg/c3x.yaml) with every phase / warm-up / patience scaled by 0.1, as
-# tools/gen_golden_rd.py ran it (C3X_SCALE): one reference seed per lambda, so the tolerance is
-# the fixed margin widened by the debug preset's largest seed spread on the same image.
+# tools/gen_golden_rd.py ran it (C3X_SCALE): two reference seeds per lambda, so the tolerance is
+# the fixed margin widened by the reference's own seed spread at that lambda (and at least by
+# the debug preset's largest spread on the same image, for a lambda the two seeds happen to agree on).
 C3X_SCALE = 0.1
 
 
@@ -127,9 +128,10 @@ def test_c3x_preset_matches_reference_rd(image, gpu):
     d = json.loads((GOLDEN / "rd_reference_c3x.json").read_text())
     ref = [r for r in d["runs"] if r["image"] == image]
     assert {r["lmbda"] for r in ref} == set(LAMBDAS)
-    spread_p = max(max(x["psnr_db"] for x in g) - min(x["psnr_db"] for x in g)
-                   for g in ([r for r in _ref("rd_reference_debug.json") if r["image"] == image and r["lmbda"] == lm]
-                             for lm in LAMBDAS))
+    assert all(len({r["seed"] for r in ref if r["lmbda"] == lm}) >= 2 for lm in LAMBDAS), "two reference seeds"
+    spread_dbg = max(max(x["psnr_db"] for x in g) - min(x["psnr_db"] for x in g)
+                     for g in ([r for r in _ref("rd_reference_debug.json") if r["image"] == image and r["lmbda"] == lm]
+                               for lm in LAMBDAS))
     x = _targets()[image]
     H, W = x.shape[-2:]
     arch = train.Arch(H, W, dim_arm=16, n_hidden=2, layers=HOP)
@@ -144,20 +146,22 @@ def test_c3x_preset_matches_reference_rd(image, gpu):
     f.write_text(json.dumps(prev, indent=1))
     lines = []
     for lm in LAMBDAS:
-        r = [x for x in ref if x["lmbda"] == lm][0]
+        r = [x for x in ref if x["lmbda"] == lm]
+        rp, rr, ri = [x["psnr_db"] for x in r], [x["rate_bpp"] for x in r], [x["iterations"] for x in r]
         o = [x for x in recs if x.lmbda == lm]
         op, orr = np.mean([x.psnr_db for x in o]), np.mean([x.rate_bpp for x in o])
-        tol_p = PSNR_MARGIN_DB + spread_p
+        tol_p = PSNR_MARGIN_DB + max(max(rp) - min(rp), spread_dbg)
+        tol_r = RATE_MARGIN + (max(rr) - min(rr)) / np.mean(rr)
         its = int(np.median([x.iterations for x in o]))
-        lines.append(f"{image} c3x lambda {lm}: PSNR ref {r['psnr_db']:.3f} gpu {op:.3f} (tol {tol_p:.2f}), "
-                     f"rate ref {r['rate_bpp']:.4f} gpu {orr:.4f}, iterations ref {r['iterations']} gpu median {its} "
-                     f"(min {min(x.iterations for x in o)}, max {max(x.iterations for x in o)})")
-        assert abs(op - r["psnr_db"]) <= tol_p, lines[-1]
-        assert abs(orr / r["rate_bpp"] - 1) <= 2 * RATE_MARGIN, lines[-1]
+        lines.append(f"{image} c3x lambda {lm}: PSNR ref {np.mean(rp):.3f} ({min(rp):.3f}..{max(rp):.3f}) gpu {op:.3f} "
+                     f"(tol {tol_p:.2f}), rate ref {np.mean(rr):.4f} gpu {orr:.4f} (tol {tol_r:.2f}), iterations ref "
+                     f"{ri} gpu median {its} (min {min(x.iterations for x in o)}, max {max(x.iterations for x in o)})")
+        assert abs(op - np.mean(rp)) <= tol_p, lines[-1]
+        assert abs(orr / np.mean(rr) - 1) <= tol_r, lines[-1]
         # patience early stopping as train.py:226-240: the same iteration counts (the third
         # phase stops when its loss stops improving; 2 % covers a record taken at one more
         # validation)
-        assert abs(its - r["iterations"]) <= 0.02 * r["iterations"], lines[-1]
+        assert abs(its - np.mean(ri)) <= 0.02 * np.mean(ri), lines[-1]
     R1, P1, _ = rd.curve(ref)
     R2, P2, _ = rd.curve(recs)
     bd = rd.bd_rate(R1, P1, R2, P2)
