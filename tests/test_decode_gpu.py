@@ -120,6 +120,26 @@ def test_hip_decode_batch_repeated_streams(gpu, ccmi_lib):
 
 
 @pytest.mark.gpu
+def test_hip_decode_batch_chunked_mixed_geometries(gpu, ccmi_lib):
+    """A batch of >= 64 streams takes the overlapped path (dec_host.cpp: frames in two
+    cost-ordered chunks, each chunk's ARM launch and decoder tail on its own HIP stream): the
+    committed JVET B / D / E streams (1080p, 240p, 720p; YUV output) twice over in ONE call, and
+    the Kodak + CLIC streams (768 x 512 to 2048 x 1365, portrait included; RGB -> PPM) eight
+    times over in another, so that both chunks hold several geometries and copies of one stream
+    land in either chunk; every output equals the reference decoder's."""
+    from ccmi import decode
+    jvet = [f for f in FILES if f.name[:2] in ("B-", "D-", "E-")]
+    rgb = [f for f in FILES if f.name.startswith("kodim")] + CLIC
+    for fs, yuv in ((jvet * 2, True), (rgb * 8, False)):
+        assert len(fs) >= 64
+        outs = decode.decode_batch([f.read_bytes() for f in fs], as_yuv=yuv)
+        for f, o in zip(fs, outs):
+            assert hashlib.md5(o).hexdigest() == MD5[_key(f)]["md5"], f.name
+        t = decode.last_timing()
+        assert t["arm_cabac"] > 0 and t["ups_syn_out"] >= 0
+
+
+@pytest.mark.gpu
 @pytest.mark.parametrize("bd,chroma,ext", [(10, 420, ".yuv"), (8, 444, ".yuv"), (10, 444, ".yuv"), (8, 0, ".ppm"),
                                            (16, 0, ".ppm")])
 def test_hip_output_variants_match_oracle(bd, chroma, ext, gpu, ccmi_lib, oracle_c, tmp_path):
