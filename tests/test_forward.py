@@ -186,6 +186,31 @@ def test_hip_forward_matches_oracle_random(H, W, seed, gpu, ccmi_lib):
     np.testing.assert_allclose(s[0].cpu().numpy(), ref["syn"].numpy(), atol=_tol(ref["syn"].numpy()))
 
 
+def _with_kernel_sizes(mp, K, Kp, seed):
+    """mp with random upsampling (K taps, even) and refine (Kp taps, odd) half kernels: the
+    reference's --ups_k_size / --ups_preconcat_k_size (upsampling.py:233-292, :110-150)."""
+    g = torch.Generator().manual_seed(100 + seed)
+    hu, hp = (K + 1) // 2, (Kp + 1) // 2
+    mp.ups_half = [0.3 * torch.randn(hu, generator=g) for _ in mp.ups_half]
+    mp.pre_half = [0.1 * torch.randn(hp, generator=g) for _ in mp.pre_half]
+    mp.ups_k, mp.pre_k = K, Kp
+    return mp
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("K,Kp", [(4, 1), (4, 3), (6, 5), (8, 1), (8, 9), (10, 7)])
+def test_hip_upsampling_kernel_sizes(K, Kp, gpu, ccmi_lib):
+    """Every upsampling / refine kernel size the reference's CLI allows (not only the default
+    8 / 7): the per-level launch against the oracle, at an odd size that exercises the crop."""
+    mp = _with_kernel_sizes(fo.ModelParams.random(45, 83, seed=K + Kp), K, Kp, K * Kp)
+    g = torch.Generator().manual_seed(K + Kp)
+    lat = [0.5 * torch.randn(h, w, generator=g) for h, w in mp.sizes]
+    ref = fo.forward(mp, lat)
+    a, u, s = _hip_forward([mp], [lat], gpu)
+    np.testing.assert_allclose(u[0].cpu().numpy(), ref["ups"].numpy(), atol=_tol(ref["ups"].numpy()))
+    np.testing.assert_allclose(s[0].cpu().numpy(), ref["syn"].numpy(), atol=_tol(ref["syn"].numpy()))
+
+
 @pytest.mark.gpu
 def test_hip_batch_of_frames_with_own_weights(gpu, ccmi_lib):
     """A batch of independent frames, each with its own network, in one launch sequence."""

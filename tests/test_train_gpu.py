@@ -217,6 +217,42 @@ def test_gpu_noise_and_quantizers_match_oracle(qtype, ntype, gpu):
     _check_grads(gout[0].cpu().numpy(), st, to.golden_param_names(meta))
 
 
+@pytest.mark.parametrize("K,Kp", [(4, 3), (6, 1), (6, 5), (8, 1), (8, 5), (8, 9)])
+def test_gpu_gradients_other_kernel_sizes(K, Kp, gpu):
+    """The upsampling backward for every kernel-size pair the training step accepts (the goldens
+    hold the default 8 / 7 only): K = 8 runs the one-launch-per-level kernel (t_lvl_bwd), 4 / 6
+    the separate refine / transposed-conv kernels.  Against the oracle's autograd, softround
+    with a given noise tensor, at an odd size so every level crops."""
+    import forward_oracle as fo
+    import train_oracle as to
+    from ccmi import train as T
+    H, W = 45, 70
+    mp = fo.ModelParams.random(H, W, seed=K + Kp)
+    g = torch.Generator().manual_seed(10 * K + Kp)
+    mp.ups_half = [0.3 * torch.randn((K + 1) // 2, generator=g) for _ in mp.ups_half]
+    mp.pre_half = [0.1 * torch.randn((Kp + 1) // 2, generator=g) for _ in mp.pre_half]
+    mp.ups_k, mp.pre_k = K, Kp
+    arch = T.Arch(H, W, ups_k=K, pre_k=Kp)
+    lat = [0.05 * torch.randn(h, w, generator=g) for h, w in mp.sizes]
+    target = torch.rand(3, H, W, generator=g)
+    st = to.TrainState(mp, lat)
+    noise = to.kumaraswamy(torch.rand(arch.n_latents, generator=g), 2.0)
+    to.grads(st, target, "softround", 0.3, 1e-3, False, noise=noise)
+    of = T.Overfitter(arch, torch.cat([x.reshape(-1) for x in lat])[None].to(gpu),
+                      T.pack_params(mp.arm, mp.ups_half, mp.pre_half, mp.syn)[None].to(gpu),
+                      target.reshape(1, -1).to(gpu), yuv420=False)
+    gout = torch.zeros(1, of.N + of.P, device=gpu)
+    of.step("softround", "kumaraswamy", 0.3, 2.0, 1e-3, update=False, noise=noise[None].to(gpu), grad_out=gout)
+    torch.cuda.synchronize()
+    got = gout[0].cpu().numpy()
+    o = 0
+    for i, p in enumerate(st.params()):
+        n = p.numel()
+        _grad_close(got[o:o + n], p.grad.reshape(-1).numpy(), f"K={K} Kp={Kp} tensor {i}" +
+                    (" latent_grids" if i < mp.n_grids else ""))
+        o += n
+
+
 def test_gpu_batch_of_frames_each_with_own_network(gpu):
     """Frames in a batch are independent: frame b's gradient equals a batch-of-1 run."""
     z = np.load(FILES[1])
