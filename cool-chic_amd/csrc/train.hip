@@ -485,10 +485,12 @@ __global__ __launch_bounds__(kT) __attribute__((amdgpu_waves_per_eu(3))) void t_
             row[D] = valid ? g_q : 0.f;
         }
         __syncthreads();
-        // halo row 0 receives nothing (context rows reach 3 rows up)
+        // the context of dims 8 / 16 reaches 3 rows up (halo row 0 receives nothing); that of
+        // dims 24 / 32 reaches 4 (offsets 4 and 2..5 of ctx_off: dy = -4)
+        constexpr int kR0 = D >= 24 ? 0 : 1;
 #pragma unroll 1
-        for (int i = threadIdx.x; i < (kALH - 1) * kALW; i += kT) {
-            const int r = 1 + i / kALW, c = i - (r - 1) * kALW;
+        for (int i = threadIdx.x; i < (kALH - kR0) * kALW; i += kT) {
+            const int r = kR0 + i / kALW, c = i - (r - kR0) * kALW;
             const int y = y0 - kAH + r, x = x0 - kAH + c;
             float v = 0.f;
             {   // own value: the latent at (r - kAH, c - kAH)

@@ -217,30 +217,34 @@ def test_gpu_noise_and_quantizers_match_oracle(qtype, ntype, gpu):
     _check_grads(gout[0].cpu().numpy(), st, to.golden_param_names(meta))
 
 
-@pytest.mark.parametrize("K,Kp", [(4, 3), (6, 1), (6, 5), (8, 1), (8, 5), (8, 9)])
-def test_gpu_gradients_other_kernel_sizes(K, Kp, gpu):
-    """The upsampling backward for every kernel-size pair the training step accepts (the goldens
-    hold the default 8 / 7 only): K = 8 runs the one-launch-per-level kernel (t_lvl_bwd), 4 / 6
-    the separate refine / transposed-conv kernels.  Against the oracle's autograd, softround
-    with a given noise tensor, at an odd size so every level crops."""
+def _random_arch_vs_oracle(gpu, H, W, seed, K=8, Kp=7, yuv420=False, **kw):
+    """Gradient of one softround + kumaraswamy step (the same noise tensor given to both) of a
+    random network against the oracle's autograd, at an odd size so every pyramid level crops.
+    kw: dim_arm / n_hidden / n_grids / layers for ModelParams.random and Arch."""
     import forward_oracle as fo
     import train_oracle as to
     from ccmi import train as T
-    H, W = 45, 70
-    mp = fo.ModelParams.random(H, W, seed=K + Kp)
-    g = torch.Generator().manual_seed(10 * K + Kp)
-    mp.ups_half = [0.3 * torch.randn((K + 1) // 2, generator=g) for _ in mp.ups_half]
-    mp.pre_half = [0.1 * torch.randn((Kp + 1) // 2, generator=g) for _ in mp.pre_half]
-    mp.ups_k, mp.pre_k = K, Kp
-    arch = T.Arch(H, W, ups_k=K, pre_k=Kp)
+    mp = fo.ModelParams.random(H, W, seed=seed, **kw)
+    g = torch.Generator().manual_seed(1000 + seed)
+    if (K, Kp) != (8, 7):
+        mp.ups_half = [0.3 * torch.randn((K + 1) // 2, generator=g) for _ in mp.ups_half]
+        mp.pre_half = [0.1 * torch.randn((Kp + 1) // 2, generator=g) for _ in mp.pre_half]
+        mp.ups_k, mp.pre_k = K, Kp
+    arch = T.Arch(H, W, dim_arm=mp.dim_arm, n_hidden=mp.n_hidden, layers=tuple(mp.layers), n_grids=mp.n_grids,
+                  ups_k=K, pre_k=Kp)
     lat = [0.05 * torch.randn(h, w, generator=g) for h, w in mp.sizes]
-    target = torch.rand(3, H, W, generator=g)
+    img = torch.rand(3, H, W, generator=g)
+    if yuv420:
+        target = {"y": img[0], "u": img[1, ::2, ::2], "v": img[2, ::2, ::2]}
+        tflat = torch.cat([target[c].reshape(-1) for c in "yuv"])
+    else:
+        target, tflat = img, img.reshape(-1)
     st = to.TrainState(mp, lat)
     noise = to.kumaraswamy(torch.rand(arch.n_latents, generator=g), 2.0)
-    to.grads(st, target, "softround", 0.3, 1e-3, False, noise=noise)
+    to.grads(st, target, "softround", 0.3, 1e-3, yuv420, noise=noise)
     of = T.Overfitter(arch, torch.cat([x.reshape(-1) for x in lat])[None].to(gpu),
                       T.pack_params(mp.arm, mp.ups_half, mp.pre_half, mp.syn)[None].to(gpu),
-                      target.reshape(1, -1).to(gpu), yuv420=False)
+                      tflat[None].to(gpu), yuv420=yuv420)
     gout = torch.zeros(1, of.N + of.P, device=gpu)
     of.step("softround", "kumaraswamy", 0.3, 2.0, 1e-3, update=False, noise=noise[None].to(gpu), grad_out=gout)
     torch.cuda.synchronize()
@@ -248,9 +252,38 @@ def test_gpu_gradients_other_kernel_sizes(K, Kp, gpu):
     o = 0
     for i, p in enumerate(st.params()):
         n = p.numel()
-        _grad_close(got[o:o + n], p.grad.reshape(-1).numpy(), f"K={K} Kp={Kp} tensor {i}" +
+        _grad_close(got[o:o + n], p.grad.reshape(-1).numpy(), f"{kw} K={K} Kp={Kp} tensor {i}" +
                     (" latent_grids" if i < mp.n_grids else ""))
         o += n
+
+
+@pytest.mark.parametrize("K,Kp", [(4, 3), (6, 1), (6, 5), (8, 1), (8, 5), (8, 9)])
+def test_gpu_gradients_other_kernel_sizes(K, Kp, gpu):
+    """The upsampling backward for every kernel-size pair the training step accepts (the goldens
+    hold the default 8 / 7 only): K = 8 runs the one-launch-per-level kernel (t_lvl_bwd), 4 / 6
+    the separate refine / transposed-conv kernels."""
+    _random_arch_vs_oracle(gpu, 45, 70, 10 * K + Kp, K, Kp)
+
+
+@pytest.mark.parametrize("dim_arm,n_hidden", [(8, 0), (16, 0), (16, 1), (16, 3), (24, 2), (32, 1), (32, 3)])
+def test_gpu_gradients_arm_variants(dim_arm, n_hidden, gpu):
+    """Every ARM the training step accepts (--dim_arm 8..32, --n_hidden_layers_arm 0..3): the
+    matrix-core ARM (dim 16) and the VALU ARM (8 / 24 / 32).  The goldens hold (8, 2), (16, 2)."""
+    _random_arch_vs_oracle(gpu, 37, 58, dim_arm + n_hidden, dim_arm=dim_arm, n_hidden=n_hidden)
+
+
+@pytest.mark.parametrize("n_grids,layers,yuv420", [
+    (2, "16-1-linear-relu|3-1-linear-none", False),
+    (4, "40-1-linear-relu|3-1-linear-none|3-3-residual-relu", True),
+    (5, "64-1-linear-relu|3-1-linear-relu|3-3-residual-relu|3-3-residual-relu|3-3-residual-none", False),
+    (7, "24-1-linear-relu|3-1-linear-none|3-3-linear-relu|3-3-residual-none", True),
+])
+def test_gpu_gradients_synthesis_and_grid_variants(n_grids, layers, yuv420, gpu):
+    """Latent-pyramid depth 2..7 (the 1x1 head's input width) and synthesis heads of 16..64
+    channels followed by 0..3 3x3 layers, residual or not, with 444 and 420 targets (even frame
+    size, as 420 needs; the coarser levels are odd and crop)."""
+    import forward_oracle as fo
+    _random_arch_vs_oracle(gpu, 42, 66, n_grids, n_grids=n_grids, layers=fo.parse_layers(layers), yuv420=yuv420)
 
 
 def test_gpu_batch_of_frames_each_with_own_network(gpu):
