@@ -14,11 +14,14 @@ Prints ONE JSON line (rank 0).  Also reports:
                   profile (profiles/*pmc*.json) when present;
   cpu_baseline -- the CPU oracle (torch fp32 restatement of the reference forward) on
                   a bounded sample of the same workload, on this host's cores.
-Side legs (same line): 1080p float forward, bit-exact .cool decode / encode (path B,
-streams sharded over ranks), and the encoder overfit on the Kodak-24 proxies (images
-sharded over ranks, per-image R-D records gathered to rank 0, compared with the
-reference's results/image/kodak/results.tsv rows).  Only the cpu_baseline legs import
-oracle/; the timed legs run libccmi alone.
+Side legs (same line): 1080p float forward, bit-exact .cool decode / encode (path B, a
+fixed number of streams per rank) with one-stream-at-a-time latency on the class-E / B /
+CLIC streams, and the encoder overfit on the Kodak-24 proxies (every rank the whole
+Kodak-24 at its own operating point, per-image R-D records gathered to rank 0, compared
+with the reference's results/image/kodak/results.tsv rows).  Every leg is weak-scaled: a
+rank's work depends on its rank, never on the world size, so `--as-rank R --as-world N`
+runs exactly rank R's share of an N-GPU job on one GPU.  Only the cpu_baseline legs import
+oracle/ (and run oracle/_ref); the timed legs run libccmi alone.
 """
 
 from __future__ import annotations
@@ -340,58 +343,98 @@ def _reduce(counters: dict, dist, dev, op="sum"):
     return D.reduce_counters(counters, op=op, device=dev) if dist else dict(counters)
 
 
-def bench_single_stream_decode(cls: str = "E", reps: int = 2):
+REF_DEC_TIMES = ROOT / "tests/golden/ref_dec_times.json"
+
+
+def _stream_set(cls: str):
+    """Committed streams of a class: "E" / "B" / "D" (JVET) or "CLIC" -> [(key in ref_md5.json, path)]."""
+    if cls == "CLIC":
+        fs = sorted((ROOT / "tests/golden/cool/clic").glob("*.cool"))
+        return [("clic20-pro-valid/" + f.name, f) for f in fs]
+    return [("jvet/" + f.name, f) for f in sorted((ROOT / "tests/golden/cool").glob(f"{cls}-*.cool"))]
+
+
+def _time_ref_one_core(path: Path, out: Path, reps: int):
+    """The reference decoder (oracle/_ref/ccdec_ref, built from the reference's own sources) on
+    one core, one stream: mean wall seconds over `reps` runs, or None when it is absent."""
+    import subprocess
+    ref = ROOT / "oracle" / "_ref" / "ccdec_ref"
+    if not ref.exists():
+        return None
+    ts = []
+    for _ in range(reps):
+        t0 = time.perf_counter()
+        subprocess.run([str(ref), f"--input={path}", f"--output={out}", "--avx2"], check=True,
+                       stdout=subprocess.DEVNULL)
+        ts.append(time.perf_counter() - t0)
+    return sum(ts) / len(ts)
+
+
+def bench_single_stream_decode(cls: str = "E", reps: int = 3, ref_reps: int = 2):
     """Path B latency, the drop-in case: ccmi_decode_file (cc_decode_cpu's replacement, file in
-    -> .yuv out: parse, upload, kernels, download, write) on each shipped class-`cls` stream,
-    ONE stream at a time, best of `reps` wall-clock runs, md5 checked against the reference
-    decoder's.  Compared with the reference decoder on one core (122.2 ms mean
-    over the 15 class-E streams, 284.3 over the class-B ones, ccdec --avx2)."""
-    import ctypes
+    -> .yuv / .ppm out: parse, upload, kernels, download, write) on each committed class-`cls`
+    stream, ONE stream at a time: mean and best of `reps` wall-clock runs per stream, md5 checked
+    against the reference decoder's.  Compared per stream with the reference decoder on one
+    core: its own results.tsv time (the authors' host, tests/golden/ref_dec_times.json) and, when
+    oracle/_ref is present, ccdec_ref --avx2 timed here on one core (mean of `ref_reps`)."""
     import hashlib
     import statistics
     import tempfile
     import ccmi
     md5 = json.loads((ROOT / "tests/golden/ref_md5.json").read_text())
-    files = sorted((ROOT / "tests/golden/cool").glob(f"{cls}-*.cool"))
+    tsv = json.loads(REF_DEC_TIMES.read_text())["streams"]
+    files = _stream_set(cls)
     L = ccmi.lib()
-    ms, exact = [], True
+    per, exact = [], True
     with tempfile.TemporaryDirectory() as td:
-        out = Path(td) / "o.yuv"
-        assert L.ccmi_decode_file(str(files[0]).encode(), str(out).encode(), 0, 0, 0, 0) == 0, ccmi.last_error()
-        for f in files:
-            best = None
+        for key, f in files:
+            out = Path(td) / ("o" + md5[key]["ext"])
+            assert L.ccmi_decode_file(str(f).encode(), str(out).encode(), 0, 0, 0, 0) == 0, ccmi.last_error()  # warm
+            ts = []
             for _ in range(reps):
                 t0 = time.perf_counter()
                 rc = L.ccmi_decode_file(str(f).encode(), str(out).encode(), 0, 0, 0, 0)
-                dt = time.perf_counter() - t0
+                ts.append(time.perf_counter() - t0)
                 assert rc == 0, ccmi.last_error()
-                best = dt if best is None else min(best, dt)
-            ms.append(best * 1e3)
-            exact &= hashlib.md5(out.read_bytes()).hexdigest() == md5["jvet/" + f.name]["md5"]
-    ref = {"E": 122.2, "B": 284.3}[cls]
-    return {"metric": "ccmi_decode_file wall ms per stream, one stream at a time (best of %d)" % reps,
-            "streams": len(files), "mean_ms": round(statistics.mean(ms), 2), "max_ms": round(max(ms), 2),
-            "min_ms": round(min(ms), 2), "reference_1core_mean_ms": ref,
-            "speedup_vs_reference_1core": round(ref / statistics.mean(ms), 3), "bit_exact_vs_reference_md5": exact}
+            exact &= hashlib.md5(out.read_bytes()).hexdigest() == md5[key]["md5"]
+            rel = str(f.relative_to(ROOT / "tests/golden/cool"))
+            r = {"stream": f.name, "mean_ms": round(statistics.mean(ts) * 1e3, 2), "best_ms": round(min(ts) * 1e3, 2),
+                 "reference_results_tsv_ms": round(tsv[rel]["dec_time_all_sec"] * 1e3, 2) if rel in tsv else None}
+            rt = _time_ref_one_core(f, Path(td) / ("r" + md5[key]["ext"]), ref_reps)
+            r["reference_1core_here_ms"] = round(rt * 1e3, 2) if rt is not None else None
+            per.append(r)
+    mean = statistics.mean(r["mean_ms"] for r in per)
+    out = {"metric": f"ccmi_decode_file wall ms per stream, one stream at a time (mean of {reps} runs; best alongside)",
+           "class": cls, "streams": len(per), "mean_ms": round(mean, 2),
+           "best_mean_ms": round(statistics.mean(r["best_ms"] for r in per), 2),
+           "max_ms": max(r["mean_ms"] for r in per), "bit_exact_vs_reference_md5": exact, "per_stream": per}
+    for k, name in (("reference_results_tsv_ms", "reference_results_tsv"), ("reference_1core_here_ms", "reference_1core_here")):
+        if all(r[k] for r in per):
+            ref = statistics.mean(r[k] for r in per)
+            out[f"{name}_mean_ms"] = round(ref, 2)
+            out[f"speedup_vs_{name}"] = round(ref / mean, 3)
+            out[f"streams_not_slower_than_{name}"] = sum(r["mean_ms"] <= r[k] for r in per)
+    return out
 
 
 def bench_bitexact_decode(reps: int, cls: str = "E", H=H, W=W, rank=0, world=1, dist=None, dev=None):
     """Path B: the bit-exact HIP decoder on the shipped JVET class-`cls` .cool streams
-    (class E: 15 files at 1280x720; class B: 5 committed files at 1920x1080).  The job is
-    `reps` copies of every stream; each rank decodes its round-robin share in ONE
-    ccmi_decode_batch call; output bytes are checked against the reference decoder's md5s.
-    Whole-job rate = all ranks' frames / the slowest rank's time."""
+    (class E: 15 files at 1280x720; class B: 5 committed files at 1920x1080).  Weak scaling:
+    every rank decodes its own `reps` copies of every stream (a fixed number of frames per
+    GPU) in ONE ccmi_decode_batch call; output bytes are checked against the reference
+    decoder's md5s.  Whole-job rate = all ranks' frames / the slowest rank's time."""
     import hashlib
     from ccmi import decode
-    from ccmi import dist as D
     md5 = json.loads((ROOT / "tests/golden/ref_md5.json").read_text())
     files = sorted((ROOT / "tests/golden/cool").glob(f"{cls}-*.cool"))
-    job = D.shard([f for _ in range(reps) for f in files], rank, world)
+    job = [f for _ in range(reps) for f in files]
     streams = [f.read_bytes() for f in job]
-    decode.decode_batch(streams[:2])
+    # warm-up: the whole batch once (sizes the pinned output pool and the cached device
+    # workspace, as a long-running decoder would have them), then the timed call
+    decode.decode_batch(streams, views=True)
     if dist: dist.barrier()
     t0 = time.perf_counter()
-    outs = decode.decode_batch(streams)
+    outs = decode.decode_batch(streams, views=True)
     wall = time.perf_counter() - t0
     tm = decode.last_timing()
     exact = all(hashlib.md5(o).hexdigest() == md5["jvet/" + f.name]["md5"] for f, o in zip(job, outs))
@@ -402,20 +445,23 @@ def bench_bitexact_decode(reps: int, cls: str = "E", H=H, W=W, rank=0, world=1, 
             "frames": n, "frames_per_gpu": len(job), "n_gpus": world,
             "value_kernels": round(n * H * W / t["kern_s"] / 1e6, 2),
             "value_wall_pcie_inclusive": round(n * H * W / t["wall"] / 1e6, 2), "unit": "Mpixel/s",
+            "wall_note": "host streams in -> decoded bytes in host memory (pinned pool, per-chunk downloads "
+                         "overlapped with the other chunk's ARM), header parse + weight decode included",
+            "per_gpu_kernels": round(len(job) * H * W / t["kern_s"] / 1e6, 2),
+            "per_gpu_wall": round(len(job) * H * W / t["wall"] / 1e6, 2),
             "stage_ms": {k: round(v, 3) for k, v in tm.items()},
             "bit_exact_vs_reference_md5": int(c["exact"]) == world,
-            "data": f"{len(files)} shipped JVET class-{cls} .cool bitstreams (results/image/jvet), x{reps}, "
-                    f"round-robin over ranks"}
+            "scaling": "weak",
+            "data": f"{len(files)} shipped JVET class-{cls} .cool bitstreams (results/image/jvet), x{reps} per GPU"}
 
 
 def bench_bitexact_encode(reps: int = 2, rank=0, world=1, dist=None, dev=None):
     """Path B writer: ccmi_encode_frame (GPU integer ARM over all latents + host CABAC, one
     thread per latent grid) re-encoding the shipped class-E streams from their decoded
-    latents (each rank its share); the output must equal the shipped bytes."""
+    latents (every rank all 15: weak scaling); the output must equal the shipped bytes."""
     from ccmi import decode, encode
-    from ccmi import dist as D
     import numpy as np
-    files = D.shard(sorted((ROOT / "tests/golden/cool").glob("E-*.cool")), rank, world)
+    files = sorted((ROOT / "tests/golden/cool").glob("E-*.cool"))
     jobs = []
     for f in files:
         data = f.read_bytes()
@@ -466,17 +512,35 @@ def encoder_flops_per_iteration(Hh, Wh):
     return 3 * (fl["arm"] + fl["ups"] + fl["syn"])
 
 
+# the reference's Kodak operating points (results/image/kodak/results.tsv), in the order ranks
+# take them: rank r of an N-GPU job encodes the Kodak-24 at REF_LAMBDAS[r % 5] with seed r // 5
+REF_LAMBDAS = (0.001, 0.0004, 0.004, 0.0001, 0.02)
+
+
+def encoder_shard(rank: int, lambdas=None):
+    """What one rank encodes (weak scaling, SURVEY §8e: images are independent units): the whole
+    Kodak-24 at its own operating point -- REF_LAMBDAS[rank % 5], seed rank // 5 -- so every rank
+    keeps full geometry batches (18 landscape + 6 portrait) and an N-GPU job covers the
+    reference's lambda set (N >= 5) as the reference's one-image-per-GPU SLURM array does
+    (sbatch-files/submit-coolchic-encoding.sh).  With explicit `lambdas`, every rank encodes
+    every image at each of them, seed = rank.  Returns ([lambda...], seed)."""
+    if lambdas:
+        return list(lambdas), rank
+    return [REF_LAMBDAS[rank % len(REF_LAMBDAS)]], rank // len(REF_LAMBDAS)
+
+
 def bench_encoder(images: int, scale: float, lambdas, rank: int, world: int, dist, dev):
     """Encoder overfit (BASELINE config 4): the c3x schedule (warm-up candidates + 3 phases +
     quantize_model, ccmi.train.overfit) on the first `images` Kodak proxies, RGB, hop decoder.
-    Images are sharded round-robin over ranks; each rank overfits its share grouped by
-    geometry (768x512 landscape / 512x768 portrait), one batch per group and lambda.
-    Geometry batches run concurrently (one host thread + HIP stream each).  Per-image
-    records are gathered to every rank (ccmi.dist.gather_records)."""
+    Every rank overfits its own encoder_shard (fixed work per GPU), grouped by geometry
+    (768x512 landscape / 512x768 portrait), one batch per group and lambda; the geometry
+    batches run concurrently (one host thread + HIP stream each).  Per-image records are
+    gathered to every rank (ccmi.dist.gather_records)."""
     from ccmi import decode, io, rd
     from ccmi import dist as D
     from ccmi import train as T
-    mine = D.shard(kodak_proxies()[:images], rank, world)
+    lms, seed = encoder_shard(rank, lambdas)
+    mine = kodak_proxies()[:images]
     recs, secs, kern = [], 0.0, 0.0
     if mine:
         outs = decode.decode_batch([s for _, s in mine], as_yuv=False)
@@ -486,38 +550,36 @@ def bench_encoder(images: int, scale: float, lambdas, rank: int, world: int, dis
             groups.setdefault(tuple(x.shape[-2:]), []).append((n, x))
         # one batch per geometry, the batches of different geometries run concurrently, each
         # from its own host thread on its own HIP stream (the small portrait batch alone
-        # would leave most of the GPU idle); CCMI_ENC_SERIAL=1 runs them one after another
+        # would leave most of the GPU idle)
         def run_group(key, stream):
             (Hh, Wh), items = key
             arch = T.Arch(Hh, Wh, dim_arm=DIM_ARM, n_hidden=N_HIDDEN, layers=HOP)
             out, flop = [], 0.0
             with torch.cuda.stream(stream):
                 tg = torch.stack([io.to_target(x, "rgb") for _, x in items]).to(dev)
-                for lm in lambdas:
-                    r = rd.encode_batch(tg, Hh, Wh, lm, arch, names=[n for n, _ in items], seeds=[rank] * len(items),
+                for lm in lms:
+                    r = rd.encode_batch(tg, Hh, Wh, lm, arch, names=[n for n, _ in items], seeds=[seed] * len(items),
                                         preset="c3x", scale=scale)
                     flop += encoder_flops_per_iteration(Hh, Wh) * sum(x.iterations for x in r)
                     out += r
             return out, flop
         keys = sorted(groups.items())
         torch.cuda.synchronize()
+        if dist: dist.barrier()
         t0 = time.perf_counter()
-        if len(keys) > 1 and not os.environ.get("CCMI_ENC_SERIAL"):
-            from concurrent.futures import ThreadPoolExecutor
-            streams = [torch.cuda.Stream(dev) for _ in keys]
-            with ThreadPoolExecutor(len(keys)) as ex:
-                results = list(ex.map(run_group, keys, streams))
-        else:
-            results = [run_group(k, torch.cuda.current_stream(dev)) for k in keys]
+        from concurrent.futures import ThreadPoolExecutor
+        streams = [torch.cuda.Stream(dev) for _ in keys]
+        with ThreadPoolExecutor(len(keys)) as ex:
+            results = list(ex.map(run_group, keys, streams))
         torch.cuda.synchronize()
         secs = time.perf_counter() - t0
         for r, f in results:
             recs += r
             kern += f
-    recs = D.gather_records([r.as_dict() for r in recs])
+    recs = D.gather_records([r.as_dict() for r in recs]) if dist else [r.as_dict() for r in recs]
     c = _reduce({"flop": kern}, dist, dev)
     t = _reduce({"s": secs}, dist, dev, op="max")
-    return recs, t["s"], c["flop"], secs
+    return recs, t["s"], c["flop"], secs, {"lambdas": lms, "seed": seed}
 
 
 def kodak_reference_rows():
@@ -531,6 +593,7 @@ def compare_with_reference(recs, lambdas):
     import numpy as np
     from ccmi import rd
     ref = {(r["seq_name"], round(r["lmbda"], 6)): r for r in kodak_reference_rows()}
+    lambdas = sorted({r["lmbda"] for r in recs}) if lambdas is None else lambdas
     out = {"lmbda": list(lambdas), "per_lambda": {}}
     for lm in lambdas:
         mine = [r for r in recs if abs(r["lmbda"] - lm) < 1e-9]
@@ -546,12 +609,11 @@ def compare_with_reference(recs, lambdas):
     if len(lambdas) >= 4:
         bds = []
         for name in sorted({r["image"] for r in recs}):
-            mine = sorted([r for r in recs if r["image"] == name], key=lambda r: r["lmbda"])
-            rr = [ref.get((name, round(r["lmbda"], 6))) for r in mine]
-            if None in rr:
+            R2, P2, lms = rd.curve([r for r in recs if r["image"] == name])  # seed means per lambda
+            rr = [ref.get((name, round(lm, 6))) for lm in lms]
+            if None in rr or len(lms) < 4:
                 continue
-            bds.append(rd.bd_rate([r["rate_bpp"] for r in rr], [r["psnr_db"] for r in rr],
-                                  [r["rate_bpp"] for r in mine], [r["psnr_db"] for r in mine]))
+            bds.append(rd.bd_rate([r["rate_bpp"] for r in rr], [r["psnr_db"] for r in rr], R2, P2))
         if bds:
             # proxies: encoded from the reference's own lambda = 1e-4 reconstructions, while
             # results.tsv was measured on the originals -- an operating-point check, not matched R-D
@@ -591,14 +653,14 @@ def cpu_encoder_baseline(iters: int = 2):
                             "source": "tests/golden/cpu_calibration.json (reference train step vs oracle, same host)"}}
 
 
-def cpu_decode_baseline(budget_s=10.0):
+def cpu_decode_baseline(budget_s=10.0, cls="E", H=H, W=W):
     """The reference C decoder (oracle/_ref, built from /root/reference sources) -- or the C oracle
-    when that binary is absent -- decoding the class-E streams, one process per core."""
+    when that binary is absent -- decoding the class-`cls` streams, one process per core."""
     import subprocess
     import tempfile
     ref = ROOT / "oracle" / "_ref" / "ccdec_ref"
     orc = ROOT / "oracle" / "_build" / "ccdec_oracle"
-    files = sorted((ROOT / "tests/golden/cool").glob("E-*.cool"))
+    files = sorted((ROOT / "tests/golden/cool").glob(f"{cls}-*.cool"))
     ncores = max(1, min(16, os.cpu_count() or 1))
     kind = "reference" if ref.exists() else "port"
     with tempfile.TemporaryDirectory() as td:
@@ -617,7 +679,7 @@ def cpu_decode_baseline(budget_s=10.0):
             frames += 1
         dt = time.perf_counter() - t0
     return {"value": round(frames * H * W / dt / 1e6, 3), "unit": "Mpixel/s", "cores": ncores, "kind": kind,
-            "sample": f"{frames} decodes of the 15 class-E 720p streams, {ncores} concurrent single-threaded "
+            "sample": f"{frames} decodes of the {len(files)} class-{cls} {W}x{H} streams, {ncores} concurrent single-threaded "
                       f"processes ({'reference ccdec --avx2' if kind == 'reference' else 'C oracle'}), {dt:.1f} s"}
 
 
@@ -649,8 +711,15 @@ def main():
     ap.add_argument("--encode-images", type=int, default=24,
                     help="Kodak proxies overfitted (the first N of kodim01..24, sharded over ranks; 0: skip)")
     ap.add_argument("--encode-scale", type=float, default=1.0, help="fraction of the c3x schedule to run")
-    ap.add_argument("--encode-lambdas", default="0.001",
-                    help="comma-separated lambdas of the encoder leg (4 or more: per-image BD-rate vs results.tsv)")
+    ap.add_argument("--encode-lambdas", default="",
+                    help="comma-separated lambdas of the encoder leg, every rank all of them (default: rank r "
+                         "encodes at REF_LAMBDAS[r %% 5]; 4 or more lambdas: per-image BD-rate vs results.tsv)")
+    ap.add_argument("--as-rank", type=int, default=None,
+                    help="run exactly rank R's shard of an --as-world N job on this one GPU, without "
+                         "torch.distributed (the per-GPU rate of one rank of the N-GPU job)")
+    ap.add_argument("--as-world", type=int, default=None)
+    ap.add_argument("--no-single-stream", action="store_true",
+                    help="skip the one-stream-at-a-time class-B / CLIC latency legs")
     ap.add_argument("--overlap", action="store_true",
                     help="run the ARM on a second HIP stream concurrently with the decode tail (the "
                          "step rate is the same within noise on MI355X; kernels then share CUs, so the "
@@ -672,6 +741,19 @@ def main():
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     dist = None
+    as_rank = None
+    if args.as_rank is not None:
+        # one rank's shard alone: every leg is weak-scaled (a rank's work depends on its rank,
+        # never on the world size), so this GPU does exactly what rank R of the N-GPU job does
+        if world != 1:
+            raise SystemExit("--as-rank runs one process (no torchrun)")
+        n = args.as_world or 8
+        if not 0 <= args.as_rank < n:
+            raise SystemExit(f"--as-rank must lie in [0, {n})")
+        as_rank = {"rank": args.as_rank, "world": n,
+                   "note": "one GPU running rank R's shard of an N-GPU job without torch.distributed; every "
+                           "number is this one GPU's (n_gpus 1)"}
+        rank = args.as_rank
     # CCMI_BENCH_BACKEND=gloo: rehearsal of the multi-rank path with several ranks on one
     # card (RCCL needs one GPU per rank); the driver's runs use the default, RCCL
     backend = os.environ.get("CCMI_BENCH_BACKEND", "nccl")
@@ -731,6 +813,7 @@ def main():
         "ms_per_step": round(dt / args.steps * 1e3, 4),
         "higher_is_better": True,
         "scaling": "weak",
+        "as_rank": as_rank,
         "vs_baseline": None,
         "dtype": "f32",
         "data": "synthetic (seeded N(0,0.5) latents, random-init hop weights per frame)",
@@ -767,29 +850,37 @@ def main():
         res["bitexact_decode"] = dec
         res["bitexact_encode"] = bench_bitexact_encode(rank=rank, world=world, dist=dist, dev=dev)
     if args.hd_decode_reps > 0:
-        res["bitexact_decode_1080p"] = bench_bitexact_decode(args.hd_decode_reps, "B", 1080, 1920, rank=rank,
-                                                             world=world, dist=dist, dev=dev)
+        dec = bench_bitexact_decode(args.hd_decode_reps, "B", 1080, 1920, rank=rank, world=world, dist=dist, dev=dev)
+        if rank == 0 and world == 1 and not args.no_cpu_baseline:
+            dec["cpu_baseline"] = cpu_decode_baseline(cls="B", H=1080, W=1920)
+        if rank == 0 and not args.no_single_stream:
+            dec["single_stream"] = bench_single_stream_decode("B")
+            dec["single_stream_clic"] = bench_single_stream_decode("CLIC")
+        res["bitexact_decode_1080p"] = dec
     if args.encode_images > 0:
-        lambdas = [float(x) for x in args.encode_lambdas.split(",") if x]
-        recs, secs, flop, my_secs = bench_encoder(args.encode_images, args.encode_scale, lambdas, rank, world, dist, dev)
-        n_enc = len(recs) // max(1, len(lambdas))
-        tot = n_enc * len(lambdas) / secs * 3600.0
+        lambdas = [float(x) for x in args.encode_lambdas.split(",") if x] or None
+        recs, secs, flop, my_secs, shard = bench_encoder(args.encode_images, args.encode_scale, lambdas, rank, world,
+                                                         dist, dev)
+        tot = len(recs) / secs * 3600.0
         ach = flop / secs / 1e12
         import numpy as np
         res["encoder_overfit"] = {
             "metric": "encoder images/hr (c3x schedule, Kodak-24 proxies 768x512 RGB, hop, all GPUs)",
             "value": round(tot, 2), "per_gpu": round(tot / world, 2), "unit": "images/hr", "n_gpus": world,
-            "images": n_enc, "lambdas": lambdas, "encodes": len(recs), "seconds_max_over_ranks": round(secs, 2),
+            "scaling": "weak", "encodes": len(recs), "encodes_per_gpu": len(recs) // max(1, world),
+            "shard": dict(shard, rank=rank), "lambdas": sorted({r["lmbda"] for r in recs}),
+            "seconds_max_over_ranks": round(secs, 2),
             "schedule": f"c3x x{args.encode_scale:g}: warm-up 5x400 + 2x400 candidates, phases 10600 + 1500 + 1000 "
                         f"iterations (mean {np.mean([r['iterations'] for r in recs]) if recs else 0:.0f} per image, "
                         f"patience early stops included); quantize_model after "
                         f"the second phase; images of one geometry and lambda overfit together as one batch, "
-                        f"the geometry batches concurrently on separate HIP streams",
+                        f"the geometry batches concurrently on separate HIP streams; rank r encodes the "
+                        f"Kodak-24 at lambda {list(REF_LAMBDAS)}[r % 5], seed r // 5 (fixed work per GPU)",
             "psnr_db_mean": round(float(np.mean([r["psnr_db"] for r in recs])), 3),
             "rate_bpp_mean": round(float(np.mean([r["rate_bpp"] for r in recs])), 4),
-            "vs_reference_results": compare_with_reference(recs, lambdas),
+            "vs_reference_results": compare_with_reference(recs, None),
             "records": [{k: (round(v, 5) if isinstance(v, float) else v) for k, v in r.items()
-                         if k in ("image", "lmbda", "psnr_db", "rate_bpp", "seconds")} for r in recs],
+                         if k in ("image", "lmbda", "seed", "psnr_db", "rate_bpp", "iterations")} for r in recs],
             "roofline": {"bound": "valu-fp32", "kernel": "whole overfit (all training kernels + host loop)",
                          "achieved": round(ach, 3), "peak": PEAK_FP32_TFLOPS, "unit": "TFLOP/s",
                          "frac": round(ach / PEAK_FP32_TFLOPS, 4),
@@ -799,7 +890,7 @@ def main():
                     "proxy, results.tsv against the original"}
         if rank == 0 and world == 1 and not args.no_cpu_baseline:
             res["encoder_overfit"]["cpu_baseline"] = cpu_encoder_baseline()
-    if rank == 0:
+    if rank == 0 or as_rank is not None:  # the process that speaks for the job
         print(json.dumps(res), flush=True)
     if dist:
         dist.destroy_process_group()

@@ -26,7 +26,7 @@ EXPORTED = [
     "ccmi_arm_forward_f32", "ccmi_arm_context_f32", "ccmi_arm_mlp_f32", "ccmi_ups_workspace_bytes", "ccmi_ups_forward_f32",
     "ccmi_syn_workspace_bytes", "ccmi_syn_forward_f32", "ccmi_post_f32", "ccmi_decode_forward_f32",
     "ccmi_decode_file", "ccmi_decode_batch", "ccmi_decode_output_size", "ccmi_decode_last_timing",
-    "ccmi_decode_latents", "ccmi_decode_batch_workspace_bytes", "ccmi_decode_batch_ws", "ccmi_decode_weights_i32",
+    "ccmi_decode_latents", "ccmi_decode_batch_workspace_bytes", "ccmi_decode_batch_plan", "ccmi_decode_batch_ws", "ccmi_decode_weights_i32",
     "ccmi_ups_workspace_bytes_i32", "ccmi_ups_forward_i32", "ccmi_syn_workspace_bytes_i32", "ccmi_syn_forward_i32",
     "ccmi_cool_parse", "ccmi_code_wb", "ccmi_decode_wb", "ccmi_code_latent_layer", "ccmi_arm_forward_i32",
     "ccmi_encode_frame", "ccmi_row_reduce_f32", "ccmi_train_param_count", "ccmi_train_workspace_bytes", "ccmi_train_step",

@@ -35,6 +35,8 @@ def _bind():
                                                         C.c_void_p]
         L.ccmi_decode_batch_ws.argtypes = [C.c_void_p, C.c_void_p, C.c_int, C.c_void_p, C.c_void_p, C.c_void_p, C.c_int,
                                            C.c_int, C.c_int, C.c_void_p, C.c_size_t, C.c_void_p]
+        L.ccmi_decode_batch_plan.argtypes = [C.c_void_p, C.c_void_p, C.c_int, C.c_int, C.c_int, C.c_int, C.c_void_p,
+                                             C.c_void_p]
         L._ccmi_dec_bound = True
     return L
 
@@ -54,31 +56,71 @@ def output_size(stream: bytes, output_bitdepth: int = 0, output_chroma_format: i
     return n.value
 
 
+class _PinnedPool:
+    """Grow-only pinned host buffer per thread for decode_batch's outputs: the decoder's
+    per-chunk downloads are then DMA copies that overlap the rest of the batch, and the
+    buffer is reused across calls (hipHostMalloc of a GB-sized buffer costs more than the
+    decode).  Like the reference decoder's frame_memory (cc-frame-decoder.cpp:1151), what
+    decode_batch(views=True) returns stays valid until the next call on this thread."""
+
+    def __init__(self):
+        import threading
+        self.tls = threading.local()
+
+    def get(self, nbytes: int):
+        import torch
+        t = getattr(self.tls, "buf", None)
+        if t is None or t.numel() < nbytes:
+            self.tls.buf = None
+            t = torch.empty(max(nbytes, 1 << 20), dtype=torch.uint8, pin_memory=True)
+            self.tls.buf = t
+        return t
+
+
+_POOL = _PinnedPool()
+
+
 def decode_batch(streams: Sequence[bytes], output_bitdepth: int = 0, output_chroma_format: int = 0,
-                 as_yuv: bool = True, stream_handle: int | None = None, workspace=None) -> list[bytes]:
+                 as_yuv: bool = True, stream_handle: int | None = None, workspace=None, views: bool = False) -> list:
     """Decode independent intra .cool streams in one batched launch sequence; returns the
-    bytes the reference decoder would write for each (YUV planes, or PPM).  workspace: an
-    optional caller-owned device buffer (a uint8 torch tensor of at least
-    decode_batch_workspace_bytes(...) bytes): ccmi_decode_batch_ws, no allocation inside."""
+    bytes the reference decoder would write for each (YUV planes, or PPM).
+
+    One header-only pass sizes the outputs and the device workspace
+    (ccmi_decode_batch_plan); the outputs land in a pinned host pool and the device
+    workspace comes from torch's caching allocator unless `workspace` (a uint8 CUDA tensor of
+    at least decode_batch_workspace_bytes(...) bytes) is given: ccmi_decode_batch_ws, no
+    allocation inside the library.  views=True returns memoryviews into the pool (no copy;
+    valid until the next call on this thread), otherwise bytes."""
+    import torch
     n = len(streams)
+    if n < 1:
+        raise ValueError("decode_batch: no streams")
     bufs = [C.create_string_buffer(s, len(s)) for s in streams]
-    sizes = [output_size(s, output_bitdepth, output_chroma_format, as_yuv) for s in streams]
-    outs = [C.create_string_buffer(k) for k in sizes]
     sp = (C.c_void_p * n)(*[C.cast(b, C.c_void_p) for b in bufs])
     ln = (C.c_size_t * n)(*[len(s) for s in streams])
-    op = (C.c_void_p * n)(*[C.cast(o, C.c_void_p) for o in outs])
-    cap = (C.c_size_t * n)(*sizes)
+    cap = (C.c_size_t * n)()
+    need = C.c_size_t(0)
+    L = _bind()
+    check(L.ccmi_decode_batch_plan(sp, ln, n, output_bitdepth, output_chroma_format, int(as_yuv), cap, C.byref(need)))
+    offs, tot = [], 0
+    for k in cap:
+        offs.append(tot)
+        tot += (int(k) + 255) // 256 * 256
+    pool = _POOL.get(tot)
+    base = pool.data_ptr()
+    op = (C.c_void_p * n)(*[base + o for o in offs])
     got = (C.c_size_t * n)()
+    dev = torch.device("cuda", torch.cuda.current_device())
     if stream_handle is None:
-        import torch
-        stream_handle = torch.cuda.current_stream().cuda_stream if torch.cuda.is_available() else None
+        stream_handle = torch.cuda.current_stream(dev).cuda_stream
     if workspace is None:
-        check(lib().ccmi_decode_batch(sp, ln, n, op, cap, got, output_bitdepth, output_chroma_format, int(as_yuv),
-                                      stream_handle))
-    else:
-        check(_bind().ccmi_decode_batch_ws(sp, ln, n, op, cap, got, output_bitdepth, output_chroma_format,
-                                           int(as_yuv), workspace.data_ptr(), workspace.numel(), stream_handle))
-    return [o.raw[: got[i]] for i, o in enumerate(outs)]
+        workspace = torch.empty(max(int(need.value), 256), dtype=torch.uint8, device=dev)
+    check(L.ccmi_decode_batch_ws(sp, ln, n, op, cap, got, output_bitdepth, output_chroma_format, int(as_yuv),
+                                 workspace.data_ptr(), workspace.numel(), stream_handle))
+    mv = memoryview(pool.numpy())
+    if views:
+        return [mv[o: o + got[i]] for i, o in enumerate(offs)]
+    return [bytes(mv[o: o + got[i]]) for i, o in enumerate(offs)]
 
 
 def decode_batch_workspace_bytes(streams: Sequence[bytes], output_bitdepth: int = 0, output_chroma_format: int = 0,

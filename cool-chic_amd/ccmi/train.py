@@ -413,11 +413,13 @@ def overfit(arch: Arch, targets: torch.Tensor, lmbda: float, yuv420: bool = True
     of = Overfitter(arch, lat, params, targets.repeat_interleave(n0, dim=0), yuv420=yuv420, seed=seed)
     ncand = n0
     # iterations per image as the reference's FrameEncoderManager.iterations_counter counts
-    # them: every warm-up candidate's, then the phases' (early stops included)
-    warm_its = 0
+    # them: the sum over the image's own warm-up candidates (trained one after another in
+    # warmup.py), then the phases' (early stops included).  Rows of `of` are image-major.
+    warm_its = [0] * B
     for i, (_, ph) in enumerate(warmup):
         res = run_phase(of, ph, lmbda, scale)
-        warm_its += ncand * max(of.phase_iterations)
+        for b in range(B):
+            warm_its[b] += sum(of.phase_iterations[b * ncand:(b + 1) * ncand])
         keep = warmup[i + 1][0] if i + 1 < len(warmup) else 1
         order = torch.argsort(res[:, 0].view(B, ncand), dim=1)[:, :keep]
         idx = (order + torch.arange(B, device=order.device)[:, None] * ncand).reshape(-1)
@@ -425,7 +427,7 @@ def overfit(arch: Arch, targets: torch.Tensor, lmbda: float, yuv420: bool = True
         ncand = keep
     best = None
     of.quantized = None
-    of.iterations = [warm_its] * of.B
+    of.iterations = list(warm_its)
     for ph in phases:
         best = run_phase(of, ph, lmbda, scale)
         of.iterations = [a + b for a, b in zip(of.iterations, of.phase_iterations)]

@@ -11,6 +11,7 @@
 
 #include <algorithm>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "ccmi_cabac.h"
@@ -72,7 +73,7 @@ Cabac<HostBytes> cabac_on(const uint8_t *p, int n)
 
 } // namespace
 
-int parse_and_decode_frame(const uint8_t *bs, size_t n, FrameHost &f)
+int parse_frame_header(const uint8_t *bs, size_t n, FrameHost &f)
 {
     Reader r{bs, n, 0, false};
     r.u(2);
@@ -115,6 +116,7 @@ int parse_and_decode_frame(const uint8_t *bs, size_t n, FrameHost &f)
     f.sig_blk = (signed char)r.u(1);
     Lqi arm{}, ups{}, syn{};
     Lqi *q[3] = {&arm, &ups, &syn};
+    static_assert(sizeof(Lqi) == sizeof(f.lqi[0]), "Lqi layout");
     for (auto *x : q) {
         x->qw = r.u(1);
         x->qb = r.u(1);
@@ -136,26 +138,57 @@ int parse_and_decode_frame(const uint8_t *bs, size_t n, FrameHost &f)
         if (r.u(1) != 1) return ccmi_set_error(CCMI_ERR_UNSUPPORTED, "only 1 feature per latent resolution");
     for (int i = 0; i < f.n_layers; ++i) f.lat_n[i] = (uint32_t)r.u(3);
     if (r.err) return ccmi_set_error(CCMI_ERR_BITSTREAM, "truncated frame header");
-    const uint8_t *arm_w = r.take(arm.nw), *arm_b = r.take(arm.nb < 0 ? 0 : arm.nb);
-    const uint8_t *ups_w = r.take(ups.nw);
+    f.wbytes[0] = r.take(arm.nw);
+    f.wbytes[1] = r.take(arm.nb < 0 ? 0 : arm.nb);
+    f.wbytes[2] = r.take(ups.nw);
     r.take(ups.nb < 0 ? 0 : ups.nb);
-    const uint8_t *syn_w = r.take(syn.nw), *syn_b = r.take(syn.nb < 0 ? 0 : syn.nb);
+    f.wbytes[3] = r.take(syn.nw);
+    f.wbytes[4] = r.take(syn.nb < 0 ? 0 : syn.nb);
     for (int i = 0; i < f.n_layers; ++i) f.lat_bytes[i] = r.take((int)f.lat_n[i]);
     if (r.err) return ccmi_set_error(CCMI_ERR_BITSTREAM, "truncated stream (payload shorter than the header says)");
     for (int l = 0, hh = f.h, ww = f.w; l < f.n_layers; ++l, hh = (hh + 1) / 2, ww = (ww + 1) / 2) {
         f.lh[l] = hh;
         f.lw[l] = ww;
     }
-
-    // ---- ARM (read_arm, cc-frame-decoder.cpp:201-258)
+    for (int i = 0; i < 3; ++i) memcpy(f.lqi[i], q[i], sizeof(Lqi));
     const int d = f.dim_arm;
     if (d != 8 && d != 16 && d != 24 && d != 32) return ccmi_set_error(CCMI_ERR_UNSUPPORTED, "dim_arm %d", d);
     if (f.n_hidden > 4) return ccmi_set_error(CCMI_ERR_UNSUPPORTED, "%d ARM hidden layers", f.n_hidden);
     if (arm.qw > 8 || arm.qb < 0 || arm.qb > 16) return ccmi_set_error(CCMI_ERR_BITSTREAM, "ARM q-step index");
+    if (ups.qw > 12 || f.n_ups < 1 || f.n_pre < 1 || f.ups_ks < 2 || f.pre_ks < 1)
+        return ccmi_set_error(CCMI_ERR_BITSTREAM, "upsampling header");
+    if (syn.qw > 12 || syn.qb < 0 || syn.qb > 24 || f.n_branches < 1 || f.n_branches > 8)
+        return ccmi_set_error(CCMI_ERR_BITSTREAM, "synthesis header");
+    size_t per_branch = 0;
+    {
+        int c = f.n_layers;
+        for (auto &L : f.layers) {
+            if (L.n_out < 1 || L.ks < 1 || (L.ks & 1) == 0) return ccmi_set_error(CCMI_ERR_UNSUPPORTED, "syn layer ks %d", L.ks);
+            per_branch += (size_t)L.n_out * c * L.ks * L.ks + L.n_out;
+            c = L.n_out;
+        }
+    }
+    if (f.layers.back().n_out < 3) return ccmi_set_error(CCMI_ERR_UNSUPPORTED, "synthesis must output >= 3 planes");
+    f.arm.assign((size_t)f.n_hidden * (d * d + d) + 2 * d + 2, 0);
+    f.ups.assign((size_t)f.n_ups * f.ups_ks + (size_t)f.n_pre * f.pre_ks, 0);
+    f.syn.assign(per_branch * f.n_branches, 0);
+    if (f.n_branches > 1) f.blend.assign(f.n_branches, 0);
+    return CCMI_OK;
+}
+
+int decode_frame_weights(FrameHost &f)
+{
+    Lqi arm{}, ups{}, syn{};
+    memcpy(&arm, f.lqi[0], sizeof(Lqi));
+    memcpy(&ups, f.lqi[1], sizeof(Lqi));
+    memcpy(&syn, f.lqi[2], sizeof(Lqi));
+    const uint8_t *arm_w = f.wbytes[0], *arm_b = f.wbytes[1], *ups_w = f.wbytes[2], *syn_w = f.wbytes[3],
+                  *syn_b = f.wbytes[4];
+    // ---- ARM (read_arm, cc-frame-decoder.cpp:201-258)
+    const int d = f.dim_arm;
     {
         auto cw = cabac_on(arm_w, arm.nw), cb = cabac_on(arm_b, arm.nb);
         const int ws = 8 - arm.qw, bsh = 16 - arm.qb;
-        f.arm.assign((size_t)f.n_hidden * (d * d + d) + 2 * d + 2, 0);
         int32_t *p = f.arm.data();
         for (int l = 0; l < f.n_hidden; ++l, p += d * d + d)
             if (!read_weights(cw, arm.sw, d * d, ws, kArmPrec, p) || !read_weights(cb, arm.sb, d, bsh, 2 * kArmPrec, p + d * d))
@@ -164,11 +197,8 @@ int parse_and_decode_frame(const uint8_t *bs, size_t n, FrameHost &f)
             return ccmi_set_error(CCMI_ERR_BITSTREAM, "ARM weights");
     }
     // ---- upsampling (read_ups :261-300): half kernels mirrored (decode_upsweights_qi)
-    if (ups.qw > 12 || f.n_ups < 1 || f.n_pre < 1 || f.ups_ks < 2 || f.pre_ks < 1)
-        return ccmi_set_error(CCMI_ERR_BITSTREAM, "upsampling header");
     {
         auto cw = cabac_on(ups_w, ups.nw);
-        f.ups.assign((size_t)f.n_ups * f.ups_ks + (size_t)f.n_pre * f.pre_ks, 0);
         int32_t *p = f.ups.data();
         auto sym = [&](int ks) {
             const int nw = (ks + 1) / 2;
@@ -183,26 +213,13 @@ int parse_and_decode_frame(const uint8_t *bs, size_t n, FrameHost &f)
             if (!sym(f.pre_ks)) return ccmi_set_error(CCMI_ERR_BITSTREAM, "upsampling weights");
     }
     // ---- synthesis (read_syn :302-353)
-    if (syn.qw > 12 || syn.qb < 0 || syn.qb > 24 || f.n_branches < 1 || f.n_branches > 8)
-        return ccmi_set_error(CCMI_ERR_BITSTREAM, "synthesis header");
     {
         auto cw = cabac_on(syn_w, syn.nw), cb = cabac_on(syn_b, syn.nb);
         const int ws = 12 - syn.qw, bsh = 24 - syn.qb;
         if (f.n_branches > 1) {
-            f.blend.assign(f.n_branches, 0);
             if (!read_weights(cw, syn.sw, f.n_branches, ws, kSynPrec, f.blend.data()))
                 return ccmi_set_error(CCMI_ERR_BITSTREAM, "blend weights");
         }
-        size_t per_branch = 0;
-        {
-            int c = f.n_layers;
-            for (auto &L : f.layers) {
-                if (L.n_out < 1 || L.ks < 1 || (L.ks & 1) == 0) return ccmi_set_error(CCMI_ERR_UNSUPPORTED, "syn layer ks %d", L.ks);
-                per_branch += (size_t)L.n_out * c * L.ks * L.ks + L.n_out;
-                c = L.n_out;
-            }
-        }
-        f.syn.assign(per_branch * f.n_branches, 0);
         int32_t *p = f.syn.data();
         for (int b = 0; b < f.n_branches; ++b) {
             int c = f.n_layers;
@@ -215,9 +232,15 @@ int parse_and_decode_frame(const uint8_t *bs, size_t n, FrameHost &f)
             }
         }
     }
-    if (f.layers.back().n_out < 3) return ccmi_set_error(CCMI_ERR_UNSUPPORTED, "synthesis must output >= 3 planes");
     return CCMI_OK;
 }
+
+int parse_and_decode_frame(const uint8_t *bs, size_t n, FrameHost &f)
+{
+    if (int rc = parse_frame_header(bs, n, f)) return rc;
+    return decode_frame_weights(f);
+}
+
 
 } // namespace ccmi
 
@@ -305,8 +328,33 @@ bool syn_weights_fit24(const FrameHost &f)
     return true;
 }
 
+// CABAC decode of every frame's network weights: host threads over the frames (each
+// stream's weights are an independent few-hundred-symbol decode, ~50-100 us)
+int decode_weights_all(std::vector<FrameHost> &fr)
+{
+    const int n = (int)fr.size();
+    const int T = n >= 32 ? std::max(1, std::min({8, n / 16, (int)std::thread::hardware_concurrency()})) : 1;
+    std::vector<int> rc(n, 0);
+    std::vector<std::string> msg(n);
+    auto work = [&](int t) {
+        for (int i = t; i < n; i += T)
+            if ((rc[i] = decode_frame_weights(fr[i])) != CCMI_OK) msg[i] = ccmi_last_error();
+    };
+    if (T == 1) {
+        work(0);
+    } else {
+        std::vector<std::thread> th;
+        for (int t = 1; t < T; ++t) th.emplace_back(work, t);
+        work(0);
+        for (auto &x : th) x.join();
+    }
+    for (int i = 0; i < n; ++i)
+        if (rc[i]) return ccmi_set_error(rc[i], "stream %d: %s", i, msg[i].c_str());
+    return CCMI_OK;
+}
+
 // ws / ws_bytes: caller-owned device workspace (NULL: one hipMalloc per call); need: when
-// not NULL, only the workspace size is computed (streams parsed, nothing launched).
+// not NULL, only the workspace size is computed (headers parsed, nothing decoded or launched).
 int decode_many(const uint8_t *const *streams, const size_t *lens, int n, uint8_t *const *outs, const size_t *caps,
                 size_t *sizes, int out_bitdepth, int out_chroma, int as_yuv, hipStream_t s,
                 int32_t *const *lat_out = nullptr, void *ws = nullptr, size_t ws_bytes = 0, size_t *need = nullptr)
@@ -316,7 +364,7 @@ int decode_many(const uint8_t *const *streams, const size_t *lens, int n, uint8_
     std::vector<OutFmt> of(n);
     for (int i = 0; i < n; ++i) {
         if (!streams[i]) return ccmi_set_error(CCMI_ERR_ARG, "decode: stream %d is NULL", i);
-        if (int rc = parse_and_decode_frame(streams[i], lens[i], fr[i])) {
+        if (int rc = parse_frame_header(streams[i], lens[i], fr[i])) {
             std::string m = ccmi_last_error();
             return ccmi_set_error(rc, "stream %d: %s", i, m.c_str());
         }
@@ -386,6 +434,11 @@ int decode_many(const uint8_t *const *streams, const size_t *lens, int n, uint8_
     size_t all_count = 0;
 #endif
 
+    if (need) {
+        *need = tot;
+        return CCMI_OK;
+    }
+    if (int rc = decode_weights_all(fr)) return rc;
     std::vector<uint8_t> host(cst, 0);
     for (int i = 0; i < n; ++i) {
         FrameHost &f = fr[i];
@@ -397,10 +450,6 @@ int decode_many(const uint8_t *const *streams, const size_t *lens, int n, uint8_
         memcpy(&host[p.syn_off], f.syn.data(), f.syn.size() * 4);
     }
 
-    if (need) {
-        *need = tot;
-        return CCMI_OK;
-    }
     uint8_t *dev = static_cast<uint8_t *>(ws);
     if (dev) {
         if (ws_bytes < tot) return ccmi_set_error(CCMI_ERR_ARG, "decode: workspace of %zu bytes, need %zu", ws_bytes, tot);
@@ -505,7 +554,7 @@ int decode_many(const uint8_t *const *streams, const size_t *lens, int n, uint8_
                                       hipMemcpyHostToDevice, s));
 
     // ---- decoder tail arguments; frames of one geometry with a fused synthesis (single
-    // branch) share one launch per stage (CCMI_DEC_TAIL_SERIAL=1: one frame at a time)
+    // branch) share one launch per stage
     std::vector<DecTailFrame> tail(n);
     for (int i = 0; i < n; ++i) {
         FrameHost &f = fr[i];
@@ -613,41 +662,76 @@ int decode_many(const uint8_t *const *streams, const size_t *lens, int n, uint8_
         }
         return CCMI_OK;
     };
-    // K > 1: streams forked from s after the uploads and joined back before the downloads
-    struct Fork {
-        std::vector<hipStream_t> st; // st[0] = the caller's stream (not destroyed)
-        std::vector<hipEvent_t> ev;  // [0] fork; per chunk c: [1 + 3c] start, [2 + 3c] ARM done, [3 + 3c] done
-        ~Fork()
-        {
-            for (size_t k = 1; k < st.size(); ++k)
-                if (st[k]) (void)hipStreamDestroy(st[k]);
-            for (auto x : ev)
-                if (x) (void)hipEventDestroy(x);
+    // the decoded bytes of chunk c: headers on the host, payloads copied back on the chunk's
+    // own stream right after its tail, so one chunk's download overlaps the other chunk's
+    // ARM chains (pinned output buffers make these real DMA copies; pageable ones are staged
+    // by the runtime)
+    auto download_chunk = [&](int c, hipStream_t cs) -> int {
+        for (int i = 0; i < n && outs; ++i) {
+            if (chunk_of[i] != c) continue;
+            if (of[i].header) memcpy(outs[i], of[i].hdr, of[i].header);
+            CCMI_HIP_CHECK(hipMemcpyAsync(outs[i] + of[i].header, dev + pl[i].out_off, of[i].payload,
+                                          hipMemcpyDeviceToHost, cs));
         }
-    } fk;
+        return CCMI_OK;
+    };
+    // K > 1: streams forked from s after the uploads; each chunk runs ARM -> tail -> download on
+    // its stream, and s waits for every chunk before it returns.  The extra stream and the
+    // events are created once per thread and device, and kept (never destroyed at exit, when
+    // the runtime may be gone).
+    struct ForkCache {
+        int device = -1;
+        std::vector<hipStream_t> st;
+        std::vector<hipEvent_t> ev; // [0] fork; per chunk c: [1 + 4c] start, [2 + 4c] ARM done, [3 + 4c] tail done, [4 + 4c] done
+    };
+    static thread_local ForkCache fk;
     if (K == 1) {
         if (int rc = launch_chunk(0, s, ev.ok ? ev.e[2] : nullptr)) return rc;
+        ev.rec(3, s);
+        if (int rc = download_chunk(0, s)) return rc;
     } else {
-        fk.st.assign(K, nullptr);
+        int device = 0;
+        CCMI_HIP_CHECK(hipGetDevice(&device));
+        if (fk.device != device || (int)fk.st.size() < K || fk.ev.size() < (size_t)(1 + 4 * K)) {
+            fk.device = -1; // rebuilt below; the old ones are left to the runtime
+            fk.st.assign(K, nullptr);
+            fk.ev.assign(1 + 4 * K, nullptr);
+            for (int c = 1; c < K; ++c) CCMI_HIP_CHECK(hipStreamCreateWithFlags(&fk.st[c], hipStreamNonBlocking));
+            for (auto &x : fk.ev) CCMI_HIP_CHECK(hipEventCreate(&x));
+            fk.device = device;
+        }
+        // an error after some chunks were queued: s still waits for them before the caller can
+        // reuse or free the workspace (the chunks' own streams never outlive it unjoined)
+        int started = 0;
+        auto join = [&]() {
+            for (int c = K - 1; c > K - 1 - started && c >= 1; --c) {
+                (void)hipEventRecord(fk.ev[4 + 4 * c], fk.st[c]);
+                (void)hipStreamWaitEvent(s, fk.ev[4 + 4 * c], 0);
+            }
+        };
         fk.st[0] = s;
-        fk.ev.assign(1 + 3 * K, nullptr);
-        for (int c = 1; c < K; ++c) CCMI_HIP_CHECK(hipStreamCreateWithFlags(&fk.st[c], hipStreamNonBlocking));
-        for (auto &x : fk.ev) CCMI_HIP_CHECK(hipEventCreate(&x));
         CCMI_HIP_CHECK(hipEventRecord(fk.ev[0], s));
         for (int c = K - 1; c >= 0; --c) { // the most expensive chunk first
             hipStream_t cs = fk.st[c];
-            if (c > 0) CCMI_HIP_CHECK(hipStreamWaitEvent(cs, fk.ev[0], 0));
-            CCMI_HIP_CHECK(hipEventRecord(fk.ev[1 + 3 * c], cs));
-            if (int rc = launch_chunk(c, cs, fk.ev[2 + 3 * c])) return rc;
-            CCMI_HIP_CHECK(hipEventRecord(fk.ev[3 + 3 * c], cs));
+            if (c > 0) {
+                if (hipStreamWaitEvent(cs, fk.ev[0], 0) != hipSuccess) {
+                    join();
+                    return ccmi_set_error(CCMI_ERR_HIP, "decode: stream fork failed");
+                }
+                ++started;
+            }
+            (void)hipEventRecord(fk.ev[1 + 4 * c], cs);
+            int rc = launch_chunk(c, cs, fk.ev[2 + 4 * c]);
+            if (!rc) {
+                (void)hipEventRecord(fk.ev[3 + 4 * c], cs);
+                rc = download_chunk(c, cs);
+            }
+            if (rc) {
+                join();
+                return rc;
+            }
         }
-        for (int c = 1; c < K; ++c) CCMI_HIP_CHECK(hipStreamWaitEvent(s, fk.ev[3 + 3 * c], 0));
-    }
-    ev.rec(3, s);
-    for (int i = 0; i < n && outs; ++i) {
-        if (of[i].header) memcpy(outs[i], of[i].hdr, of[i].header);
-        CCMI_HIP_CHECK(hipMemcpyAsync(outs[i] + of[i].header, dev + pl[i].out_off, of[i].payload,
-                                      hipMemcpyDeviceToHost, s));
+        join();
     }
     ev.rec(4, s);
     for (int i = 0; i < n && lat_out; ++i)
@@ -668,18 +752,23 @@ int decode_many(const uint8_t *const *streams, const size_t *lens, int n, uint8_
     }
 #endif
     if (ev.ok) {
-        for (int k = 0; k < 4; ++k) (void)hipEventElapsedTime(&g_last_ms[k], ev.e[k], ev.e[k + 1]);
-        if (K > 1) {
+        if (K == 1) {
+            for (int k = 0; k < 4; ++k) (void)hipEventElapsedTime(&g_last_ms[k], ev.e[k], ev.e[k + 1]);
+        } else {
             // overlapped stages: ARM = the longest chunk's ARM (its start to its ARM end, events
-            // of one stream), tail = the rest of the kernel span
-            float span = 0.f, arm = 0.f;
-            (void)hipEventElapsedTime(&span, ev.e[1], ev.e[3]);
+            // of one stream), tail = from the uploads to the last chunk's tail minus that ARM,
+            // download = what is left after the last tail (the part not hidden under kernels)
+            float span = 0.f, arm = 0.f, all = 0.f;
+            (void)hipEventElapsedTime(&g_last_ms[0], ev.e[0], ev.e[1]);
+            (void)hipEventElapsedTime(&all, ev.e[1], ev.e[4]);
             for (int c = 0; c < K; ++c) {
                 float t = 0.f;
-                if (hipEventElapsedTime(&t, fk.ev[1 + 3 * c], fk.ev[2 + 3 * c]) == hipSuccess) arm = std::max(arm, t);
+                if (hipEventElapsedTime(&t, fk.ev[1 + 4 * c], fk.ev[2 + 4 * c]) == hipSuccess) arm = std::max(arm, t);
+                if (hipEventElapsedTime(&t, ev.e[1], fk.ev[3 + 4 * c]) == hipSuccess) span = std::max(span, t);
             }
             g_last_ms[1] = arm;
             g_last_ms[2] = span - arm;
+            g_last_ms[3] = all - span;
             (void)hipGetLastError(); // a timing query that failed must not surface in the next call
         }
     }
@@ -700,7 +789,7 @@ extern "C" int ccmi_decode_output_size(const uint8_t *stream, size_t len, int ou
 {
     if (!stream || !size) return ccmi_set_error(CCMI_ERR_ARG, "decode_output_size: null argument");
     FrameHost f;
-    if (int rc = parse_and_decode_frame(stream, len, f)) return rc;
+    if (int rc = parse_frame_header(stream, len, f)) return rc;
     OutFmt o;
     if (int rc = out_format(f, out_bitdepth, out_chroma, as_yuv, o)) return rc;
     *size = o.header + o.payload;
@@ -722,6 +811,14 @@ extern "C" int ccmi_decode_batch_workspace_bytes(const uint8_t *const *streams, 
     if (!streams || !lens || !bytes) return ccmi_set_error(CCMI_ERR_ARG, "decode_batch_workspace_bytes: null argument");
     return decode_many(streams, lens, n, nullptr, nullptr, nullptr, out_bitdepth, out_chroma, as_yuv, nullptr, nullptr,
                        nullptr, 0, bytes);
+}
+
+extern "C" int ccmi_decode_batch_plan(const uint8_t *const *streams, const size_t *lens, int n, int out_bitdepth,
+                                      int out_chroma, int as_yuv, size_t *out_sizes, size_t *workspace_bytes)
+{
+    if (!streams || !lens || !out_sizes || !workspace_bytes) return ccmi_set_error(CCMI_ERR_ARG, "decode_batch_plan: null argument");
+    return decode_many(streams, lens, n, nullptr, nullptr, out_sizes, out_bitdepth, out_chroma, as_yuv, nullptr, nullptr,
+                       nullptr, 0, workspace_bytes);
 }
 
 extern "C" int ccmi_decode_batch_ws(const uint8_t *const *streams, const size_t *lens, int n, uint8_t *const *out,

@@ -33,6 +33,10 @@ struct FrameHost {
     int lh[CCMI_MAX_GRIDS] = {}, lw[CCMI_MAX_GRIDS] = {};
     const uint8_t *lat_bytes[CCMI_MAX_GRIDS] = {};
     uint32_t lat_n[CCMI_MAX_GRIDS] = {};
+    // network substreams (arm w / b, ups w, syn w / b) and their q-step records (qw, qb, sw,
+    // sb, nw, nb for arm / ups / syn), kept by the header parse for decode_frame_weights
+    const uint8_t *wbytes[5] = {};
+    int lqi[3][6] = {};
     // decoded networks
     std::vector<int32_t> arm;   // per hidden layer: W[d][d] (out, in) then b[d]; then Wout[2][d], bout[2]
     std::vector<int32_t> ups;   // n_ups kernels of ups_ks taps, then n_pre kernels of pre_ks taps (mirrored)
@@ -44,6 +48,11 @@ struct FrameHost {
 // Parses the GOP + first frame of `bs` and decodes its weights.  Returns CCMI_OK or an
 // error code (message set).  Pointers in `f` alias `bs`.
 int parse_and_decode_frame(const uint8_t *bs, size_t n, FrameHost &f);
+// The two halves: headers only (geometry, architecture, substream sizes; the weight arrays
+// sized, not filled) -- enough to plan memory and output sizes -- then the CABAC decode of
+// the network weights.
+int parse_frame_header(const uint8_t *bs, size_t n, FrameHost &f);
+int decode_frame_weights(FrameHost &f);
 
 // Descriptor of one latent-layer CABAC stream for the ARM decode kernel.
 struct ArmStreamDesc {

@@ -1888,7 +1888,8 @@ struct AdamArgs {
 // per-frame bias corrections when frames carry their own Adam step (a frame whose optimizer
 // state was reloaded from its best record, train.py:226-236): computed in double like the
 // host path (torch.optim.Adam's bias_correction1/2 are Python floats); step <= 0 freezes
-// the frame (lr 0)
+// the frame: its parameters AND its Adam moments stay as they are (marked by a negative
+// second entry, which t_adam checks first)
 __global__ void t_adam_bc(const int32_t *__restrict__ steps, double lr, double beta1, double beta2, int B,
                           float *__restrict__ bc)
 {
@@ -1897,7 +1898,7 @@ __global__ void t_adam_bc(const int32_t *__restrict__ steps, double lr, double b
     const int t = steps[b];
     if (t <= 0) {
         bc[2 * b] = 0.f;
-        bc[2 * b + 1] = 1.f;
+        bc[2 * b + 1] = -1.f;
         return;
     }
     bc[2 * b] = (float)(lr / (1.0 - pow(beta1, (double)t)));
@@ -1911,6 +1912,7 @@ __global__ void t_adam(const float *__restrict__ G, float *__restrict__ lat, flo
     const int b = blockIdx.y;
     const int64_t i = (int64_t)blockIdx.x * kT + threadIdx.x;
     if (i >= A.n || (A.latents_only && i >= A.N)) return;
+    if (A.bc && A.bc[2 * b + 1] < 0.f) return; // frozen frame (adam_steps <= 0)
     float coef = 1.f;
     if (A.clip > 0.f) coef = fminf(A.clip / (sqrtf(acc4[b * 4 + 2]) + 1e-6f), 1.f);
     const float g = G[(int64_t)b * A.gstride + i] * coef;

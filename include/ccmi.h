@@ -220,10 +220,15 @@ int ccmi_row_reduce_f32(const float *a, int64_t a_stride, const float *t, int64_
                         int mode, double *out, void *stream);
 
 /* ccmi_decode_batch with a caller-owned device workspace (no allocation inside):
- * ccmi_decode_batch_workspace_bytes() parses the streams and returns the size the same
- * arguments need; the workspace must be 256-byte aligned. */
+ * ccmi_decode_batch_workspace_bytes() parses the streams' headers and returns the size the
+ * same arguments need; the workspace must be 256-byte aligned.  ccmi_decode_batch_plan()
+ * returns both the workspace size and every stream's output size (out_sizes[n]) from one
+ * header-only pass (no CABAC, no GPU work).  Output buffers in pinned host memory make the
+ * downloads real DMA copies that overlap the rest of the batch. */
 int ccmi_decode_batch_workspace_bytes(const uint8_t *const *streams, const size_t *lens, int n,
                                       int out_bitdepth, int out_chroma, int as_yuv, size_t *bytes);
+int ccmi_decode_batch_plan(const uint8_t *const *streams, const size_t *lens, int n, int out_bitdepth,
+                           int out_chroma, int as_yuv, size_t *out_sizes, size_t *workspace_bytes);
 int ccmi_decode_batch_ws(const uint8_t *const *streams, const size_t *lens, int n,
                          uint8_t *const *out, const size_t *out_caps, size_t *out_sizes,
                          int out_bitdepth, int out_chroma, int as_yuv, void *workspace,
@@ -416,7 +421,8 @@ typedef struct ccmi_train_args {
                                the built-in lmbda / (H W) */
     const int32_t *adam_steps; /* optional device [batch]: each frame's own Adam step (overrides
                                `step`; a frame whose optimizer state was reloaded from its best
-                               record, train.py:226-236); a step <= 0 leaves that frame unchanged */
+                               record, train.py:226-236); a step <= 0 leaves that frame unchanged:
+                               neither its parameters nor its Adam moments are written */
 } ccmi_train_args;
 size_t ccmi_train_param_count(const ccmi_train_args *args);
 size_t ccmi_train_workspace_bytes(const ccmi_train_args *args);

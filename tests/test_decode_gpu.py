@@ -140,6 +140,39 @@ def test_hip_decode_batch_chunked_mixed_geometries(gpu, ccmi_lib):
 
 
 @pytest.mark.gpu
+def test_hip_decode_batch_c_abi_pageable_and_views(gpu, ccmi_lib):
+    """ccmi_decode_batch itself (library-allocated workspace, caller's pageable output buffers,
+    sizes from ccmi_decode_batch_plan) on >= 64 streams, i.e. the two-chunk path with its
+    per-chunk downloads; then decode_batch(views=True) (pinned pool, no copies) on the same
+    streams, twice, so the second call reuses the pool.  Every output equals the reference's."""
+    import ctypes as C
+    import torch
+    from ccmi import decode
+    fs = [f for f in FILES if f.name[:2] in ("D-", "E-")] * 2
+    assert len(fs) >= 64
+    data = [f.read_bytes() for f in fs]
+    n = len(data)
+    L = decode._bind()
+    bufs = [C.create_string_buffer(d, len(d)) for d in data]
+    sp = (C.c_void_p * n)(*[C.cast(b, C.c_void_p) for b in bufs])
+    ln = (C.c_size_t * n)(*[len(d) for d in data])
+    cap, need = (C.c_size_t * n)(), C.c_size_t(0)
+    assert L.ccmi_decode_batch_plan(sp, ln, n, 0, 0, 1, cap, C.byref(need)) == 0
+    assert need.value > 0 and all(int(c) == MD5[_key(f)]["bytes"] for f, c in zip(fs, cap))
+    outs = [C.create_string_buffer(int(c)) for c in cap]
+    op = (C.c_void_p * n)(*[C.cast(o, C.c_void_p) for o in outs])
+    got = (C.c_size_t * n)()
+    rc = ccmi_lib.ccmi_decode_batch(sp, ln, n, op, cap, got, 0, 0, 1, C.c_void_p(torch.cuda.current_stream().cuda_stream))
+    assert rc == 0, decode.lib().ccmi_last_error()
+    for f, o, g in zip(fs, outs, got):
+        assert hashlib.md5(o.raw[:g]).hexdigest() == MD5[_key(f)]["md5"], f.name
+    for _ in range(2):
+        views = decode.decode_batch(data, views=True)
+        for f, v in zip(fs, views):
+            assert isinstance(v, memoryview) and hashlib.md5(v).hexdigest() == MD5[_key(f)]["md5"], f.name
+
+
+@pytest.mark.gpu
 @pytest.mark.parametrize("bd,chroma,ext", [(10, 420, ".yuv"), (8, 444, ".yuv"), (10, 444, ".yuv"), (8, 0, ".ppm"),
                                            (16, 0, ".ppm")])
 def test_hip_output_variants_match_oracle(bd, chroma, ext, gpu, ccmi_lib, oracle_c, tmp_path):

@@ -98,6 +98,30 @@ def test_bench_reference_comparison_and_proxies():
         assert v["psnr_db_mean"] == v["reference_psnr_db_mean"] and v["images"] == 2
 
 
+def test_bench_encoder_shards_are_weak_scaled():
+    """A rank's encoder work depends on its rank only: the Kodak-24 at REF_LAMBDAS[r % 5] with
+    seed r // 5, so rank R of any N-GPU job does the work of --as-rank R; 8 ranks cover the
+    reference's 5 operating points with distinct (lambda, seed) pairs."""
+    import importlib.util
+    from pathlib import Path
+    root = Path(__file__).resolve().parents[1]
+    spec = importlib.util.spec_from_file_location("bench_mod2", root / "bench.py")
+    bench = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(bench)
+    shards = [bench.encoder_shard(r) for r in range(8)]
+    assert shards[0] == ([0.001], 0)
+    assert len({(lm[0], sd) for lm, sd in shards}) == 8
+    assert {lm[0] for lm, _ in shards} == {0.0001, 0.0004, 0.001, 0.004, 0.02}
+    assert bench.encoder_shard(3, [0.02, 0.001]) == ([0.02, 0.001], 3)
+    # seeds of one (image, lambda) are averaged before the BD fit
+    rows = {(r["seq_name"], r["lmbda"]): r for r in bench.kodak_reference_rows()}
+    lms = [0.02, 0.004, 0.001, 0.0004]
+    recs = [{"image": "kodim05", "lmbda": lm, "psnr_db": rows[("kodim05", lm)]["psnr_db"] + d,
+             "rate_bpp": rows[("kodim05", lm)]["rate_bpp"]} for lm in lms for d in (-0.1, 0.1)]
+    c = bench.compare_with_reference(recs, None)
+    assert c["bd_rate_images"] == 1 and abs(c["bd_rate_vs_results_tsv_on_proxies_pct_mean"]) < 1e-6
+
+
 @pytest.mark.gpu
 def test_bench_two_ranks_gloo_on_one_gpu(tmp_path):
     """bench.py's multi-rank path end to end: torch.distributed.run with 2 ranks on the one
@@ -114,15 +138,44 @@ def test_bench_two_ranks_gloo_on_one_gpu(tmp_path):
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2",
            "--master-addr=127.0.0.1", f"--master-port={_free_port()}", str(root / "bench.py"), "--gpus", "2",
            "--steps", "2", "--warmup", "1", "--batch", "2", "--hd-steps", "0", "--decode-reps", "1",
-           "--hd-decode-reps", "1", "--encode-images", "3", "--encode-scale", "0.002", "--no-cpu-baseline"]
+           "--hd-decode-reps", "1", "--encode-images", "3", "--encode-scale", "0.002", "--no-cpu-baseline",
+           "--no-single-stream"]
     p = subprocess.run(cmd, cwd=root, env=env, capture_output=True, text=True, timeout=110)
     assert p.returncode == 0, p.stderr[-3000:]
     line = [x for x in p.stdout.splitlines() if x.startswith("{")]
     assert len(line) == 1, p.stdout[-2000:]
     r = json.loads(line[0])
     assert r["n_gpus"] == 2 and r["per_gpu"] * 2 == pytest.approx(r["value"], rel=1e-3)
-    assert r["bitexact_decode"]["frames"] == 15 and r["bitexact_decode"]["bit_exact_vs_reference_md5"]
-    assert r["bitexact_decode_1080p"]["frames"] == 5
-    assert r["bitexact_encode"]["identical_to_shipped_streams"] and r["bitexact_encode"]["frames"] == 30
+    # weak scaling: every rank decodes its own copy of the stream set, encodes the 3 images
+    # at its own lambda (rank 0: 1e-3, rank 1: 4e-4)
+    assert r["bitexact_decode"]["frames"] == 30 and r["bitexact_decode"]["bit_exact_vs_reference_md5"]
+    assert r["bitexact_decode"]["frames_per_gpu"] == 15
+    assert r["bitexact_decode_1080p"]["frames"] == 10
+    assert r["bitexact_encode"]["identical_to_shipped_streams"] and r["bitexact_encode"]["frames"] == 60
     e = r["encoder_overfit"]
-    assert sorted(x["image"] for x in e["records"]) == ["kodim01", "kodim02", "kodim03"]
+    assert e["encodes"] == 6 and e["encodes_per_gpu"] == 3
+    assert sorted((x["image"], x["lmbda"]) for x in e["records"]) == sorted(
+        (f"kodim0{i}", lm) for i in (1, 2, 3) for lm in (0.001, 0.0004))
+
+
+@pytest.mark.gpu
+def test_bench_as_rank_runs_one_shard():
+    """--as-rank R --as-world N: rank R's shard of an N-GPU job alone on this GPU (no
+    torch.distributed); the encoder leg takes rank R's operating point."""
+    import json
+    import subprocess
+    import sys
+    from pathlib import Path
+    root = Path(__file__).resolve().parents[1]
+    cmd = [sys.executable, str(root / "bench.py"), "--as-rank", "6", "--as-world", "8", "--steps", "2", "--warmup",
+           "1", "--batch", "2", "--hd-steps", "0", "--decode-reps", "1", "--hd-decode-reps", "0", "--encode-images",
+           "2", "--encode-scale", "0.002", "--no-cpu-baseline", "--no-single-stream"]
+    env = dict(os.environ, OMP_NUM_THREADS="2")
+    p = subprocess.run(cmd, cwd=root, env=env, capture_output=True, text=True, timeout=110)
+    assert p.returncode == 0, p.stderr[-3000:]
+    r = json.loads([x for x in p.stdout.splitlines() if x.startswith("{")][0])
+    assert r["n_gpus"] == 1 and r["as_rank"]["rank"] == 6 and r["as_rank"]["world"] == 8
+    assert r["bitexact_decode"]["frames"] == 15 and r["bitexact_decode"]["bit_exact_vs_reference_md5"]
+    e = r["encoder_overfit"]
+    assert e["shard"] == {"lambdas": [0.0004], "seed": 1, "rank": 6}
+    assert sorted(x["image"] for x in e["records"]) == ["kodim01", "kodim02"]

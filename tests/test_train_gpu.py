@@ -265,10 +265,11 @@ def test_gpu_gradients_other_kernel_sizes(K, Kp, gpu):
     _random_arch_vs_oracle(gpu, 45, 70, 10 * K + Kp, K, Kp)
 
 
-@pytest.mark.parametrize("dim_arm,n_hidden", [(8, 0), (16, 0), (16, 1), (16, 3), (24, 2), (32, 1), (32, 3)])
+@pytest.mark.parametrize("dim_arm,n_hidden", [(d, nh) for d in (8, 16, 24, 32) for nh in range(4)])
 def test_gpu_gradients_arm_variants(dim_arm, n_hidden, gpu):
-    """Every ARM the training step accepts (--dim_arm 8..32, --n_hidden_layers_arm 0..3): the
-    matrix-core ARM (dim 16) and the VALU ARM (8 / 24 / 32).  The goldens hold (8, 2), (16, 2)."""
+    """Every ARM the training step accepts (--dim_arm 8..32 x --n_hidden_layers_arm 0..3, the
+    full product): the matrix-core ARM (dim 16) and the VALU ARM (8 / 24 / 32; 24 and 32 gather
+    context row 4 above the tile).  The goldens hold (8, 2), (16, 2)."""
     _random_arch_vs_oracle(gpu, 37, 58, dim_arm + n_hidden, dim_arm=dim_arm, n_hidden=n_hidden)
 
 
@@ -349,3 +350,95 @@ def test_gpu_c3x_schedule_short(gpu):
     torch.cuda.synchronize()
     assert of.B == 2 and torch.isfinite(best).all()
     assert bool((best[:, 0] < init[:, 0]).all())
+
+
+def _adam_pair(gpu, k):
+    """A 2-frame batch (frames with different networks) after k - 1 clipped-Adam steps, so
+    its moments are non-zero; returns the Overfitter and a deep copy of its state."""
+    z = np.load(FILES[1])
+    of, st, target, meta = _setup(z, gpu, batch=2)
+    torch.manual_seed(0)
+    of.params[1] += 0.01 * torch.randn_like(of.params[1])
+    for _ in range(k - 1):
+        of.step("ste", "none", 1e-4, 1.0, 1e-3, lr=1e-2)
+    state = [x.clone() for x in (of.latents, of.params, of.m, of.v, of.steps)]
+    return of, state, meta
+
+
+def _restore(of, state, t):
+    for dst, src in zip((of.latents, of.params, of.m, of.v, of.steps), state):
+        dst.copy_(src)
+    of.t = t
+
+
+def test_gpu_per_frame_adam_steps_uniform_equals_scalar(gpu):
+    """adam_steps = [k, k] (the per-frame bias-correction path, t_adam_bc) gives the update of
+    the scalar step = k path: the same parameters, latents and moments."""
+    k = 4
+    of, state, meta = _adam_pair(gpu, k)
+    of.step("ste", "none", 1e-4, 1.0, 1e-3, lr=1e-2)        # scalar path, step k
+    scalar = [x.clone() for x in (of.latents, of.params, of.m, of.v)]
+    _restore(of, state, k - 1)
+    of.steps_uniform = False                                  # per-frame path, steps [k, k]
+    of.step("ste", "none", 1e-4, 1.0, 1e-3, lr=1e-2)
+    torch.cuda.synchronize()
+    assert of.steps.tolist() == [k, k]
+    for a, b, name in zip((of.latents, of.params, of.m, of.v), scalar, ("latents", "params", "m", "v")):
+        # same formula in double on host and device, rounded once to fp32; the gradients of
+        # two launches may differ in summation order (atomics), hence the ulp-level bound
+        torch.testing.assert_close(a, b, rtol=1e-5, atol=1e-8, msg=name)
+
+
+def test_gpu_per_frame_adam_steps_diverging(gpu):
+    """Frames of one batch at their own Adam steps [k1, k2] move as the scalar path moves them at
+    k1 (frame 0) and at k2 (frame 1); a frame at step <= 0 keeps its parameters and moments."""
+    k1, k2 = 2, 7
+    of, state, meta = _adam_pair(gpu, 3)
+    ref = {}
+    for k in (k1, k2):
+        _restore(of, state, k - 1)
+        of.step("ste", "none", 1e-4, 1.0, 1e-3, lr=1e-2)
+        ref[k] = [x.clone() for x in (of.latents, of.params, of.m, of.v)]
+    _restore(of, state, 0)
+    of.steps.copy_(torch.tensor([k1 - 1, k2 - 1], dtype=torch.int32))
+    of.steps_uniform = False
+    of.step("ste", "none", 1e-4, 1.0, 1e-3, lr=1e-2)
+    torch.cuda.synchronize()
+    assert of.steps.tolist() == [k1, k2]
+    for b, k in ((0, k1), (1, k2)):
+        for a, r, name in zip((of.latents, of.params, of.m, of.v), ref[k], ("latents", "params", "m", "v")):
+            torch.testing.assert_close(a[b], r[b], rtol=1e-5, atol=1e-8, msg=f"frame {b} step {k} {name}")
+    # the two bias corrections really differ: the frames did not both take one of them
+    d1 = (ref[k1][1][0] - state[1][0]).abs().max()
+    d2 = (ref[k2][1][0] - state[1][0]).abs().max()
+    assert abs(float(d1) / float(d2) - 1) > 0.2
+    # step <= 0: frozen frame (parameters, latents and Adam moments untouched)
+    _restore(of, state, 0)
+    of.steps.copy_(torch.tensor([-1, k2 - 1], dtype=torch.int32))
+    of.steps_uniform = False
+    of.step("ste", "none", 1e-4, 1.0, 1e-3, lr=1e-2)
+    torch.cuda.synchronize()
+    for a, s0, name in zip((of.latents, of.params, of.m, of.v), state, ("latents", "params", "m", "v")):
+        assert torch.equal(a[0], s0[0]), f"frozen frame changed its {name}"
+    torch.testing.assert_close(of.params[1], ref[k2][1][1], rtol=1e-5, atol=1e-8)
+
+
+def test_gpu_run_phase_reload_uses_per_frame_steps(gpu):
+    """A cosine phase with a short patience on a real Overfitter: frames whose loss stalls
+    reload their best parameters AND Adam state (train.py:226-236), which sends the batch down
+    the per-frame Adam-step path; the phase ends on every frame's best record."""
+    from ccmi import train as T
+    z = np.load(FILES[1])
+    of, st, target, meta = _setup(z, gpu, batch=2)
+    torch.manual_seed(1)
+    of.params[1] += 0.01 * torch.randn_like(of.params[1])
+    # lr 0.5: the loss blows up after a few steps, so the records stop and patience expires
+    ph = T.Phase(lr=0.5, max_itr=40, freq_valid=2, patience=4, schedule_lr=True, end_lr=0.4,
+                 quantizer_type="ste", quantizer_noise_type="none", softround_temperature=(1e-4, 1e-4))
+    best = T.run_phase(of, ph, 1e-3)
+    torch.cuda.synchronize()
+    assert not of.steps_uniform, "no frame reloaded its optimizer state"
+    assert torch.isfinite(best).all()
+    assert of.phase_iterations == [40, 40]
+    # the phase restores each frame's best record: validating now gives the recorded loss
+    torch.testing.assert_close(of.validate(1e-3)[:, 0], best[:, 0], rtol=1e-5, atol=0)

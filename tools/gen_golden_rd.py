@@ -74,6 +74,11 @@ REF = Path("/root/reference")
 GOLD = ROOT / "tests" / "golden"
 HOP = dict(layers=["48-1-linear-relu", "3-1-linear-none", "3-3-residual-relu", "3-3-residual-none"],
            dim_arm=16, n_hidden=2)
+# the reference's default decoder (coolchic/utils/types.py:120-143): 40-wide synthesis head,
+# ARM "24,2" -- the dim-24 ARM whose training gradients take the 4-rows-up context path
+DEFAULT_ARCH = dict(layers=["40-1-linear-relu", "3-1-linear-none", "3-3-residual-relu", "3-3-residual-none"],
+                    dim_arm=24, n_hidden=2)
+ARCHS = {"hop": HOP, "default": DEFAULT_ARCH}
 LAMBDAS = [0.02, 0.004, 0.001, 0.0004]
 SEEDS = [0, 1]
 C3X_SCALE = 0.1
@@ -163,9 +168,10 @@ def encode(x: torch.Tensor, preset_cfg: PresetConfig, lmbda: float, seed: int, a
                        fe.coolchic_encoder.get_network_quantization_step().items()}}
 
 
-def run_rd(kind: str, out_path: Path, images=None, lambdas=None, seeds=None, scale: float = C3X_SCALE):
-    """kind: "debug" (debug preset) or "c3x" (c3x preset, every length x scale).  Runs
-    already in out_path are skipped, so an interrupted run resumes."""
+def run_rd(kind: str, out_path: Path, images=None, lambdas=None, seeds=None, scale: float = C3X_SCALE,
+           arch: str = "hop"):
+    """kind: "debug" (debug preset) or "c3x" (c3x preset, every length x scale); arch: a key
+    of ARCHS.  Runs already in out_path are skipped, so an interrupted run resumes."""
     targets = load_targets()
     res = json.loads(out_path.read_text()) if out_path.exists() else {"runs": []}
     done = {(r["image"], r["preset"], r["lmbda"], r["seed"]) for r in res["runs"]}
@@ -182,9 +188,9 @@ def run_rd(kind: str, out_path: Path, images=None, lambdas=None, seeds=None, sca
                 key = (name, tag, lm, s)
                 if key in done:
                     continue
-                r = encode(x, cfg, lm, s)
+                r = encode(x, cfg, lm, s, arch=ARCHS[arch])
                 r.update(image=name, preset=key[1], lmbda=lm, seed=s, H=int(x.shape[1]), W=int(x.shape[2]),
-                         arch="hop")
+                         arch=arch)
                 print(json.dumps(r), flush=True)
                 res["runs"].append(r)
                 out_path.write_text(json.dumps(res, indent=1))
@@ -380,6 +386,11 @@ if __name__ == "__main__":
         gen_bd(GOLD / "bd_reference.json")
     if what in ("debug", "all"):
         run_rd("debug", GOLD / "rd_reference_debug.json")
+    if what == "debug_default":  # the reference's default decoder (arm 24,2; 40-wide head)
+        if len(sys.argv) > 2:
+            torch.set_num_threads(int(sys.argv[2]))
+        run_rd("debug", GOLD / "rd_reference_debug_default.json", images=["kodim15_192x128", "kodim01_768x512"],
+               arch="default")
     if what in ("quant", "all"):
         gen_quant()
     if what in ("c3x", "all"):
