@@ -43,10 +43,19 @@ constexpr int kThreads = 256;
 //    clamp(oy + i) (replicate padding); rows whose image row lies outside the image
 //    or outside the stage's valid band are computed but never read or stored, which
 //    keeps control flow uniform.
-constexpr int kFThreads = 512;
-constexpr int kRW = 64, kRH = 32;
+// window height (and threads per workgroup) overridable at build time for the window-size
+// A/B of DESIGN.md 7 (tools/ab_fused_window.sh); the product build uses 32 rows, 512 threads
+#ifndef CCMI_FUSED_RH
+#define CCMI_FUSED_RH 32
+#endif
+#ifndef CCMI_FUSED_THREADS
+#define CCMI_FUSED_THREADS 512
+#endif
+constexpr int kFThreads = CCMI_FUSED_THREADS;
+constexpr int kRW = 64, kRH = CCMI_FUSED_RH;
 constexpr int kPlane = kRW * (kRH + 2); // LDS plane: window rows -1 .. kRH (guard rows)
 constexpr int kRowsPerThread = kRH / (kFThreads / kRW); // 4
+constexpr int kNW = kFThreads / 64;                     // waves per workgroup (8)
 
 // Fused-upsampling input (UPS = true): the window's CIN input channels are not read from
 // a [CIN][H][W] tensor but evaluated in the kernel from the level-1 stack and the
@@ -151,6 +160,9 @@ constexpr int fused_lds_floats(int cin, int cmid, bool ups)
 // the LDS fits three (<= 160 KB / 3), else 2
 constexpr int fused_wpe(int cin, int cmid, bool ups, bool mh = false)
 {
+#ifdef CCMI_FUSED_WPE
+    if (!mh) return CCMI_FUSED_WPE; // window-size A/B builds only
+#endif
     return !mh && 4 * fused_lds_floats(cin, cmid, ups) <= 160 * 1024 / 3 ? 6 : 4;
 }
 
@@ -231,7 +243,7 @@ __global__ __launch_bounds__(kFThreads) __attribute__((amdgpu_waves_per_eu(fused
     // the records are fetched right where they are staged (L2-resident: every workgroup of a
     // frame reads the same ones); holding them in registers across the upsampling phases
     // cost spill slots at the 80-VGPR budget
-    constexpr int kHeadRegs = kMaxHid * 16 / kFThreads;
+    constexpr int kHeadRegs = (kMaxHid * 16 + kFThreads - 1) / kFThreads;
     auto stage_head = [&]() {
         const int tid = threadIdx.x;
         float hv[kHeadRegs];
@@ -239,7 +251,7 @@ __global__ __launch_bounds__(kFThreads) __attribute__((amdgpu_waves_per_eu(fused
         for (int k = 0; k < kHeadRegs; ++k) {
             const int i = tid + k * kFThreads, j = i >> 4, f = i & 15;
             float v = 0.f;
-            if (A.n_head == 2 && j < A.hid) {
+            if (i < kMaxHid * 16 && A.n_head == 2 && j < A.hid) {
                 if (f < CIN) v = prm[A.w0_off + j * CIN + f];
                 else if (f == CIN) v = prm[A.b0_off + j];
                 else if (f <= CIN + CMID) v = prm[A.w1_off + (f - CIN - 1) * A.hid + j];
@@ -249,7 +261,7 @@ __global__ __launch_bounds__(kFThreads) __attribute__((amdgpu_waves_per_eu(fused
 #pragma unroll
         for (int k = 0; k < kHeadRegs; ++k) {
             const int i = tid + k * kFThreads, j = i >> 4, f = i & 15;
-            if (f <= CIN + CMID) s_head[j][hr(f)] = hv[k]; // other slots are never operands
+            if (i < kMaxHid * 16 && f <= CIN + CMID) s_head[j][hr(f)] = hv[k]; // other slots are never operands
         }
         if constexpr (MH) {
             // [tile][lane row][m][4 units]: the second layer's weights of the 4 hidden units a
@@ -283,23 +295,23 @@ __global__ __launch_bounds__(kFThreads) __attribute__((amdgpu_waves_per_eu(fused
 #pragma unroll
         for (int k = 0; k < 7; ++k) wr[k] = uprm[U.pre_off + k];
         const int jbase = Ya / 2 + FT::D0, ibase = Xa / 2 + FT::D0;
-        // Phases A + B are row-parallel and wave-private: wave wv owns the rows r = wv + 8u of
-        // a group's [GC][kHsRows] raw tile and the raw latent rows yr = wv + 8u; lane = column.
+        // Phases A + B are row-parallel and wave-private: wave wv owns the rows r = wv + kNW u of
+        // a group's [GC][kHsRows] raw tile and the raw latent rows yr = wv + kNW u; lane = column.
         // Row addresses are wave-uniform (scalar), so a load costs no VALU index math, and a
         // wave's horizontal passes read back only rows it wrote itself -- a wave-level fence
         // instead of a workgroup barrier between the raw tiles and the horizontal passes.
         const int wv = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
         const int lane = threadIdx.x & 63;
-        constexpr int kSR = GC * kHsRows, kSU = (kSR + 7) / 8; // a group's source rows, per wave
-        constexpr int kLU = (kHrRows + 7) / 8;                 // latent rows per wave
-        static_assert(kSW <= 64 && kTW <= 128 && kTW > 64 && kHsRows >= 8, "lane = raw column, one row wrap per step");
+        constexpr int kSR = GC * kHsRows, kSU = (kSR + kNW - 1) / kNW; // a group's source rows, per wave
+        constexpr int kLU = (kHrRows + kNW - 1) / kNW;         // latent rows per wave
+        static_assert(kSW <= 64 && kTW <= 128 && kTW > 64 && kHsRows >= kNW, "lane = raw column, one row wrap per step");
         const float *src = U.src + (int64_t)b * U.src_stride;
         const float *rs = U.ref_src + (int64_t)b * U.ref_stride;
         float sv[NG][kSU], tv[kLU][2];
         bool tin[2];
         // phase A: every group's raw rows and the latent tile, all loads in flight at once;
         // clamped source coordinates are always inside the stack.  (channel, row) of
-        // r = wv + 8u in 32-bit scalar registers (a frame's stack stays below 2 GB; checked
+        // r = wv + kNW u in 32-bit scalar registers (a frame's stack stays below 2 GB; checked
         // at launch)
         {
             const int splane = U.hs * U.ws;
@@ -309,9 +321,9 @@ __global__ __launch_bounds__(kFThreads) __attribute__((amdgpu_waves_per_eu(fused
             for (int G = 0; G < NG; ++G)
 #pragma unroll
                 for (int u = 0; u < kSU; ++u) {
-                    const int r = wv + 8 * u;
-                    // ch = r / kHsRows without a division: wv < 8 moves r past at most one boundary
-                    const int c0 = (8 * u) / kHsRows, tb = kHsRows * (c0 + 1) - 8 * u; // folded (u unrolled)
+                    const int r = wv + kNW * u;
+                    // ch = r / kHsRows without a division: wv < kNW moves r past at most one boundary
+                    const int c0 = (kNW * u) / kHsRows, tb = kHsRows * (c0 + 1) - kNW * u; // folded (u unrolled)
                     const int lc = c0 + (wv >= tb ? 1 : 0), jj = r - lc * kHsRows;
                     sv[G][u] = 0.f;
                     if ((u < kSU - 1 || r < kSR) && G * GC + lc < C) {
@@ -333,7 +345,7 @@ __global__ __launch_bounds__(kFThreads) __attribute__((amdgpu_waves_per_eu(fused
             }
 #pragma unroll
             for (int u = 0; u < kLU; ++u) {
-                const int yr = wv + 8 * u;
+                const int yr = wv + kNW * u;
                 const int Y = Ya - 3 + yr;
                 const int row = clampi(Y, U.hd - 1) * U.wd;
 #pragma unroll
@@ -357,14 +369,14 @@ __global__ __launch_bounds__(kFThreads) __attribute__((amdgpu_waves_per_eu(fused
             if constexpr (G > 0) __syncthreads(); // every wave done with the previous group
 #pragma unroll
             for (int u = 0; u < kSU; ++u) {
-                const int r = wv + 8 * u;
+                const int r = wv + kNW * u;
                 if ((u < kSU - 1 || r < kSR) && lane < kSW)
                     s_st[r * kSW + lane] = U.src_quant ? rintf(U.gain * sv[G][u]) : sv[G][u];
             }
             if constexpr (G == 0) {
 #pragma unroll
                 for (int u = 0; u < kLU; ++u) {
-                    const int yr = wv + 8 * u;
+                    const int yr = wv + kNW * u;
                     if (yr >= kHrRows) continue;
                     const int Y = Ya - 3 + yr;
                     const bool yin = Y >= 0 && Y < U.hd;
@@ -399,18 +411,18 @@ __global__ __launch_bounds__(kFThreads) __attribute__((amdgpu_waves_per_eu(fused
                 };
 #pragma unroll
                 for (int u = 0; u < kSU; u += 2) {
-                    const int r = wv + 8 * (u + hsel);
+                    const int r = wv + kNW * (u + hsel);
                     if (u + 1 < kSU - 1 || r < kSR) pair(r, k, xe);
                 }
                 if (odd) { // pair 32 of every row (window columns 63, 64)
-                    const int r = wv + 8 * lane;
+                    const int r = wv + kNW * lane;
                     if (lane < kSU && r < kSR) pair(r, 32, 63);
                 }
                 if constexpr (G == 0) {
                     // refine: lane = window column, 7-tap sliding window over the wave's latent rows
 #pragma unroll
                     for (int u = 0; u < kLU; ++u) {
-                        const int yr = wv + 8 * u;
+                        const int yr = wv + kNW * u;
                         if (yr >= kHrRows) continue;
                         const float *tr = s_yt + yr * kTW + lane;
                         float acc = 0.f;

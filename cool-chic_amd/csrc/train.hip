@@ -224,9 +224,12 @@ __device__ __forceinline__ void mfma_outer(const float *s_g, const float *s_a, v
     for (int mt = 0; mt < MT; ++mt) ca[mt] = 16 * mt + ln < R ? 16 * mt + ln : R;
 #pragma unroll
     for (int nt = 0; nt < NT; ++nt) cb[nt] = 16 * nt + ln < D ? 16 * nt + ln : D;
+    // K = rows in the order r = s + 16 lk: the two 16-lane groups of a 32-lane half read rows 16
+    // apart, 16 banks apart for the odd pitches D + 1 / R + 1 (4 s + lk put rows 1 apart:
+    // a 2-way conflict per read)
 #pragma unroll 4
     for (int s = 0; s < 16; ++s) {
-        const int r = 4 * s + lk;
+        const int r = s + 16 * lk;
         float bv[NT];
 #pragma unroll
         for (int nt = 0; nt < NT; ++nt) bv[nt] = s_a[r * (D + 1) + cb[nt]];
@@ -366,9 +369,11 @@ __global__ __launch_bounds__(kT) __attribute__((amdgpu_waves_per_eu(3))) void t_
         tile_geo(t, l, y0, x0);
         const int H = g.h[l], W = g.w[l];
         const float *src = yq + (int64_t)b * g.N + g.off[l];
+        int tid = threadIdx.x; // opaque: its tile-invariant indices are not hoisted and kept live
+        asm volatile("" : "+v"(tid));
 #pragma unroll
         for (int u = 0; u < kSU; ++u) {
-            const int i = threadIdx.x + u * kT;
+            const int i = tid + u * kT;
             const int r = i / kALW, c = i - r * kALW;
             const int y = y0 - kAH + r, x = x0 - kAH + c;
             pre[u] = (i < kALH * kALW && y >= 0 && y < H && x >= 0 && x < W) ? src[y * W + x] : 0.f;
@@ -488,14 +493,21 @@ __global__ __launch_bounds__(kT) __attribute__((amdgpu_waves_per_eu(3))) void t_
         // the context of dims 8 / 16 reaches 3 rows up (halo row 0 receives nothing); that of
         // dims 24 / 32 reaches 4 (offsets 4 and 2..5 of ctx_off: dy = -4)
         constexpr int kR0 = D >= 24 ? 0 : 1;
-#pragma unroll 1
-        for (int i = threadIdx.x; i < (kALH - kR0) * kALW; i += kT) {
+        // a fixed number of atomics per thread (positions past the halo or outside the grid add
+        // 0 at a clamped in-grid address): the next tile's staging then waits for its prefetch
+        // loads only, not for these atomics; indices from an opaque thread index (not hoisted)
+        constexpr int kGN = (kALH - kR0) * kALW, kGI = (kGN + kT - 1) / kT;
+        int tid = threadIdx.x;
+        asm volatile("" : "+v"(tid));
+#pragma unroll
+        for (int u = 0; u < kGI; ++u) {
+            const int i = tid + u * kT;
             const int r = kR0 + i / kALW, c = i - (r - kR0) * kALW;
             const int y = y0 - kAH + r, x = x0 - kAH + c;
             float v = 0.f;
             {   // own value: the latent at (r - kAH, c - kAH)
                 const int ly = r - kAH, lx = c - kAH;
-                if (ly >= 0 && lx >= 0 && lx < kATX) v = s_g[(ly * kATX + lx) * (D + 1) + D];
+                if (ly >= 0 && ly < kATY && lx >= 0 && lx < kATX) v = s_g[(ly * kATX + lx) * (D + 1) + D];
             }
 #pragma unroll
             for (int k = 0; k < D; ++k) {
@@ -504,7 +516,8 @@ __global__ __launch_bounds__(kT) __attribute__((amdgpu_waves_per_eu(3))) void t_
                 const int ly = r - kAH - dy, lx = c - kAH - dx;
                 if (ly >= 0 && ly < kATY && lx >= 0 && lx < kATX) v += s_g[(ly * kATX + lx) * (D + 1) + k];
             }
-            if (y >= 0 && y < H && x >= 0 && x < W && v != 0.f) atomicAdd(&gdst[y * W + x], v);
+            const bool in = i < kGN && y >= 0 && y < H && x >= 0 && x < W;
+            atomicAdd(&gdst[min(max(y, 0), H - 1) * W + min(max(x, 0), W - 1)], in ? v : 0.f);
         }
     }
     // ---- flush this wave's weight / bias gradients and rate
@@ -548,15 +561,11 @@ __global__ __launch_bounds__(kT) __attribute__((amdgpu_waves_per_eu(CCMI_ARM16_W
     const cfloat_ptr P = (cfloat_ptr)(size_t)(th + (int64_t)b * ps);
     float *sg = s_g + 64 * w * (D + 1), *sa = s_a + 64 * w * (D + 1);
 
-    float WA[NL][4], WT[NL][4], BI[NL][4];
-#pragma unroll
-    for (int L = 0; L < NH; ++L)
-#pragma unroll
-        for (int s = 0; s < 4; ++s) {
-            WA[L][s] = P[L * LS + ln * D + 4 * lk + s];   // A = W[j = ln][i = 4 lk + s]
-            WT[L][s] = P[L * LS + (4 * lk + s) * D + ln]; // A = W^T[i = ln][j = 4 lk + s]
-            BI[L][s] = P[L * LS + D * D + 4 * lk + s];    // bias of unit 4 lk + s
-        }
+    // the hidden layers' weights and biases in LDS (2.2 KB for two layers: the workgroup's LDS
+    // stays <= 40 KB, 4 workgroups per CU), read per tile as the MFMA A operands: held in
+    // registers (24 VGPRs) they pushed the kernel past 128 VGPRs into scratch
+    __shared__ __attribute__((aligned(16))) float s_w[NL][LS];
+    for (int i = threadIdx.x; i < NH * LS; i += kT) s_w[i / LS][i % LS] = P[i];
     const cfloat_ptr Wo = P + NH * LS;
     float WO0[4], WO1[4];
 #pragma unroll
@@ -565,19 +574,23 @@ __global__ __launch_bounds__(kT) __attribute__((amdgpu_waves_per_eu(CCMI_ARM16_W
         WO1[r] = Wo[D + 4 * lk + r];
     }
     const float bo0 = Wo[2 * D], bo1 = Wo[2 * D + 1];
-    // s_y offsets of the context inputs k = 4 lk + s
-    int coff[4];
+    // s_y offsets of the context inputs k = 4 lk + s, derived per tile from an opaque lane
+    // index (kept across the tile loop they were 4 more persistent VGPRs)
+    auto ctx_offsets = [&](int (&coff)[4]) {
+        int lko = lk;
+        asm volatile("" : "+v"(lko));
 #pragma unroll
-    for (int s = 0; s < 4; ++s) {
-        int o[4];
+        for (int s = 0; s < 4; ++s) {
+            int o[4];
 #pragma unroll
-        for (int q = 0; q < 4; ++q) {
-            int dy, dx;
-            ctx_off<D>(4 * q + s, dy, dx);
-            o[q] = dy * kALW + dx;
+            for (int q = 0; q < 4; ++q) {
+                int dy, dx;
+                ctx_off<D>(4 * q + s, dy, dx);
+                o[q] = dy * kALW + dx;
+            }
+            coff[s] = lko == 0 ? o[0] : lko == 1 ? o[1] : lko == 2 ? o[2] : o[3];
         }
-        coff[s] = lk == 0 ? o[0] : lk == 1 ? o[1] : lk == 2 ? o[2] : o[3];
-    }
+    };
 
     const v4f z4 = {0.f, 0.f, 0.f, 0.f};
     v4f acc_h[NL][1][1], accb_dummy[1];
@@ -608,9 +621,11 @@ __global__ __launch_bounds__(kT) __attribute__((amdgpu_waves_per_eu(CCMI_ARM16_W
         tile_geo(t, l, y0, x0);
         const int H = g.h[l], W = g.w[l];
         const float *src = yq + (int64_t)b * g.N + g.off[l];
+        int tid = threadIdx.x; // opaque: its tile-invariant indices are not hoisted and kept live
+        asm volatile("" : "+v"(tid));
 #pragma unroll
         for (int u = 0; u < kSU; ++u) {
-            const int i = threadIdx.x + u * kT;
+            const int i = tid + u * kT;
             const int r = i / kALW, c = i - r * kALW;
             const int y = y0 - kAH + r, x = x0 - kAH + c;
             pre[u] = (i < kALH * kALW && y >= 0 && y < H && x >= 0 && x < W) ? src[y * W + x] : 0.f;
@@ -634,23 +649,42 @@ __global__ __launch_bounds__(kT) __attribute__((amdgpu_waves_per_eu(CCMI_ARM16_W
         __syncthreads();
         const bool valid = (y0 + cy) < H && (x0 + cx) < W;
 
-        // ---- forward: X[L][g][r] = input / activation unit 4 lk + r of latent 16 g + ln
+        // ---- forward: X[L][g][r] = input / activation unit 4 lk + r of latent 16 g + ln.
+        // What the backward needs of the hidden activations is kept small: their ReLU masks as
+        // bits (bit 4 g + r of mask[L] = X[L + 1][g][r] > 0), and the input of the last hidden
+        // layer (X[NH - 1], NH >= 2) staged in this wave's rows of s_a right away, where that
+        // layer's weight-gradient MFMAs read it -- 32 fewer live VGPRs across the backward, so
+        // the kernel fits 4 waves / SIMD without spills (round 3: 168 VGPRs + 13 spilled, and
+        // the spill reloads' vmcnt(0) waited for the previous tile's gradient atomics)
         const float *yrow = &s_y[cy + kAH][kAH + ln];
+        int coff[4];
+        ctx_offsets(coff);
         float X[NH + 1][4][4];
+        uint32_t mask[NL];
+#pragma unroll
+        for (int L = 0; L < NL; ++L) mask[L] = 0u;
 #pragma unroll
         for (int gg = 0; gg < 4; ++gg)
 #pragma unroll
             for (int s = 0; s < 4; ++s) X[0][gg][s] = yrow[16 * gg + coff[s]];
 #pragma unroll
-        for (int L = 0; L < NH; ++L)
+        for (int L = 0; L < NH; ++L) {
+            // A = W[j = ln][i = 4 lk + s]; bias of unit 4 lk + r
+            const v4f WA = *reinterpret_cast<const v4f *>(&s_w[L][ln * D + 4 * lk]);
+            const v4f BI = *reinterpret_cast<const v4f *>(&s_w[L][D * D + 4 * lk]);
 #pragma unroll
             for (int gg = 0; gg < 4; ++gg) {
-                v4f acc = {BI[L][0], BI[L][1], BI[L][2], BI[L][3]};
+                v4f acc = BI;
 #pragma unroll
-                for (int s = 0; s < 4; ++s) acc = mfma4(WA[L][s], X[L][gg][s], acc);
+                for (int s = 0; s < 4; ++s) acc = mfma4(WA[s], X[L][gg][s], acc);
 #pragma unroll
-                for (int r = 0; r < 4; ++r) X[L + 1][gg][r] = fmaxf(acc[r] + X[L][gg][r], 0.f);
+                for (int r = 0; r < 4; ++r) {
+                    X[L + 1][gg][r] = fmaxf(acc[r] + X[L][gg][r], 0.f);
+                    mask[L] |= (X[L + 1][gg][r] > 0.f ? 1u : 0u) << (4 * gg + r);
+                    if (NH >= 2 && L + 1 == NH - 1) sa[(16 * gg + ln) * (D + 1) + 4 * lk + r] = X[L + 1][gg][r];
+                }
             }
+        }
         // output layer: partial dot products over this lane's 4 units, summed over the 4
         // lanes of the latent; group g's (mu, ls) kept by the lanes with lk == g
         float mu = 0.f, ls = 0.f;
@@ -705,22 +739,28 @@ __global__ __launch_bounds__(kT) __attribute__((amdgpu_waves_per_eu(CCMI_ARM16_W
             for (int gg = 0; gg < 4; ++gg)
 #pragma unroll
                 for (int r = 0; r < 4; ++r) {
-                    gz[gg][r] = X[L + 1][gg][r] > 0.f ? G[gg][r] : 0.f;
+                    gz[gg][r] = (mask[L] >> (4 * gg + r)) & 1u ? G[gg][r] : 0.f;
                     sg[(16 * gg + ln) * (D + 1) + 4 * lk + r] = gz[gg][r];
-                    // layer 0's input is the context, re-read from the tile (not kept live)
-                    sa[(16 * gg + ln) * (D + 1) + 4 * lk + r] = L == 0 ? yrow[16 * gg + coff[r]] : X[L][gg][r];
+                    // layer 0's input is the context, re-read from the tile (not kept live);
+                    // the last hidden layer's input was staged by the forward
+                    if (L == 0) sa[(16 * gg + ln) * (D + 1) + 4 * lk + r] = yrow[16 * gg + coff[r]];
+                    else if (L != NH - 1) sa[(16 * gg + ln) * (D + 1) + 4 * lk + r] = X[L][gg][r];
                 }
 #pragma unroll
             for (int r = 0; r < 4; ++r) accb[L][r] += (gz[0][r] + gz[1][r]) + (gz[2][r] + gz[3][r]);
             wave_lds_sync(); // each wave stages and reads only its own 64 rows
             mfma_outer<D, D, false>(sg, sa, acc_h[L], accb_dummy);
             wave_lds_sync();
-            // input gradient: W^T gz + gz (residual), K permuted like the forward
+            // input gradient: W^T gz + gz (residual), K permuted like the forward;
+            // A = W^T[i = ln][j = 4 lk + s]
+            float WT[4];
+#pragma unroll
+            for (int s = 0; s < 4; ++s) WT[s] = s_w[L][(4 * lk + s) * D + ln];
 #pragma unroll
             for (int gg = 0; gg < 4; ++gg) {
                 v4f acc = {gz[gg][0], gz[gg][1], gz[gg][2], gz[gg][3]};
 #pragma unroll
-                for (int s = 0; s < 4; ++s) acc = mfma4(WT[L][s], gz[gg][s], acc);
+                for (int s = 0; s < 4; ++s) acc = mfma4(WT[s], gz[gg][s], acc);
 #pragma unroll
                 for (int r = 0; r < 4; ++r) G[gg][r] = acc[r];
             }
@@ -733,14 +773,23 @@ __global__ __launch_bounds__(kT) __attribute__((amdgpu_waves_per_eu(CCMI_ARM16_W
             for (int r = 0; r < 4; ++r) sg[(16 * gg + ln) * (D + 1) + 4 * lk + r] = G[gg][r];
         sg[lane * (D + 1) + D] = g_q;
         __syncthreads();
-#pragma unroll 1
-        for (int i = threadIdx.x; i < (kALH - 1) * kALW; i += kT) {
+        // exactly two atomics per thread (positions past the halo, or outside the grid, add 0 at
+        // a clamped in-grid address): with a fixed count after the next tile's prefetch loads,
+        // the next tile's staging waits for those loads only (vmcnt(2)), not for these atomics
+        static_assert((kALH - 1) * kALW <= 2 * kT, "two gather positions per thread");
+        // the positions' tile-invariant indices are re-derived from an opaque copy of the
+        // thread index per tile: hoisted out of the tile loop they held ~60 VGPRs
+        int tid = threadIdx.x;
+        asm volatile("" : "+v"(tid));
+#pragma unroll
+        for (int u = 0; u < 2; ++u) {
+            const int i = tid + u * kT;
             const int r = 1 + i / kALW, c = i - (r - 1) * kALW;
             const int y = y0 - kAH + r, x = x0 - kAH + c;
             float v = 0.f;
             {
                 const int ly = r - kAH, lx = c - kAH;
-                if (ly >= 0 && lx >= 0 && lx < kATX) v = s_g[(ly * kATX + lx) * (D + 1) + D];
+                if (ly >= 0 && ly < kATY && lx >= 0 && lx < kATX) v = s_g[(ly * kATX + lx) * (D + 1) + D];
             }
 #pragma unroll
             for (int k = 0; k < D; ++k) {
@@ -749,7 +798,8 @@ __global__ __launch_bounds__(kT) __attribute__((amdgpu_waves_per_eu(CCMI_ARM16_W
                 const int ly = r - kAH - dy, lx = c - kAH - dx;
                 if (ly >= 0 && ly < kATY && lx >= 0 && lx < kATX) v += s_g[(ly * kATX + lx) * (D + 1) + k];
             }
-            if (y >= 0 && y < H && x >= 0 && x < W && v != 0.f) atomicAdd(&gdst[y * W + x], v);
+            const bool in = i < (kALH - 1) * kALW && y >= 0 && y < H && x >= 0 && x < W;
+            atomicAdd(&gdst[min(max(y, 0), H - 1) * W + min(max(x, 0), W - 1)], in ? v : 0.f);
         }
     }
     // ---- flush
@@ -1159,7 +1209,9 @@ __global__ __launch_bounds__(kHeadT) void t_head_bwd(const float *__restrict__ d
     // columns let every lane read its MFMA operand unconditionally (no exec-mask branches
     // between the LDS reads and the MFMAs).
     extern __shared__ float s_dyn[];
-    constexpr int kXP = CIN + 2 > 4 ? CIN + 2 : 4;
+    // odd row pitch: conflict-free row writes (lane * kXP covers the 32 banks once per half),
+    // and rows s and s + 16 of the MFMA operand reads land 16 banks apart
+    constexpr int kXP = (CIN + 2 > 5 ? CIN + 2 : 5) | 1;
     // hidden unit j: w0[j][0..CIN), b0[j], w1[0..3)[j] -- read back as broadcast ds_read_b128
     __shared__ __attribute__((aligned(16))) float s_rec[64][12];
     static_assert(CIN + 4 <= 12, "hidden-unit record");
@@ -1207,17 +1259,29 @@ __global__ __launch_bounds__(kHeadT) void t_head_bwd(const float *__restrict__ d
     float db1[3] = {0.f, 0.f, 0.f};
     __syncthreads(); // s_rec staged
     const int64_t nchunk = (npx + kHeadT - 1) / kHeadT;
+    // the next chunk's pixel inputs (x, g_out) are loaded into registers while this one is
+    // processed: at 2 waves / SIMD (LDS-bound) the loads' latency was left exposed per chunk
+    float nx[CIN], ng[3];
+    auto load_chunk = [&](int64_t ch) {
+        const int64_t p = ch * kHeadT + t;
+        const bool valid = p < npx;
+        const float *x = dense + (int64_t)b * CIN * npx + p;
+        const float *G = gz0 + (int64_t)b * 3 * npx + p;
+#pragma unroll
+        for (int i = 0; i < CIN; ++i) nx[i] = valid ? x[i * npx] : 0.f;
+#pragma unroll
+        for (int k = 0; k < 3; ++k) ng[k] = valid ? G[k * npx] : 0.f;
+    };
+    if ((int64_t)blockIdx.x < nchunk) load_chunk(blockIdx.x);
     for (int64_t ch = blockIdx.x; ch < nchunk; ch += gridDim.x) {
         const int64_t p = ch * kHeadT + t;
         const bool valid = p < npx;
         float xv[CIN], gp1[3];
-        const float *x = dense + (int64_t)b * CIN * npx + p;
 #pragma unroll
-        for (int i = 0; i < CIN; ++i) xv[i] = valid ? x[i * npx] : 0.f;
-        const float *G = gz0 + (int64_t)b * 3 * npx + p;
-        gp1[0] = valid ? G[0] : 0.f;
-        gp1[1] = valid ? G[npx] : 0.f;
-        gp1[2] = valid ? G[2 * npx] : 0.f;
+        for (int i = 0; i < CIN; ++i) xv[i] = nx[i];
+#pragma unroll
+        for (int k = 0; k < 3; ++k) gp1[k] = ng[k];
+        if (ch + gridDim.x < nchunk) load_chunk(ch + gridDim.x);
         // ---- hidden layer (kept in this lane's LDS row) and the output pre-activations
         float o0 = bo0, o1 = bo1, o2 = bo2;
         if constexpr (PAIR) {
@@ -1262,13 +1326,15 @@ __global__ __launch_bounds__(kHeadT) void t_head_bwd(const float *__restrict__ d
         for (int k = 0; k < 3; ++k) db1[k] += gp1[k];
         // ---- dW1 += gp^T h (invalid pixels have gp = 0)
 #pragma unroll
-        for (int k = 0; k < 3; ++k) sw[lane * 4 + k] = gp1[k];
-        sw[lane * 4 + 3] = 0.f;
+        for (int k = 0; k < 3; ++k) sw[lane * kXP + k] = gp1[k];
+        sw[lane * kXP + 3] = 0.f;
         wave_lds_sync();
+        // K = pixels in the order px = s + 16 (lane >> 4): the two 16-lane groups of each
+        // 32-lane half read rows 16 apart, i.e. 16 banks apart (pitches hp, kXP odd)
 #pragma unroll
         for (int s = 0; s < 16; ++s) {
-            const int px = 4 * s + lk;
-            const float a = sw[px * 4 + ia];
+            const int px = s + 16 * lk;
+            const float a = sw[px * kXP + ia];
 #pragma unroll
             for (int q = 0; q < NT; ++q) a1[q] = HEAD_MFMA(a, sv[px * hp + 16 * q + ln], a1[q]);
         }
@@ -1324,7 +1390,7 @@ __global__ __launch_bounds__(kHeadT) void t_head_bwd(const float *__restrict__ d
         wave_lds_sync();
 #pragma unroll
         for (int s = 0; s < 16; ++s) {
-            const int px = 4 * s + lk;
+            const int px = s + 16 * lk;
             const float bb = sw[px * kXP + ib];
 #pragma unroll
             for (int q = 0; q < NT; ++q) a0[q] = HEAD_MFMA(sv[px * hp + 16 * q + ln], bb, a0[q]);
@@ -2116,7 +2182,7 @@ void launch_head(bool bwd, dim3 grid, hipStream_t s, const float *dense, const f
 {
     if (!bwd) hipLaunchKernelGGL((t_head_fwd<CIN>), grid, dim3(kT), 0, s, dense, g, th, ps, z0_or_gdense);
     else {
-        constexpr int kXP = CIN + 2 > 4 ? CIN + 2 : 4; // t_head_bwd's per-wave LDS rows
+        constexpr int kXP = (CIN + 2 > 5 ? CIN + 2 : 5) | 1; // t_head_bwd's per-wave LDS rows
         const size_t lds = sizeof(float) * (kHeadT / 64) * 64 * (16 * ((g.hid + 15) / 16) + 1 + kXP);
 #define CCMI_HB(N)                                                                                                     \
     hipLaunchKernelGGL((t_head_bwd<CIN, N, true>), grid, dim3(kHeadT), lds, s, dense, gz0, g, th, ps, z0_or_gdense, gth, gstride)

@@ -31,10 +31,11 @@ BUDGET = {
     "dec_arm_kernel<16, 2>": (128, 0, 0),                   # path B ARM + CABAC
     "dec_arm_spec_kernel<16, 2>": (128, 0, 0),
     "dec_ups_level_batch": (64, 0, 0),
-    # training step (3 waves / SIMD).  t_arm16<2> holds the MFMA weights of both layers in
-    # registers and spills a few values across its tile loop: measured faster than the
-    # spill-free 2-wave build (profiles/r2_train_ab.json), so the spills are budgeted
-    "t_arm16<2>": (168, 16, 64),
+    # training step (3 waves / SIMD).  t_arm16<2>: round 3 spilled 13 VGPRs across its tile
+    # loop (their reloads' vmcnt(0) waited for the previous tile's gradient atomics); since
+    # round 4 the hidden-layer weights sit in LDS, the ReLU masks in bits and the tile-invariant
+    # indices are re-derived per tile: no spills
+    "t_arm16<2>": (168, 0, 0),
     "t_head_bwd<7, 3, true>": (168, 0, 0),  # unit-pair packed form (default)
     "t_sp_bwd<1>": (128, 0, 0),  # 3x3 backward, input gradient
     "t_sp_bwd<2>": (128, 0, 0),  # 3x3 backward, weight gradients (4 waves / SIMD)

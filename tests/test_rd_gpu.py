@@ -115,11 +115,50 @@ def test_debug_preset_matches_reference_rd(image, gpu):
     assert np.isfinite(bd)
 
 
+# The reference's DEFAULT decoder (coolchic/utils/types.py:120-143: synthesis
+# 40-1-linear-relu,X-1-linear-none,X-3-residual-relu,X-3-residual-none, ARM "24,2"), debug
+# preset: the dim-24 ARM is the VALU training kernel whose context-gradient gather reaches 4
+# rows up (wrong until round 3's last commit), so its R-D is pinned end to end here against
+# the reference encoder run with the same architecture (tools/gen_golden_rd.py debug_default).
+DEFAULT_ARCH = dict(dim_arm=24, n_hidden=2,
+                    layers=((40, 1, False, True), (3, 1, False, False), (3, 3, True, True), (3, 3, True, False)))
+
+
+@pytest.mark.skipif(not (GOLDEN / "rd_reference_debug_default.json").exists(), reason="default-arch fixture absent")
+@pytest.mark.parametrize("image", ["kodim15_192x128", "kodim01_768x512"])
+def test_debug_preset_default_arch_matches_reference_rd(image, gpu):
+    from ccmi import io, rd, train
+    ref = [r for r in _ref("rd_reference_debug_default.json") if r["image"] == image and r["arch"] == "default"]
+    if {r["lmbda"] for r in ref} != set(LAMBDAS):
+        pytest.skip(f"default-arch fixture incomplete for {image}")
+    x = _targets()[image]
+    H, W = x.shape[-2:]
+    arch = train.Arch(H, W, **DEFAULT_ARCH)
+    tgt = io.to_target(x, "rgb").to(gpu)
+    recs = rd.encode_points(tgt, H, W, LAMBDAS, arch, yuv420=False, seeds=GPU_SEEDS, preset="debug", name=image,
+                            write=True)
+    out = ROOT / "gpurun_out"
+    out.mkdir(exist_ok=True)
+    f = out / "rd_gpu_debug_default.json"
+    prev = json.loads(f.read_text()) if f.exists() else {}
+    prev[image] = [r.as_dict() for r in recs]
+    f.write_text(json.dumps(prev, indent=1))
+    bd = _check(image, recs, ref, bd_band=image != "kodim15_192x128")
+    for r in recs:
+        assert r.cool_bpp == r.cool_bpp and r.cool_bpp > 0
+    assert np.isfinite(bd)
+
+
 # c3x preset (preset_cfg/c3x.yaml) with every phase / warm-up / patience scaled by 0.1, as
 # tools/gen_golden_rd.py ran it (C3X_SCALE): two reference seeds per lambda, so the tolerance is
-# the fixed margin widened by the reference's own seed spread at that lambda (and at least by
-# the debug preset's largest spread on the same image, for a lambda the two seeds happen to agree on).
+# the reference's own seed spread at that lambda plus a fixed margin, set from what round 3
+# observed (worst |dPSNR| 0.11 dB against the reference mean, rates within 3 % of it:
+# profiles/r3i_rd_gpu_summary.txt) -- 0.3 dB and 8 %.  The 192 x 128 image's rates swing by
+# 8-11 % between the reference's two seeds; against one seed alone the GPU looked "-7 % ... +5 %
+# across lambda", against their mean it is -3.0 ... +2.9 % with no trend.
 C3X_SCALE = 0.1
+C3X_PSNR_MARGIN_DB = 0.3
+C3X_RATE_MARGIN = 0.08
 
 
 @pytest.mark.parametrize("image", ["kodim15_192x128", "kodim01_768x512"])
@@ -129,9 +168,6 @@ def test_c3x_preset_matches_reference_rd(image, gpu):
     ref = [r for r in d["runs"] if r["image"] == image]
     assert {r["lmbda"] for r in ref} == set(LAMBDAS)
     assert all(len({r["seed"] for r in ref if r["lmbda"] == lm}) >= 2 for lm in LAMBDAS), "two reference seeds"
-    spread_dbg = max(max(x["psnr_db"] for x in g) - min(x["psnr_db"] for x in g)
-                     for g in ([r for r in _ref("rd_reference_debug.json") if r["image"] == image and r["lmbda"] == lm]
-                               for lm in LAMBDAS))
     x = _targets()[image]
     H, W = x.shape[-2:]
     arch = train.Arch(H, W, dim_arm=16, n_hidden=2, layers=HOP)
@@ -150,8 +186,8 @@ def test_c3x_preset_matches_reference_rd(image, gpu):
         rp, rr, ri = [x["psnr_db"] for x in r], [x["rate_bpp"] for x in r], [x["iterations"] for x in r]
         o = [x for x in recs if x.lmbda == lm]
         op, orr = np.mean([x.psnr_db for x in o]), np.mean([x.rate_bpp for x in o])
-        tol_p = PSNR_MARGIN_DB + max(max(rp) - min(rp), spread_dbg)
-        tol_r = RATE_MARGIN + (max(rr) - min(rr)) / np.mean(rr)
+        tol_p = C3X_PSNR_MARGIN_DB + (max(rp) - min(rp))
+        tol_r = C3X_RATE_MARGIN + (max(rr) - min(rr)) / np.mean(rr)
         its = int(np.median([x.iterations for x in o]))
         lines.append(f"{image} c3x lambda {lm}: PSNR ref {np.mean(rp):.3f} ({min(rp):.3f}..{max(rp):.3f}) gpu {op:.3f} "
                      f"(tol {tol_p:.2f}), rate ref {np.mean(rr):.4f} gpu {orr:.4f} (tol {tol_r:.2f}), iterations ref "

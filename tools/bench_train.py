@@ -9,6 +9,16 @@ from pathlib import Path
 import torch
 
 ROOT = Path(__file__).resolve().parents[1]
+# --lib PATH: time another libccmi build (A/B; set before ccmi is imported -- no env hop, so
+# the command can run under rocprofv3)
+if "--lib" in sys.argv:
+    import os
+    i = sys.argv.index("--lib")
+    os.environ["CCMI_LIB"] = str((ROOT / sys.argv[i + 1]).resolve())
+    del sys.argv[i:i + 2]
+NO_CPU = "--no-cpu" in sys.argv
+if NO_CPU:
+    sys.argv.remove("--no-cpu")
 sys.path.insert(0, str(ROOT / "cool-chic_amd"))
 sys.path.insert(0, str(ROOT / "oracle"))
 
@@ -63,6 +73,7 @@ if __name__ == "__main__":
     for B in [int(x) for x in (sys.argv[1:] or ["1", "8"])]:
         res["gpu_ms_per_iter"][B] = round(gpu_ms(H, W, B), 3)
         print(json.dumps(res), flush=True)
-    res["cpu_ms_per_iter"] = round(cpu_ms(H, W), 1)
-    res["cpu_threads"] = torch.get_num_threads()
-    print(json.dumps(res), flush=True)
+    if not NO_CPU:
+        res["cpu_ms_per_iter"] = round(cpu_ms(H, W), 1)
+        res["cpu_threads"] = torch.get_num_threads()
+        print(json.dumps(res), flush=True)

@@ -1,0 +1,28 @@
+#!/bin/bash
+# Round 4, session c: the training step with the ARM on a side stream (tests + A/B against the
+# round-3 library + kernel trace) and the fused-kernel window A/B (tools/ab_fused_window.sh).
+# Usage (GPU box, repo root): bash tools/gpu_r4c.sh OUTDIR
+set -u
+ROOT=$(pwd)
+OUT=$ROOT/${1:-gpurun_out/r4c}
+mkdir -p "$OUT"
+export TMPDIR=/tmp
+run() { # name seconds command...
+    local name=$1 secs=$2
+    shift 2
+    echo "== $name" | tee -a "$OUT/steps.log"
+    timeout -k 10 "$secs" "$@" > "$OUT/$name.log" 2>&1
+    local rc=$?
+    echo "   rc=$rc" | tee -a "$OUT/steps.log"
+    tail -3 "$OUT/$name.log"
+    if [ $rc -ne 0 ]; then tail -40 "$OUT/$name.log"; exit $rc; fi
+}
+run pytest_train 600 python -u -m pytest tests/test_train_gpu.py tests/test_mirror_train_gpu.py tests/test_quantize_gpu.py tests/test_forward.py tests/test_codec_e2e.py tests/test_sanity_gpu.py -m gpu -x -q --timeout 300 --timeout-method thread
+for r in 1 2; do
+  run new$r 200 python tools/bench_train.py 8 --no-cpu
+  run r3_$r 200 env CCMI_LIB=$ROOT/tools/ablib/r3base.so python tools/bench_train.py 8 --no-cpu
+done
+run trace_train 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/trace_train -o run -- python3 tools/bench_train.py 8 --no-cpu
+run abwin 900 bash tools/ab_fused_window.sh run ${1:-gpurun_out/r4c}/abwin
+run enc 400 python bench.py --steps 10 --warmup 2 --no-cpu-baseline --decode-reps 0 --hd-steps 0 --hd-decode-reps 0
+echo "all steps passed" | tee -a "$OUT/steps.log"
