@@ -881,6 +881,7 @@ def main():
             "vs_reference_results": compare_with_reference(recs, None),
             "records": [{k: (round(v, 5) if isinstance(v, float) else v) for k, v in r.items()
                          if k in ("image", "lmbda", "seed", "psnr_db", "rate_bpp", "iterations")} for r in recs],
+            "batch_timing": [r["timing"] for r in recs if r.get("timing")],
             "roofline": {"bound": "valu-fp32", "kernel": "whole overfit (all training kernels + host loop)",
                          "achieved": round(ach, 3), "peak": PEAK_FP32_TFLOPS, "unit": "TFLOP/s",
                          "frac": round(ach / PEAK_FP32_TFLOPS, 4),

@@ -69,6 +69,7 @@ class Record:
     iterations: int
     seconds: float
     cool_bpp: float = float("nan")   # size of the written .cool stream (when written)
+    timing: dict | None = None        # the batch's schedule timing (ccmi.train.overfit), on its first record
 
     def as_dict(self):
         return asdict(self)
@@ -104,6 +105,8 @@ def encode_batch(targets: torch.Tensor, H: int, W: int, lmbda: float, arch, *, n
                      iterations=int(of.iterations[b]), seconds=dt / B)
         if write and qm is not None:
             rec.cool_bpp = 8 * len(encode.write_cool(arch, of.latents[b], qm, yuv420=yuv420)) / npx
+        if b == 0:
+            rec.timing = dict(getattr(of, "timing", {}), batch=B, total_s=dt)
         out.append(rec)
     return out
 

@@ -404,9 +404,13 @@ def overfit(arch: Arch, targets: torch.Tensor, lmbda: float, yuv420: bool = True
     (ccmi.quantize.quantize_model, as video.py:302-310) and later phases train with them;
     the per-frame QuantizedModel list is state.quantized (None if no phase asks for it);
     state.iterations the per-frame iteration counts.  Returns (state, best validation)."""
+    import time
     dev = targets.device
     B = targets.shape[0]
     n0 = warmup[0][0] if warmup else 1
+    stream = torch.cuda.current_stream(dev)
+    timing = {"warmup_s": 0.0, "phases_s": [], "quantize_s": 0.0}
+    t0 = time.perf_counter()
     g = torch.Generator().manual_seed(seed)
     params = torch.stack([init_params(arch, g) for _ in range(B * n0)]).to(dev)
     lat = torch.zeros(B * n0, arch.n_latents, device=dev)
@@ -428,11 +432,17 @@ def overfit(arch: Arch, targets: torch.Tensor, lmbda: float, yuv420: bool = True
     best = None
     of.quantized = None
     of.iterations = list(warm_its)
+    stream.synchronize()
+    timing["warmup_s"] = time.perf_counter() - t0
     for ph in phases:
+        t0 = time.perf_counter()
         best = run_phase(of, ph, lmbda, scale)
         of.iterations = [a + b for a, b in zip(of.iterations, of.phase_iterations)]
+        stream.synchronize()
+        timing["phases_s"].append(time.perf_counter() - t0)
         if ph.quantize_model:
             from .quantize import quantize_model
+            t0 = time.perf_counter()
             qms = []
             for b in range(of.B):
                 qm = quantize_model(arch, of.latents[b], of.params[b], of.targets[b], lmbda, yuv420, bitdepth)
@@ -440,6 +450,11 @@ def overfit(arch: Arch, targets: torch.Tensor, lmbda: float, yuv420: bool = True
                 qms.append(qm)
             of.quantized = qms
             best = of.validate(lmbda).clone()
+            stream.synchronize()
+            timing["quantize_s"] += time.perf_counter() - t0
+    # wall seconds of the schedule's parts (host clock, this stream synchronised at each
+    # boundary): what the bench's encoder leg reports next to its images/hr
+    of.timing = timing
     return of, best
 
 

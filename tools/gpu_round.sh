@@ -16,7 +16,9 @@ run() { # name seconds command...
     echo "   rc=$rc" | tee -a "$OUT/steps.log"
     if [ $rc -ne 0 ]; then tail -40 "$OUT/$name.log"; exit $rc; fi
 }
-run pytest_gpu 900 python -u -m pytest $ROOT/tests -m gpu -x -v -s --timeout 300 --timeout-method thread
+# TESTS: the test files to run, relative to the repo root (default: the whole suite)
+if [ -n "${TESTS:-}" ]; then TESTS=$(for t in $TESTS; do printf '%s ' "$ROOT/$t"; done); else TESTS=$ROOT/tests; fi
+run pytest_gpu 900 python -u -m pytest $TESTS -m gpu -x -v -s --timeout 300 --timeout-method thread
 run bench 600 python3 $ROOT/bench.py
 QB="$ROOT/bench.py --steps 20 --warmup 5 --no-cpu-baseline --decode-reps 0 --encode-images 0 --hd-steps 0 --hd-decode-reps 0"
 run trace 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/trace -- python3 $QB
