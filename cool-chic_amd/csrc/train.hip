@@ -323,8 +323,16 @@ __device__ __forceinline__ void arm_rate(float q, float mu, float ls, bool valid
     }
 }
 
+// waves / SIMD the VALU ARM's registers are budgeted for (3: <= 168 VGPRs); the dim-24 / 32
+// ARMs with 2+ hidden layers hold more per-latent state than that (-DCCMI_TARM_WPE24=2 builds
+// the A/B variant with their 256-VGPR budget)
+#ifndef CCMI_TARM_WPE24
+#define CCMI_TARM_WPE24 3
+#endif
+constexpr int t_arm_wpe(int d, int nh) { return d >= 24 && nh >= 2 ? CCMI_TARM_WPE24 : 3; }
+
 template <int D, int NH>
-__global__ __launch_bounds__(kT) __attribute__((amdgpu_waves_per_eu(3))) void t_arm(const float *__restrict__ yq, Geo g, ArmTiles at, const float *__restrict__ th,
+__global__ __launch_bounds__(kT) __attribute__((amdgpu_waves_per_eu(t_arm_wpe(D, NH)))) void t_arm(const float *__restrict__ yq, Geo g, ArmTiles at, const float *__restrict__ th,
                                             int64_t ps, float lam_px, float *__restrict__ gq,
                                             float *__restrict__ gth, int64_t gstride, float *__restrict__ acc4,
                                             const float *__restrict__ grad_rate, float *__restrict__ rate_out)

@@ -19,6 +19,10 @@ if "--lib" in sys.argv:
 NO_CPU = "--no-cpu" in sys.argv
 if NO_CPU:
     sys.argv.remove("--no-cpu")
+# --default-arch: the reference's default decoder (ARM 24,2; synthesis head 40 wide) instead of hop
+DEFAULT_ARCH = "--default-arch" in sys.argv
+if DEFAULT_ARCH:
+    sys.argv.remove("--default-arch")
 sys.path.insert(0, str(ROOT / "cool-chic_amd"))
 sys.path.insert(0, str(ROOT / "oracle"))
 
@@ -28,11 +32,17 @@ from ccmi import train as T  # noqa: E402
 def gpu_ms(H, W, B, iters=20):
     import forward_oracle as fo
     dev = torch.device("cuda:0")
-    arch = T.Arch(H, W)
     rows = []
-    for b in range(B):
-        mp = fo.ModelParams.random(H, W, seed=b)
-        rows.append(T.pack_params(mp.arm, mp.ups_half, mp.pre_half, mp.syn))
+    if DEFAULT_ARCH:
+        layers = ((40, 1, False, True), (3, 1, False, False), (3, 3, True, True), (3, 3, True, False))
+        arch = T.Arch(H, W, dim_arm=24, n_hidden=2, layers=layers)
+        for b in range(B):
+            rows.append(T.init_params(arch, torch.Generator().manual_seed(b)))
+    else:
+        arch = T.Arch(H, W)
+        for b in range(B):
+            mp = fo.ModelParams.random(H, W, seed=b)
+            rows.append(T.pack_params(mp.arm, mp.ups_half, mp.pre_half, mp.syn))
     g = torch.Generator().manual_seed(0)
     lat = 0.01 * torch.randn(B, arch.n_latents, generator=g)
     tgt = torch.rand(B, H * W + 2 * (H // 2) * (W // 2), generator=g)

@@ -10,6 +10,10 @@ for r in 1 2; do
   timeout -k 10 200 python tools/bench_train.py 8 --no-cpu > $ROOT/$OUT/train_new$r.log 2>&1 || exit 1
   timeout -k 10 200 env CCMI_LIB=$ROOT/tools/ablib/r3base.so python tools/bench_train.py 8 --no-cpu > $ROOT/$OUT/train_r3_$r.log 2>&1 || exit 1
 done
+for r in 1 2; do
+  timeout -k 10 200 python tools/bench_train.py 8 --no-cpu --default-arch > $ROOT/$OUT/train_def_new$r.log 2>&1 || exit 1
+  timeout -k 10 200 env CCMI_LIB=$ROOT/tools/ablib/tarm2.so python tools/bench_train.py 8 --no-cpu --default-arch > $ROOT/$OUT/train_def_tarm2_$r.log 2>&1 || exit 1
+done
 tail -n1 $ROOT/$OUT/train_*.log
 cd /tmp && timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $ROOT/$OUT/trace_train -o run -- python3 $ROOT/tools/bench_train.py 8 --no-cpu > $ROOT/$OUT/trace_train.log 2>&1 || exit 1
 echo "r4d done"
