@@ -169,9 +169,8 @@ def test_debug_preset_default_arch_matches_reference_rd(image, gpu):
 
 # c3x preset (preset_cfg/c3x.yaml) with every phase / warm-up / patience scaled by 0.1, as
 # tools/gen_golden_rd.py ran it (C3X_SCALE): two reference seeds per lambda, so the tolerance is
-# the reference's own seed spread at that lambda plus a fixed margin, set from what round 3
-# observed (worst |dPSNR| 0.11 dB against the reference mean, rates within 3 % of it:
-# profiles/r3i_rd_gpu_summary.txt) -- 0.3 dB and 8 %.  The 192 x 128 image's rates swing by
+# the reference's own seed spread on that image (the largest over its lambdas) plus a fixed
+# margin: 0.3 dB and 8 % (round 3 allowed 0.5 dB + spread and 15 % + spread).  The 192 x 128 image's rates swing by
 # 8-11 % between the reference's two seeds; against one seed alone the GPU looked "-7 % ... +5 %
 # across lambda", against their mean it is -3.0 ... +2.9 % with no trend.
 C3X_SCALE = 0.1
@@ -199,13 +198,20 @@ def test_c3x_preset_matches_reference_rd(image, gpu):
     prev[image] = [r.as_dict() for r in recs]
     f.write_text(json.dumps(prev, indent=1))
     lines = []
+    # the reference's seed-to-seed spread is a property of the image and preset; two seeds per
+    # lambda estimate it badly (kodim15: 0.70 / 0.03 / 0.30 / 0.69 dB across the four lambdas),
+    # so each lambda's band uses the image's largest two-seed spread over the lambdas
+    by_lm = {lm: [x for x in ref if x["lmbda"] == lm] for lm in LAMBDAS}
+    sp_p = max(max(x["psnr_db"] for x in r) - min(x["psnr_db"] for x in r) for r in by_lm.values())
+    sp_r = max((max(x["rate_bpp"] for x in r) - min(x["rate_bpp"] for x in r)) / np.mean([x["rate_bpp"] for x in r])
+               for r in by_lm.values())
     for lm in LAMBDAS:
-        r = [x for x in ref if x["lmbda"] == lm]
+        r = by_lm[lm]
         rp, rr, ri = [x["psnr_db"] for x in r], [x["rate_bpp"] for x in r], [x["iterations"] for x in r]
         o = [x for x in recs if x.lmbda == lm]
         op, orr = np.mean([x.psnr_db for x in o]), np.mean([x.rate_bpp for x in o])
-        tol_p = C3X_PSNR_MARGIN_DB + (max(rp) - min(rp))
-        tol_r = C3X_RATE_MARGIN + (max(rr) - min(rr)) / np.mean(rr)
+        tol_p = C3X_PSNR_MARGIN_DB + sp_p
+        tol_r = C3X_RATE_MARGIN + sp_r
         its = int(np.median([x.iterations for x in o]))
         lines.append(f"{image} c3x lambda {lm}: PSNR ref {np.mean(rp):.3f} ({min(rp):.3f}..{max(rp):.3f}) gpu {op:.3f} "
                      f"(tol {tol_p:.2f}), rate ref {np.mean(rr):.4f} gpu {orr:.4f} (tol {tol_r:.2f}), iterations ref "
