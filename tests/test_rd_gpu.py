@@ -245,9 +245,9 @@ FULL_RATE_MARGIN = 0.10
 
 
 @pytest.mark.skipif(not (GOLDEN / "rd_reference_c3x_full.json").exists(), reason="full-schedule reference fixture absent")
-@pytest.mark.parametrize("lm", [0.001, 0.0004])
+@pytest.mark.parametrize("lm", [0.001, 0.0004, 0.004])
 def test_c3x_full_schedule_matches_reference(lm, gpu):
-    """lambda 1e-3 (round 3) and 4e-4 (round 4): two full-schedule reference seeds each."""
+    """lambda 1e-3 (round 3), 4e-4 and 4e-3 (round 4): two full-schedule reference seeds each."""
     from ccmi import io, rd, train
     ref = json.loads((GOLDEN / "rd_reference_c3x_full.json").read_text())["runs"]
     image = "kodim01_768x512"
