@@ -13,7 +13,7 @@ disp = collections.defaultdict(set)
 for f in sorted(src.rglob("*counter_collection.csv")):
     for r in csv.DictReader(open(f)):
         name = r["Kernel_Name"]
-        short = name.split("(")[0].replace("void ", "").replace("(anonymous namespace)::", "")
+        short = name.replace("(anonymous namespace)::", "").replace("void ", "").split("(")[0]
         tot[short][r["Counter_Name"]] += float(r["Counter_Value"])
         disp[(short, r["Counter_Name"])].add(r["Dispatch_Id"])
 for k in sorted(tot):
@@ -25,7 +25,7 @@ for k in sorted(tot):
     pw = lambda n: c.get(n, 0.0) / waves
     pd = lambda n: c.get(n, 0.0) / max(1, len(disp[(k, n)]))
     print(f"{k}: dispatches {nd}, waves/dispatch {waves / max(1, len(disp[(k, 'SQ_WAVES')])):.0f}")
-    print("   per wave: " + ", ".join(f"{n[9:] if n.startswith('SQ_INSTS') else n} {pw(n):.0f}" for n in
+    print("   per wave: " + ", ".join(f"{n[9:] if n.startswith('SQ_INSTS_') else n} {pw(n):.0f}" for n in
                                       ("SQ_INSTS_VALU", "SQ_INSTS_MFMA", "SQ_INSTS_LDS", "SQ_INSTS_SALU", "SQ_INSTS_SMEM",
                                        "SQ_INSTS_VMEM_RD", "SQ_INSTS_VMEM_WR")))
     w = pw("SQ_WAVE_CYCLES")
