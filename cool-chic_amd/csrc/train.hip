@@ -200,7 +200,72 @@ __device__ __forceinline__ void ctx_off(int i, int &dy, int &dx)
     dx = k % 9 - 4;
 }
 
+// The context gradients a position (r, c) of the tile + causal halo receives: the gradient of
+// every latent of the tile whose context holds it (context input k of the latent at
+// (r - kAH - dy_k, c - kAH - dx_k)), plus the latent's own gradient (column D of its s_g row)
+// when (r, c) is a latent of the tile.  s_g: [kATY * kATX][D + 1].  Every term's LDS read is
+// issued unconditionally -- a term outside the tile reads s_zero -- so a position's D + 1
+// reads are in flight together (as `if (inside) v += s_g[..]` they compiled to D + 1
+// exec-mask branches with one LDS round trip each).
+// Summation order as before (own value, then k = 0 .. D - 1).
+template <int D>
+__device__ __forceinline__ float gather_ctx(const float *s_g, const float *s_zero, int r, int c)
+{
+    const int ly0 = r - kAH, lx0 = c - kAH;
+    const int base = (ly0 * kATX + lx0) * (D + 1);
+    auto inside = [](int ly, int lx) { return (unsigned)ly < (unsigned)kATY && (unsigned)lx < (unsigned)kATX; };
+    float t[D + 1];
+    t[D] = *(inside(ly0, lx0) ? s_g + base + D : s_zero);
+#pragma unroll
+    for (int k = 0; k < D; ++k) {
+        int dy, dx;
+        ctx_off<D>(k, dy, dx);
+        t[k] = *(inside(ly0 - dy, lx0 - dx) ? s_g + base + (-dy * kATX - dx) * (D + 1) + k : s_zero);
+    }
+    // all reads issued before the first add (the scheduler otherwise sinks each read to its
+    // add: one LDS round trip per term again)
+    __builtin_amdgcn_sched_barrier(0);
+    float v = t[D];
+#pragma unroll
+    for (int k = 0; k < D; ++k) v += t[k];
+    return v;
+}
+
 typedef float v4f __attribute__((ext_vector_type(4)));
+
+// Lane exchanges between the four 16-lane rows of a wave on gfx950's permlane swaps (VALU ops,
+// no LDS round trip as ds_bpermute / __shfl): v_permlane16_swap exchanges rows 1 <-> 0 and
+// 3 <-> 2 of its two operands, v_permlane32_swap lanes 32..63 <-> 0..31.
+struct f2 {
+    float a, b;
+};
+__device__ __forceinline__ f2 swap16(float x)
+{
+    const auto r = __builtin_amdgcn_permlane16_swap(__float_as_uint(x), __float_as_uint(x), false, false);
+    return {__uint_as_float(r[0]), __uint_as_float(r[1])}; // {rows 0, 0, 2, 2}, {rows 1, 1, 3, 3}
+}
+__device__ __forceinline__ f2 swap32(float x)
+{
+    const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(x), __float_as_uint(x), false, false);
+    return {__uint_as_float(r[0]), __uint_as_float(r[1])}; // {rows 0, 1, 0, 1}, {rows 2, 3, 2, 3}
+}
+// x + x[lane ^ 16], then + the same at lane ^ 32: the sum over the four rows, in every lane
+// (the values and their order are those of two __shfl_xor steps)
+__device__ __forceinline__ float sum_rows(float x)
+{
+    const f2 h = swap16(x);
+    const f2 q = swap32(h.a + h.b);
+    return q.a + q.b;
+}
+// bc[g] = row g of x, in every row (as __shfl(x, 16 g + (lane & 15)))
+__device__ __forceinline__ void bcast_rows(float x, float (&bc)[4])
+{
+    const f2 h = swap32(x), lo = swap16(h.a), hi = swap16(h.b);
+    bc[0] = lo.a;
+    bc[1] = lo.b;
+    bc[2] = hi.a;
+    bc[3] = hi.b;
+}
 // v_mfma_f32_16x16x4_f32 (f32 in, f32 accumulate: an fmaf chain in another order).
 // Lane l supplies A[m = l & 15][k = l >> 4] and B[k = l >> 4][n = l & 15]; accumulator
 // register r of lane l is D[m = 4 (l >> 4) + r][n = l & 15].
@@ -343,6 +408,8 @@ __global__ __launch_bounds__(kT) __attribute__((amdgpu_waves_per_eu(t_arm_wpe(D,
     // context-gradient planes can span both once the MFMA stage is over
     __shared__ float s_ga[2 * kT * (D + 1)];
     float *const s_g = s_ga, *const s_a = s_ga + kT * (D + 1);
+    __shared__ float s_zero[1]; // what the context gather reads for terms outside the tile
+    if (threadIdx.x == 0) s_zero[0] = 0.f; // visible after the tile loop's first barrier
 
     const int b = blockIdx.y;
     const int w = threadIdx.x >> 6;
@@ -442,7 +509,14 @@ __global__ __launch_bounds__(kT) __attribute__((amdgpu_waves_per_eu(t_arm_wpe(D,
         float g_q, g_mu, g_ls, rbits;
         {
             const int64_t li = (int64_t)b * g.N + g.off[l] + (int64_t)(y0 + cy) * W + (x0 + cx);
-            const float lam = valid && grad_rate ? grad_rate[li] : lam_px;
+            float lam = lam_px;
+            if (valid && grad_rate) {
+                lam = grad_rate[li];
+                // waited for here: at the use below, past the branch, the compiler's wait is a
+                // vmcnt(0) on every path -- also behind the next tile's prefetch loads and the
+                // gather atomics when there is no grad_rate (training)
+                __builtin_amdgcn_s_waitcnt(0x0f70); // vmcnt(0)
+            }
             arm_rate(q, mu, ls, valid, lam, rbits, g_q, g_mu, g_ls);
             if (valid) {
                 rsum += rbits;
@@ -519,18 +593,7 @@ __global__ __launch_bounds__(kT) __attribute__((amdgpu_waves_per_eu(t_arm_wpe(D,
             const int i = tid + u * kT;
             const int r = kR0 + i / kALW, c = i - (r - kR0) * kALW;
             const int y = y0 - kAH + r, x = x0 - kAH + c;
-            float v = 0.f;
-            {   // own value: the latent at (r - kAH, c - kAH)
-                const int ly = r - kAH, lx = c - kAH;
-                if (ly >= 0 && ly < kATY && lx >= 0 && lx < kATX) v = s_g[(ly * kATX + lx) * (D + 1) + D];
-            }
-#pragma unroll
-            for (int k = 0; k < D; ++k) {
-                int dy, dx;
-                ctx_off<D>(k, dy, dx);
-                const int ly = r - kAH - dy, lx = c - kAH - dx;
-                if (ly >= 0 && ly < kATY && lx >= 0 && lx < kATX) v += s_g[(ly * kATX + lx) * (D + 1) + k];
-            }
+            const float v = gather_ctx<D>(s_g, s_zero, r, c);
             const bool in = i < kGN && y >= 0 && y < H && x >= 0 && x < W;
             atomicAdd(&gdst[min(max(y, 0), H - 1) * W + min(max(x, 0), W - 1)], in ? v : 0.f);
         }
@@ -571,6 +634,8 @@ __global__ __launch_bounds__(kT) __attribute__((amdgpu_waves_per_eu(CCMI_ARM16_W
     __shared__ float s_y[kALH][kALW];
     __shared__ float s_ga[2 * kT * (D + 1)];
     float *const s_g = s_ga, *const s_a = s_ga + kT * (D + 1);
+    __shared__ float s_zero[1]; // what the context gather reads for terms outside the tile
+    if (threadIdx.x == 0) s_zero[0] = 0.f; // visible after the tile loop's first barrier
     const int b = blockIdx.y, w = threadIdx.x >> 6, lane = threadIdx.x & 63, ln = lane & 15, lk = lane >> 4;
     const int cy = w, cx = lane; // per-latent phase: this lane's latent in the tile
     const cfloat_ptr P = (cfloat_ptr)(size_t)(th + (int64_t)b * ps);
@@ -708,10 +773,8 @@ __global__ __launch_bounds__(kT) __attribute__((amdgpu_waves_per_eu(CCMI_ARM16_W
                 pm = fmaf(WO0[r], X[NH][gg][r], pm);
                 pl = fmaf(WO1[r], X[NH][gg][r], pl);
             }
-            pm += __shfl_xor(pm, 16);
-            pl += __shfl_xor(pl, 16);
-            pm += __shfl_xor(pm, 32);
-            pl += __shfl_xor(pl, 32);
+            pm = sum_rows(pm);
+            pl = sum_rows(pl);
             if (gg == lk) {
                 mu = pm + bo0;
                 ls = pl + bo1;
@@ -722,7 +785,14 @@ __global__ __launch_bounds__(kT) __attribute__((amdgpu_waves_per_eu(CCMI_ARM16_W
         float g_q, g_mu, g_ls, rbits;
         {
             const int64_t li = (int64_t)b * g.N + g.off[l] + (int64_t)(y0 + cy) * W + (x0 + cx);
-            const float lam = valid && grad_rate ? grad_rate[li] : lam_px;
+            float lam = lam_px;
+            if (valid && grad_rate) {
+                lam = grad_rate[li];
+                // waited for here: at the use below, past the branch, the compiler's wait is a
+                // vmcnt(0) on every path -- also behind the next tile's prefetch loads and the
+                // gather atomics when there is no grad_rate (training)
+                __builtin_amdgcn_s_waitcnt(0x0f70); // vmcnt(0)
+            }
             arm_rate(q, mu, ls, valid, lam, rbits, g_q, g_mu, g_ls);
             if (valid) {
                 rsum += rbits;
@@ -732,10 +802,12 @@ __global__ __launch_bounds__(kT) __attribute__((amdgpu_waves_per_eu(CCMI_ARM16_W
         accbo0 += g_mu;
         accbo1 += g_ls;
         // ---- backward: output layer (VALU), its weight gradients as per-lane partial sums
-        float G[4][4];
+        float G[4][4], gmb[4], glb[4];
+        bcast_rows(g_mu, gmb);
+        bcast_rows(g_ls, glb);
 #pragma unroll
         for (int gg = 0; gg < 4; ++gg) {
-            const float gm = __shfl(g_mu, 16 * gg + ln), gl = __shfl(g_ls, 16 * gg + ln);
+            const float gm = gmb[gg], gl = glb[gg];
 #pragma unroll
             for (int r = 0; r < 4; ++r) {
                 G[gg][r] = WO0[r] * gm + WO1[r] * gl;
@@ -798,18 +870,7 @@ __global__ __launch_bounds__(kT) __attribute__((amdgpu_waves_per_eu(CCMI_ARM16_W
             const int i = tid + u * kT;
             const int r = 1 + i / kALW, c = i - (r - 1) * kALW;
             const int y = y0 - kAH + r, x = x0 - kAH + c;
-            float v = 0.f;
-            {
-                const int ly = r - kAH, lx = c - kAH;
-                if (ly >= 0 && ly < kATY && lx >= 0 && lx < kATX) v = s_g[(ly * kATX + lx) * (D + 1) + D];
-            }
-#pragma unroll
-            for (int k = 0; k < D; ++k) {
-                int dy, dx;
-                ctx_off<D>(k, dy, dx);
-                const int ly = r - kAH - dy, lx = c - kAH - dx;
-                if (ly >= 0 && ly < kATY && lx >= 0 && lx < kATX) v += s_g[(ly * kATX + lx) * (D + 1) + k];
-            }
+            const float v = gather_ctx<D>(s_g, s_zero, r, c);
             const bool in = i < (kALH - 1) * kALW && y >= 0 && y < H && x >= 0 && x < W;
             atomicAdd(&gdst[min(max(y, 0), H - 1) * W + min(max(x, 0), W - 1)], in ? v : 0.f);
         }
