@@ -613,19 +613,22 @@ __global__ __launch_bounds__(kT) __attribute__((amdgpu_waves_per_eu(t_arm_wpe(D,
 // register r of lane l then holds unit 4 (l >> 4) + r of latent l & 15 -- exactly the B
 // operand of the next layer, so activations never leave the registers, and residual, bias
 // and ReLU are elementwise on the accumulators.  The weights (W for the forward, W^T for
-// the input gradients) are 8 VGPRs per layer per lane, loaded ONCE per workgroup (one
-// frame): no per-tile weight loads at all (their scalar-load waits were 37 % of the
-// VALU kernel, tools/arm_diag.sh NOWLOAD).  The 2-wide output layer and the rate are VALU
+// the input gradients, the output layer) are loaded from HBM ONCE per workgroup (one frame)
+// into LDS and read from there per tile: no per-tile global weight loads (their scalar-load
+// waits were 37 % of the VALU kernel, tools/arm_diag.sh NOWLOAD).  The 2-wide output layer and the rate are VALU
 // (an M = 2 MFMA would be 8x padding); the rate runs one latent per lane (lane = tile
 // column: group g's values sit in the lanes with lane >> 4 == g).  Weight gradients of the
 // hidden layers: LDS-staged rows on the matrix cores (mfma_outer, K = latents); biases and
 // the output layer's weight gradients: per-lane partial sums over every tile the workgroup
 // visits, reduced once at the end.
-template <int NH>
+// waves / SIMD the register allocation targets: 4 (<= 128 VGPRs) for up to two hidden layers --
+// the few values it spills are the epilogue's, outside the tile loop -- 3 for three
 #ifndef CCMI_ARM16_WAVES
-#define CCMI_ARM16_WAVES 3
+#define CCMI_ARM16_WAVES 4
 #endif
-__global__ __launch_bounds__(kT) __attribute__((amdgpu_waves_per_eu(CCMI_ARM16_WAVES))) void t_arm16(
+constexpr int t_arm16_wpe(int nh) { return nh <= 2 ? CCMI_ARM16_WAVES : 3; }
+template <int NH>
+__global__ __launch_bounds__(kT) __attribute__((amdgpu_waves_per_eu(t_arm16_wpe(NH)))) void t_arm16(
     const float *__restrict__ yq, Geo g, ArmTiles at, const float *__restrict__ th, int64_t ps, float lam_px,
     float *__restrict__ gq, float *__restrict__ gth, int64_t gstride, float *__restrict__ acc4,
     const float *__restrict__ grad_rate, float *__restrict__ rate_out)
@@ -647,12 +650,9 @@ __global__ __launch_bounds__(kT) __attribute__((amdgpu_waves_per_eu(CCMI_ARM16_W
     __shared__ __attribute__((aligned(16))) float s_w[NL][LS];
     for (int i = threadIdx.x; i < NH * LS; i += kT) s_w[i / LS][i % LS] = P[i];
     const cfloat_ptr Wo = P + NH * LS;
-    float WO0[4], WO1[4];
-#pragma unroll
-    for (int r = 0; r < 4; ++r) {
-        WO0[r] = Wo[4 * lk + r];
-        WO1[r] = Wo[D + 4 * lk + r];
-    }
+    // the output layer's weights in LDS too, read where used (8 fewer persistent VGPRs)
+    __shared__ __attribute__((aligned(16))) float s_wo[2 * D];
+    for (int i = threadIdx.x; i < 2 * D; i += kT) s_wo[i] = Wo[i];
     const float bo0 = Wo[2 * D], bo1 = Wo[2 * D + 1];
     // s_y offsets of the context inputs k = 4 lk + s, derived per tile from an opaque lane
     // index (kept across the tile loop they were 4 more persistent VGPRs)
@@ -765,6 +765,7 @@ __global__ __launch_bounds__(kT) __attribute__((amdgpu_waves_per_eu(CCMI_ARM16_W
         // output layer: partial dot products over this lane's 4 units, summed over the 4
         // lanes of the latent; group g's (mu, ls) kept by the lanes with lk == g
         float mu = 0.f, ls = 0.f;
+        v4f WO0 = *reinterpret_cast<const v4f *>(&s_wo[4 * lk]), WO1 = *reinterpret_cast<const v4f *>(&s_wo[D + 4 * lk]);
 #pragma unroll
         for (int gg = 0; gg < 4; ++gg) {
             float pm = 0.f, pl = 0.f;
@@ -793,7 +794,11 @@ __global__ __launch_bounds__(kT) __attribute__((amdgpu_waves_per_eu(CCMI_ARM16_W
                 // gather atomics when there is no grad_rate (training)
                 __builtin_amdgcn_s_waitcnt(0x0f70); // vmcnt(0)
             }
+#if defined(CCMI_DIAG_A16_NORATE) // diagnostic builds only (tools/arm_diag.sh): wrong results
+            rbits = mu; g_q = ls * lam; g_mu = q * ls; g_ls = mu * q;
+#else
             arm_rate(q, mu, ls, valid, lam, rbits, g_q, g_mu, g_ls);
+#endif
             if (valid) {
                 rsum += rbits;
                 if (rate_out) rate_out[li] = rbits;
@@ -802,6 +807,8 @@ __global__ __launch_bounds__(kT) __attribute__((amdgpu_waves_per_eu(CCMI_ARM16_W
         accbo0 += g_mu;
         accbo1 += g_ls;
         // ---- backward: output layer (VALU), its weight gradients as per-lane partial sums
+        WO0 = *reinterpret_cast<const v4f *>(&s_wo[4 * lk]);
+        WO1 = *reinterpret_cast<const v4f *>(&s_wo[D + 4 * lk]);
         float G[4][4], gmb[4], glb[4];
         bcast_rows(g_mu, gmb);
         bcast_rows(g_ls, glb);
@@ -833,7 +840,9 @@ __global__ __launch_bounds__(kT) __attribute__((amdgpu_waves_per_eu(CCMI_ARM16_W
 #pragma unroll
             for (int r = 0; r < 4; ++r) accb[L][r] += (gz[0][r] + gz[1][r]) + (gz[2][r] + gz[3][r]);
             wave_lds_sync(); // each wave stages and reads only its own 64 rows
+#if !defined(CCMI_DIAG_A16_NOOUTER)
             mfma_outer<D, D, false>(sg, sa, acc_h[L], accb_dummy);
+#endif
             wave_lds_sync();
             // input gradient: W^T gz + gz (residual), K permuted like the forward;
             // A = W^T[i = ln][j = 4 lk + s]
@@ -865,6 +874,9 @@ __global__ __launch_bounds__(kT) __attribute__((amdgpu_waves_per_eu(CCMI_ARM16_W
         // thread index per tile: hoisted out of the tile loop they held ~60 VGPRs
         int tid = threadIdx.x;
         asm volatile("" : "+v"(tid));
+#if defined(CCMI_DIAG_A16_NOGATHER)
+        if (tid < 0)
+#endif
 #pragma unroll
         for (int u = 0; u < 2; ++u) {
             const int i = tid + u * kT;
