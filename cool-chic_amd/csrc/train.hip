@@ -29,6 +29,9 @@
 #include <stdlib.h>
 
 #include <cmath>
+#include <map>
+#include <mutex>
+#include <tuple>
 
 #include "fwd_common.h"
 
@@ -310,10 +313,11 @@ __device__ __forceinline__ void mfma_outer(const float *s_g, const float *s_a, v
     }
 }
 
-// Flush of mfma_outer's accumulators into a [R][D] weight-gradient block and its [R] bias.
+// mfma_outer's accumulators stored into a wave's partial [R][D] weight-gradient block and its
+// [R] bias in LDS (every element is written), for the workgroup-level reduction of the flush
 template <int R, int D>
-__device__ __forceinline__ void flush_outer(const v4f (&acc)[(R + 15) / 16][(D + 15) / 16], const v4f (&accb)[(R + 15) / 16],
-                                            float *__restrict__ dst, float *__restrict__ dstb)
+__device__ __forceinline__ void stage_outer(const v4f (&acc)[(R + 15) / 16][(D + 15) / 16], const v4f (&accb)[(R + 15) / 16],
+                                            float *dst, float *dstb)
 {
     constexpr int MT = (R + 15) / 16, NT = (D + 15) / 16;
     const int lane = threadIdx.x & 63, ln = lane & 15, lk = lane >> 4;
@@ -324,8 +328,8 @@ __device__ __forceinline__ void flush_outer(const v4f (&acc)[(R + 15) / 16][(D +
 #pragma unroll
             for (int r = 0; r < 4; ++r) {
                 const int m = 16 * mt + 4 * lk + r, n = 16 * nt + ln;
-                if (m < R && n < D) atomicAdd(&dst[m * D + n], acc[mt][nt][r]);
-                if (nt == 0 && m < R && ln == 0) atomicAdd(&dstb[m], accb[mt][r]);
+                if (m < R && n < D) dst[m * D + n] = acc[mt][nt][r];
+                if (nt == 0 && m < R && ln == 0) dstb[m] = accb[mt][r];
             }
 }
 
@@ -598,11 +602,20 @@ __global__ __launch_bounds__(kT) __attribute__((amdgpu_waves_per_eu(t_arm_wpe(D,
             atomicAdd(&gdst[min(max(y, 0), H - 1) * W + min(max(x, 0), W - 1)], in ? v : 0.f);
         }
     }
-    // ---- flush this wave's weight / bias gradients and rate
-    float *G = gth + (int64_t)b * gstride;
-    flush_outer<2, D>(acc_o, accb_o, G + NH * (D * D + D), G + NH * (D * D + D) + 2 * D);
+    // ---- flush: the four waves' weight / bias gradients meet in LDS, then one atomic per value
+    // per workgroup (see t_arm16's flush)
+    static_assert(kT == 4 * 64, "four waves per workgroup");
+    constexpr int LS = D * D + D, kRed = NH * LS + 2 * D + 2;
+    static_assert(4 * kRed <= 2 * kT * (D + 1), "the partial rows fit s_ga");
+    float *red = s_ga + w * kRed;
+    __syncthreads(); // last tile's gather reads of s_g are done
+    stage_outer<2, D>(acc_o, accb_o, red + NH * LS, red + NH * LS + 2 * D);
 #pragma unroll
-    for (int L = 0; L < NH; ++L) flush_outer<D, D>(acc_h[L], accb_h[L], G + L * (D * D + D), G + L * (D * D + D) + D * D);
+    for (int L = 0; L < NH; ++L) stage_outer<D, D>(acc_h[L], accb_h[L], red + L * LS, red + L * LS + D * D);
+    __syncthreads();
+    float *G = gth + (int64_t)b * gstride;
+    for (int e = threadIdx.x; e < kRed; e += kT)
+        atomicAdd(&G[e], (s_ga[e] + s_ga[kRed + e]) + (s_ga[2 * kRed + e] + s_ga[3 * kRed + e]));
     wave_add(rsum, &acc4[b * 4 + 1]);
 }
 
@@ -887,16 +900,23 @@ __global__ __launch_bounds__(kT) __attribute__((amdgpu_waves_per_eu(t_arm16_wpe(
             atomicAdd(&gdst[min(max(y, 0), H - 1) * W + min(max(x, 0), W - 1)], in ? v : 0.f);
         }
     }
-    // ---- flush
-    float *Gp = gth + (int64_t)b * gstride;
+    // ---- flush: the four waves' partial sums meet in LDS (s_ga is free after the tile loop) and
+    // each value goes out with ONE atomic per workgroup.  (One atomic per value per wave, every
+    // workgroup of a frame on the same ~600 addresses, serialised in L2: the kernel's time grew
+    // linearly with its grid -- 293 / 460 / 572 / 745 us for 1024 / 2048 / 3072 / 4096
+    // workgroups, profiles/r4l_*.)
+    static_assert(kT == 4 * 64, "four waves per workgroup");
+    constexpr int kRed = NH * LS + 2 * D + 2; // the gradient row's ARM part, Gp layout
+    float *red = s_ga + w * kRed;             // this wave's partial row
+    __syncthreads();                          // last tile's gather reads of s_g are done
 #pragma unroll
     for (int L = 0; L < NH; ++L) {
 #pragma unroll
         for (int r = 0; r < 4; ++r) { // dW_L[m = 4 lk + r][n = ln]
-            atomicAdd(&Gp[L * LS + (4 * lk + r) * D + ln], acc_h[L][0][0][r]);
+            red[L * LS + (4 * lk + r) * D + ln] = acc_h[L][0][0][r];
             float v = accb[L][r];
             for (int o = 1; o < 16; o <<= 1) v += __shfl_xor(v, o);
-            if (ln == 0) atomicAdd(&Gp[L * LS + D * D + 4 * lk + r], v);
+            if (ln == 0) red[L * LS + D * D + 4 * lk + r] = v;
         }
     }
 #pragma unroll
@@ -907,12 +927,22 @@ __global__ __launch_bounds__(kT) __attribute__((amdgpu_waves_per_eu(t_arm16_wpe(
             v1 += __shfl_xor(v1, o);
         }
         if (ln == 0) {
-            atomicAdd(&Gp[NH * LS + 4 * lk + r], v0);
-            atomicAdd(&Gp[NH * LS + D + 4 * lk + r], v1);
+            red[NH * LS + 4 * lk + r] = v0;
+            red[NH * LS + D + 4 * lk + r] = v1;
         }
     }
-    wave_add(accbo0, &Gp[NH * LS + 2 * D]);
-    wave_add(accbo1, &Gp[NH * LS + 2 * D + 1]);
+    for (int o = 32; o > 0; o >>= 1) {
+        accbo0 += __shfl_xor(accbo0, o);
+        accbo1 += __shfl_xor(accbo1, o);
+    }
+    if (lane == 0) {
+        red[NH * LS + 2 * D] = accbo0;
+        red[NH * LS + 2 * D + 1] = accbo1;
+    }
+    __syncthreads();
+    float *Gp = gth + (int64_t)b * gstride;
+    for (int e = threadIdx.x; e < kRed; e += kT)
+        atomicAdd(&Gp[e], (s_ga[e] + s_ga[kRed + e]) + (s_ga[2 * kRed + e] + s_ga[3 * kRed + e]));
     wave_add(rsum, &acc4[b * 4 + 1]);
 }
 
@@ -1482,8 +1512,15 @@ __global__ __launch_bounds__(kHeadT) void t_head_bwd(const float *__restrict__ d
         }
         wave_lds_sync();
     }
-    // ---- flush: accumulator register r of lane l holds D[m = 4 (l >> 4) + r][n = l & 15]
-    float *Gp = gth + (int64_t)b * gstride;
+    // ---- flush: accumulator register r of lane l holds D[m = 4 (l >> 4) + r][n = l & 15].
+    // The waves' partial sums meet in LDS (each wave's own rows, free after the chunk loop),
+    // then ONE atomic per value per workgroup (one per wave put every workgroup of a frame on
+    // the same few hundred addresses -- the t_arm16 flush lesson, profiles/r4l_*)
+    // partial row: w0 [hid][CIN] | b0 [hid] | w1 [3][hid] | b1 [3]
+    const int nred = hid * (CIN + 4) + 3;
+    float *red = s_dyn + w * 64 * (hp + kXP);
+    static_assert(64 * (hp + kXP) >= 16 * NT * (CIN + 4) + 3, "a wave's partial row fits its LDS rows");
+    __syncthreads();
 #pragma unroll
     for (int q = 0; q < NT; ++q) {
 #pragma unroll
@@ -1491,12 +1528,12 @@ __global__ __launch_bounds__(kHeadT) void t_head_bwd(const float *__restrict__ d
             const int m = 4 * lk + r;
             if (m < 3) { // dW1[k = m][j]
                 const int j = 16 * q + ln;
-                if (j < hid) atomicAdd(&Gp[g.w1 + m * hid + j], a1[q][r]);
+                if (j < hid) red[hid * (CIN + 1) + m * hid + j] = a1[q][r];
             }
             const int j = 16 * q + m; // dW0[j][i = ln]
             if (j < hid) {
-                if (ln < CIN) atomicAdd(&Gp[g.w0 + j * CIN + ln], a0[q][r]);
-                else if (ln == CIN) atomicAdd(&Gp[g.b0 + j], a0[q][r]);
+                if (ln < CIN) red[j * CIN + ln] = a0[q][r];
+                else if (ln == CIN) red[hid * CIN + j] = a0[q][r];
             }
         }
     }
@@ -1504,7 +1541,20 @@ __global__ __launch_bounds__(kHeadT) void t_head_bwd(const float *__restrict__ d
     for (int k = 0; k < 3; ++k) {
         float v = db1[k];
         for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
-        if (lane == 0) atomicAdd(&Gp[g.b1 + k], v);
+        if (lane == 0) red[hid * (CIN + 4) + k] = v;
+    }
+    __syncthreads();
+    float *Gp = gth + (int64_t)b * gstride;
+    constexpr int kW = kHeadT / 64;
+    for (int e = t; e < nred; e += kHeadT) {
+        float v = 0.f;
+#pragma unroll
+        for (int ww = 0; ww < kW; ++ww) v += s_dyn[ww * 64 * (hp + kXP) + e];
+        const int dst = e < hid * CIN ? g.w0 + e
+                        : e < hid * (CIN + 1) ? g.b0 + (e - hid * CIN)
+                        : e < hid * (CIN + 4) ? g.w1 + (e - hid * (CIN + 1))
+                                              : g.b1 + (e - hid * (CIN + 4));
+        atomicAdd(&Gp[dst], v);
     }
 }
 
@@ -2234,8 +2284,35 @@ int make_plan(const ccmi_train_args *a, Plan &pl)
     return CCMI_OK;
 }
 
+// Workgroups of `fn` that fit on the device at once (occupancy x CUs): the grid of the
+// persistent (grid-stride) training kernels is ONE resident round.  A second round only adds
+// workgroups, and each workgroup's flush costs one atomic per value on addresses every
+// workgroup of the frame shares (t_arm16: 227 us with one round of 1024 workgroups, 232 us
+// with 2048, after the flush reduction; before it 293 vs 460 us, profiles/r4l_*, r4m_*).
+static int resident_wgs(const void *fn, int threads, size_t lds, int max_per_cu)
+{
+    static std::mutex mu;
+    static std::map<std::tuple<const void *, size_t, int>, int> cache;
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess) dev = 0;
+    std::lock_guard<std::mutex> lk(mu);
+    const auto key = std::make_tuple(fn, lds, dev);
+    auto it = cache.find(key);
+    if (it != cache.end()) return it->second;
+    int cus = 0, per = 0;
+    if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus < 1) cus = 256;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, fn, threads, lds) != hipSuccess || per < 1) per = 1;
+    return cache[key] = std::min(per, max_per_cu) * cus;
+}
+// grid of a persistent kernel over `units` work units per frame, B frames
+static dim3 resident_grid(const void *fn, int threads, size_t lds, int64_t units, int B, int max_per_cu = 64)
+{
+    const int64_t per_frame = std::max<int64_t>(1, resident_wgs(fn, threads, lds, max_per_cu) / B);
+    return dim3((unsigned)std::max<int64_t>(1, std::min<int64_t>(units, per_frame)), (unsigned)B);
+}
+
 template <int D>
-int launch_arm_d(int nh, dim3 grid, hipStream_t s, const float *yq, const Geo &g, const ArmTiles &at, const float *th,
+int launch_arm_d(int nh, int64_t nblk, int B, hipStream_t s, const float *yq, const Geo &g, const ArmTiles &at, const float *th,
                  int64_t ps, float lam_px, float *gq, float *gth, int64_t gstride, float *acc4, const float *grate,
                  float *rate_out)
 {
@@ -2244,19 +2321,19 @@ int launch_arm_d(int nh, dim3 grid, hipStream_t s, const float *yq, const Geo &g
         // the VALU kernel's tile loop (606 -> 499 us per 8-frame iteration)
         {
             switch (nh) {
-            case 0: hipLaunchKernelGGL((t_arm16<0>), grid, dim3(kT), 0, s, yq, g, at, th, ps, lam_px, gq, gth, gstride, acc4, grate, rate_out); break;
-            case 1: hipLaunchKernelGGL((t_arm16<1>), grid, dim3(kT), 0, s, yq, g, at, th, ps, lam_px, gq, gth, gstride, acc4, grate, rate_out); break;
-            case 2: hipLaunchKernelGGL((t_arm16<2>), grid, dim3(kT), 0, s, yq, g, at, th, ps, lam_px, gq, gth, gstride, acc4, grate, rate_out); break;
-            default: hipLaunchKernelGGL((t_arm16<3>), grid, dim3(kT), 0, s, yq, g, at, th, ps, lam_px, gq, gth, gstride, acc4, grate, rate_out); break;
+            case 0: hipLaunchKernelGGL((t_arm16<0>), resident_grid((const void *)t_arm16<0>, kT, 0, nblk, B), dim3(kT), 0, s, yq, g, at, th, ps, lam_px, gq, gth, gstride, acc4, grate, rate_out); break;
+            case 1: hipLaunchKernelGGL((t_arm16<1>), resident_grid((const void *)t_arm16<1>, kT, 0, nblk, B), dim3(kT), 0, s, yq, g, at, th, ps, lam_px, gq, gth, gstride, acc4, grate, rate_out); break;
+            case 2: hipLaunchKernelGGL((t_arm16<2>), resident_grid((const void *)t_arm16<2>, kT, 0, nblk, B), dim3(kT), 0, s, yq, g, at, th, ps, lam_px, gq, gth, gstride, acc4, grate, rate_out); break;
+            default: hipLaunchKernelGGL((t_arm16<3>), resident_grid((const void *)t_arm16<3>, kT, 0, nblk, B), dim3(kT), 0, s, yq, g, at, th, ps, lam_px, gq, gth, gstride, acc4, grate, rate_out); break;
             }
             return CCMI_OK;
         }
     }
     switch (nh) {
-    case 0: hipLaunchKernelGGL((t_arm<D, 0>), grid, dim3(kT), 0, s, yq, g, at, th, ps, lam_px, gq, gth, gstride, acc4, grate, rate_out); break;
-    case 1: hipLaunchKernelGGL((t_arm<D, 1>), grid, dim3(kT), 0, s, yq, g, at, th, ps, lam_px, gq, gth, gstride, acc4, grate, rate_out); break;
-    case 2: hipLaunchKernelGGL((t_arm<D, 2>), grid, dim3(kT), 0, s, yq, g, at, th, ps, lam_px, gq, gth, gstride, acc4, grate, rate_out); break;
-    default: hipLaunchKernelGGL((t_arm<D, 3>), grid, dim3(kT), 0, s, yq, g, at, th, ps, lam_px, gq, gth, gstride, acc4, grate, rate_out); break;
+    case 0: hipLaunchKernelGGL((t_arm<D, 0>), resident_grid((const void *)t_arm<D, 0>, kT, 0, nblk, B), dim3(kT), 0, s, yq, g, at, th, ps, lam_px, gq, gth, gstride, acc4, grate, rate_out); break;
+    case 1: hipLaunchKernelGGL((t_arm<D, 1>), resident_grid((const void *)t_arm<D, 1>, kT, 0, nblk, B), dim3(kT), 0, s, yq, g, at, th, ps, lam_px, gq, gth, gstride, acc4, grate, rate_out); break;
+    case 2: hipLaunchKernelGGL((t_arm<D, 2>), resident_grid((const void *)t_arm<D, 2>, kT, 0, nblk, B), dim3(kT), 0, s, yq, g, at, th, ps, lam_px, gq, gth, gstride, acc4, grate, rate_out); break;
+    default: hipLaunchKernelGGL((t_arm<D, 3>), resident_grid((const void *)t_arm<D, 3>, kT, 0, nblk, B), dim3(kT), 0, s, yq, g, at, th, ps, lam_px, gq, gth, gstride, acc4, grate, rate_out); break;
     }
     return CCMI_OK;
 }
@@ -2269,8 +2346,13 @@ void launch_head(bool bwd, dim3 grid, hipStream_t s, const float *dense, const f
     else {
         constexpr int kXP = (CIN + 2 > 5 ? CIN + 2 : 5) | 1; // t_head_bwd's per-wave LDS rows
         const size_t lds = sizeof(float) * (kHeadT / 64) * 64 * (16 * ((g.hid + 15) / 16) + 1 + kXP);
+        // one resident round over the pixel chunks, at most 4 workgroups per CU: the occupancy
+        // query allows 5 (32 KB of LDS each), but 5 per CU measured 399 us against 286 us for 4;
+        // 512 / 768 / 2048 workgroups for the batch 515 / 356 / 333 us (profiles/r4n_*, r4o_*)
+        const int64_t nchunk = ((int64_t)g.H * g.W + kHeadT - 1) / kHeadT;
 #define CCMI_HB(N)                                                                                                     \
-    hipLaunchKernelGGL((t_head_bwd<CIN, N, true>), grid, dim3(kHeadT), lds, s, dense, gz0, g, th, ps, z0_or_gdense, gth, gstride)
+    hipLaunchKernelGGL((t_head_bwd<CIN, N, true>), resident_grid((const void *)t_head_bwd<CIN, N, true>, kHeadT, lds, nchunk, (int)grid.y, 4), \
+                       dim3(kHeadT), lds, s, dense, gz0, g, th, ps, z0_or_gdense, gth, gstride)
         switch ((g.hid + 15) / 16) {
         case 1: CCMI_HB(1); break;
         case 2: CCMI_HB(2); break;
@@ -2388,13 +2470,12 @@ extern "C" int ccmi_train_step(const ccmi_train_args *a, void *stream)
                        a->noise, quant_args(a->temperature, a->noise_param), (uint64_t)a->seed, a->step, a->noise_in, yq,
                        dq, gq);
     {
-        // persistent over the latent tiles: about one resident wave of workgroups for the batch
-        dim3 grid((unsigned)std::max(1, std::min(pl.nblk_arm, 2048 / B)), B);
+        // persistent over the latent tiles: one resident round of workgroups for the batch
         switch (g.d) {
-        case 8: launch_arm_d<8>(g.nh, grid, s, yq, g, pl.at, a->params, a->param_stride, lam_px, gq, Gth, GS, acc4, a->grad_rate, a->rate_out); break;
-        case 16: launch_arm_d<16>(g.nh, grid, s, yq, g, pl.at, a->params, a->param_stride, lam_px, gq, Gth, GS, acc4, a->grad_rate, a->rate_out); break;
-        case 24: launch_arm_d<24>(g.nh, grid, s, yq, g, pl.at, a->params, a->param_stride, lam_px, gq, Gth, GS, acc4, a->grad_rate, a->rate_out); break;
-        default: launch_arm_d<32>(g.nh, grid, s, yq, g, pl.at, a->params, a->param_stride, lam_px, gq, Gth, GS, acc4, a->grad_rate, a->rate_out); break;
+        case 8: launch_arm_d<8>(g.nh, pl.nblk_arm, B, s, yq, g, pl.at, a->params, a->param_stride, lam_px, gq, Gth, GS, acc4, a->grad_rate, a->rate_out); break;
+        case 16: launch_arm_d<16>(g.nh, pl.nblk_arm, B, s, yq, g, pl.at, a->params, a->param_stride, lam_px, gq, Gth, GS, acc4, a->grad_rate, a->rate_out); break;
+        case 24: launch_arm_d<24>(g.nh, pl.nblk_arm, B, s, yq, g, pl.at, a->params, a->param_stride, lam_px, gq, Gth, GS, acc4, a->grad_rate, a->rate_out); break;
+        default: launch_arm_d<32>(g.nh, pl.nblk_arm, B, s, yq, g, pl.at, a->params, a->param_stride, lam_px, gq, Gth, GS, acc4, a->grad_rate, a->rate_out); break;
         }
         CCMI_HIP_CHECK(hipGetLastError());
     }
@@ -2467,10 +2548,8 @@ extern "C" int ccmi_train_step(const ccmi_train_args *a, void *stream)
         gcur = gin;
     }
     {
-        // grid-stride over pixel chunks: about one resident wave of workgroups for the batch
-        const int64_t nchunk = (npx + kHeadT - 1) / kHeadT;
-        const unsigned nb = (unsigned)std::max<int64_t>(1, std::min<int64_t>(nchunk, 1024 / B));
-        head_dispatch(g.L, true, dim3(nb, B), s, dense, gcur, g, a->params, a->param_stride, gd, Gth, GS);
+        // grid-stride over pixel chunks: one resident round of workgroups (set by launch_head)
+        head_dispatch(g.L, true, dim3(1, B), s, dense, gcur, g, a->params, a->param_stride, gd, Gth, GS);
     }
 
     // ---- upsampling backward, finest level first (step L-2 .. 0)
