@@ -32,6 +32,7 @@
 #include <map>
 #include <mutex>
 #include <tuple>
+#include <type_traits>
 
 #include "fwd_common.h"
 
@@ -58,9 +59,29 @@ struct Geo {
 
 __device__ __forceinline__ int clampi(int v, int hi) { return v < 0 ? 0 : (v > hi ? hi : v); }
 
+// Sum over the wave, in every lane, without an LDS round trip: DPP within the 16-lane rows
+// (xor 1, xor 2, half-row mirror, row mirror), then gfx950's permlane16 / permlane32 swaps
+// across them.  (The __shfl_xor butterfly is six ds_bpermute_b32 in a dependent chain.)
+template <int CTRL>
+__device__ __forceinline__ float dpp_mov(float v)
+{
+    return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), CTRL, 0xf, 0xf, false));
+}
+__device__ __forceinline__ float wave_sum(float v)
+{
+    v += dpp_mov<0xb1>(v);  // quad_perm [1, 0, 3, 2]: lane ^ 1
+    v += dpp_mov<0x4e>(v);  // quad_perm [2, 3, 0, 1]: lane ^ 2
+    v += dpp_mov<0x141>(v); // row_half_mirror: the other quad of the half-row
+    v += dpp_mov<0x140>(v); // row_mirror: the other half of the row
+    const auto h = __builtin_amdgcn_permlane16_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+    v = __uint_as_float(h[0]) + __uint_as_float(h[1]);
+    const auto q = __builtin_amdgcn_permlane32_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+    return __uint_as_float(q[0]) + __uint_as_float(q[1]);
+}
+
 __device__ __forceinline__ float block_sum(float v, float *red)
 {
-    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
+    v = wave_sum(v);
     const int wid = threadIdx.x >> 6, nw = blockDim.x >> 6;
     __syncthreads();
     if ((threadIdx.x & 63) == 0) red[wid] = v;
@@ -345,7 +366,7 @@ __device__ __forceinline__ void wave_lds_sync()
 // Sum over the wave of v, added to *dst by lane 0.
 __device__ __forceinline__ void wave_add(float v, float *dst)
 {
-    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
+    v = wave_sum(v);
     if ((threadIdx.x & 63) == 0) atomicAdd(dst, v);
 }
 
@@ -1591,8 +1612,7 @@ __device__ __forceinline__ void reduce_taps(float (&dw)[K], float *__restrict__ 
     const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
 #pragma unroll
     for (int k = 0; k < K; ++k) {
-        float v = dw[k];
-        for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
+        const float v = wave_sum(dw[k]);
         if (lane == 0) s_r[wid][k] = v;
     }
     __syncthreads();
@@ -1930,16 +1950,23 @@ __device__ __forceinline__ void up_bwd_tile(float *pool, int bx, const UpBwd &Q)
         }
     }
     __syncthreads();
-    // U: destination column x0 + q reads source columns m0 + (q >> 1) + d
-    for (int i = tid; i < SR * TX; i += kT) {
-        const int r = i / TX, q = i - r * TX, a = q & 1;
-        float acc = 0.f;
+    // U: destination column x0 + q reads source columns m0 + (q >> 1) + d.  A thread takes the
+    // column pair (2 j, 2 j + 1), so the tap index of each parity is a compile-time constant (a
+    // per-lane parity made every w[t] a select chain over the K registers)
+    for (int i = tid; i < SR * TM; i += kT) {
+        const int r = i / TM, j = i - r * TM;
+        float acc[2] = {0.f, 0.f};
 #pragma unroll
         for (int d = DLO; d <= DHI; ++d) {
-            const int t = a + K2 - 1 - 2 * d;
-            if (t >= 0 && t < K) acc = fmaf(w[t], s_s[r][(q >> 1) + d - DLO], acc);
+            const float sv = s_s[r][j + d - DLO];
+#pragma unroll
+            for (int a = 0; a < 2; ++a) {
+                const int t = a + K2 - 1 - 2 * d;
+                if (t >= 0 && t < K) acc[a] = fmaf(w[t], sv, acc[a]);
+            }
         }
-        s_u[r][q] = acc;
+        s_u[r][2 * j] = acc[0];
+        s_u[r][2 * j + 1] = acc[1];
     }
     // GU at source row r0 + tr, destination column gx0 + q
     for (int i = tid; i < TR * GC; i += kT) {
@@ -2003,31 +2030,47 @@ __device__ __forceinline__ void up_bwd_tile(float *pool, int bx, const UpBwd &Q)
         float *o = gsb + (int64_t)r * ws + m;
         *o = accumulate ? *o + acc : acc;
     }
+#if defined(CCMI_DIAG_LVL_NODW)
+    return;
+#endif
     // tap gradients: vertical use (GY x U at the tile's destination rows), horizontal use
     // (GU x S at the tile's source rows)
     float dw[K];
 #pragma unroll
     for (int k = 0; k < K; ++k) dw[k] = 0.f;
-    for (int i = tid; i < 2 * TR * TX; i += kT) {
-        const int ty = i / TX, q = i - ty * TX;
-        if (2 * r0 + ty >= hd || x0 + q >= wd) continue;
-        const float g = s_gy[ty + 2 * DHI][q + 2 * DHI];
-        const int a = ty & 1;
+    // vertical use: destination row ty has parity a = ty & 1 -- with kT a multiple of 2 TX, the
+    // parity of a wave's rows (tid >> 6) never changes: a wave-uniform branch into a loop whose
+    // tap indices are compile-time constants
+    static_assert(kT % (2 * TX) == 0 && TX == 64, "row parity is wave-uniform");
+    auto vertical = [&](auto par) {
+        constexpr int a = decltype(par)::value;
+        for (int i = tid; i < 2 * TR * TX; i += kT) {
+            const int ty = i / TX, q = i - ty * TX;
+            if (2 * r0 + ty >= hd || x0 + q >= wd) continue;
+            const float g = s_gy[ty + 2 * DHI][q + 2 * DHI];
 #pragma unroll
-        for (int d = DLO; d <= DHI; ++d) {
-            const int t = a + K2 - 1 - 2 * d;
-            if (t >= 0 && t < K) dw[t] = fmaf(g, s_u[(ty >> 1) + d - DLO][q], dw[t]);
+            for (int d = DLO; d <= DHI; ++d) {
+                const int t = a + K2 - 1 - 2 * d;
+                if (t >= 0 && t < K) dw[t] = fmaf(g, s_u[(ty >> 1) + d - DLO][q], dw[t]);
+            }
         }
-    }
-    for (int i = tid; i < TR * TX; i += kT) {
-        const int tr = i / TX, q = i - tr * TX;
-        if (r0 + tr >= hs || x0 + q >= wd) continue;
-        const float g = s_gu[tr][q + 2 * DHI];
-        const int a = q & 1;
+    };
+    if (((tid >> 6) & 1) == 0) vertical(std::integral_constant<int, 0>{});
+    else vertical(std::integral_constant<int, 1>{});
+    // horizontal use: a thread takes the column pair (2 j, 2 j + 1), one per parity
+    for (int i = tid; i < TR * TM; i += kT) {
+        const int tr = i / TM, j = i - tr * TM;
+        if (r0 + tr >= hs) continue;
 #pragma unroll
-        for (int d = DLO; d <= DHI; ++d) {
-            const int t = a + K2 - 1 - 2 * d;
-            if (t >= 0 && t < K) dw[t] = fmaf(g, s_s[tr - DLO][(q >> 1) + d - DLO], dw[t]);
+        for (int a = 0; a < 2; ++a) {
+            const int q = 2 * j + a;
+            if (x0 + q >= wd) continue;
+            const float g = s_gu[tr][q + 2 * DHI];
+#pragma unroll
+            for (int d = DLO; d <= DHI; ++d) {
+                const int t = a + K2 - 1 - 2 * d;
+                if (t >= 0 && t < K) dw[t] = fmaf(g, s_s[tr - DLO][j + d - DLO], dw[t]);
+            }
         }
     }
     reduce_taps<K>(dw, slots + ((int64_t)b * kDwSlots + bx % kDwSlots) * gstride + hoff);
@@ -2043,6 +2086,12 @@ __global__ __launch_bounds__(kT) void t_lvl_bwd(RefBwd R, UpBwd Q, int nref)
 {
     constexpr int n = ref_bwd_lds<KP>() > up_bwd_lds<K>() ? ref_bwd_lds<KP>() : up_bwd_lds<K>();
     __shared__ __attribute__((aligned(16))) float pool[n];
+#if defined(CCMI_DIAG_LVL_NOREF) // diagnostic builds only (tools/arm_diag.sh): wrong results
+    if ((int)blockIdx.x < nref) return;
+#endif
+#if defined(CCMI_DIAG_LVL_NOUP)
+    if ((int)blockIdx.x >= nref) return;
+#endif
     if ((int)blockIdx.x < nref) ref_bwd_tile<KP>(pool, blockIdx.x, R);
     else up_bwd_tile<K>(pool, blockIdx.x - nref, Q);
 }

@@ -1,6 +1,6 @@
 #!/bin/bash
-# Round 4, session i: t_arm16 ablations (tools/arm_diag.sh A16_* variants, wrong results by
-# construction, timed only) -- kernel traces of tools/bench_train.py 8 per library.
+# Round 4, sessions i / s: training-kernel ablations (tools/arm_diag.sh A16_* / LVL_* variants,
+# wrong results by construction, timed only) -- kernel traces of tools/bench_train.py 8 per library.
 # Usage: bash tools/gpu_r4i.sh OUTDIR LIB...
 set -u
 ROOT=$(pwd)
