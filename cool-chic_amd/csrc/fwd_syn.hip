@@ -496,13 +496,17 @@ __global__ __launch_bounds__(kFThreads) __attribute__((amdgpu_waves_per_eu(fused
                         const int k = 1 + G * GC + lc;
                         if (k >= CIN) break;
                         const float *h = s_hs + (lc * kHsRows + jj0) * kRW + xi;
-                        float acc = 0.f;
+                        // both parities' chains (compile-time taps), then a select: a per-lane
+                        // parity had made every wu[t] a compare / select chain over the taps
+                        float acc_e = 0.f, acc_o = 0.f;
 #pragma unroll
                         for (int m = 0; m < FT::NS; ++m) {
                             const int te = FT::tap(0, FT::D0 + m), to = FT::tap(1, FT::D0 + m);
-                            if ((a ? to : te) >= 0) acc = fmaf(wu[a ? to : te], h[m * kRW], acc);
+                            const float hv = h[m * kRW];
+                            if (te >= 0) acc_e = fmaf(wu[te], hv, acc_e);
+                            if (to >= 0) acc_o = fmaf(wu[to], hv, acc_o);
                         }
-                        x[p][k] = acc;
+                        x[p][k] = a ? acc_o : acc_e;
                     }
                 }
             }

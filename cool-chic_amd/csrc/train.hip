@@ -1294,8 +1294,7 @@ __global__ __launch_bounds__(kT) __attribute__((amdgpu_waves_per_eu(MODE == 2 ? 
     const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
 #pragma unroll
     for (int e = 0; e < 84; ++e) {
-        float v = acc[e];
-        for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
+        const float v = wave_sum(acc[e]);
         if (lane == 0) s_red[wid][e] = v;
     }
     __syncthreads();
