@@ -1348,7 +1348,9 @@ __global__ __launch_bounds__(kHeadT) void t_head_bwd(const float *__restrict__ d
     // and rows s and s + 16 of the MFMA operand reads land 16 banks apart
     constexpr int kXP = (CIN + 2 > 5 ? CIN + 2 : 5) | 1;
     // hidden unit j: w0[j][0..CIN), b0[j], w1[0..3)[j] -- read back as broadcast ds_read_b128
-    __shared__ __attribute__((aligned(16))) float s_rec[64][12];
+    // (sized for the 16 NT units of the instantiation: 2.3 KB at NT = 3, where 64 units' worth
+    // put the workgroup at exactly 32 KB and five per CU did not fit)
+    __shared__ __attribute__((aligned(16))) float s_rec[16 * NT][12];
     static_assert(CIN + 4 <= 12, "hidden-unit record");
     const int b = blockIdx.y, t = threadIdx.x, lane = t & 63, w = t >> 6;
     const int hid = g.hid; // NT = ceil(hid / 16), a template argument: the accumulator tiles
@@ -1359,9 +1361,9 @@ __global__ __launch_bounds__(kHeadT) void t_head_bwd(const float *__restrict__ d
     // pair records: unit pair jp = units 2jp, 2jp + 1, field f interleaved as [2f + parity]
     constexpr int kPR = 2 * (CIN + 4) <= 24 ? 24 : 32;
     float(*s_rec2)[kPR] = reinterpret_cast<float(*)[kPR]>(&s_rec[0][0]);
-    static_assert(32 * kPR <= 64 * 12, "pair records fit in the record area");
+    static_assert(8 * NT * kPR <= 16 * NT * 12, "pair records fit in the record area");
     if constexpr (!PAIR) {
-        for (int e = t; e < 64 * 12; e += kHeadT) {
+        for (int e = t; e < 16 * NT * 12; e += kHeadT) {
             const int j = e / 12, f = e - j * 12;
             float v = 0.f;
             if (j < hid) {
@@ -1372,7 +1374,7 @@ __global__ __launch_bounds__(kHeadT) void t_head_bwd(const float *__restrict__ d
             s_rec[j][f] = v;
         }
     } else {
-        for (int e = t; e < 32 * kPR; e += kHeadT) {
+        for (int e = t; e < 8 * NT * kPR; e += kHeadT) {
             const int jp = e / kPR, r = e - jp * kPR, f = r >> 1, j = 2 * jp + (r & 1);
             float v = 0.f;
             if (j < hid) {
@@ -2394,12 +2396,13 @@ void launch_head(bool bwd, dim3 grid, hipStream_t s, const float *dense, const f
     else {
         constexpr int kXP = (CIN + 2 > 5 ? CIN + 2 : 5) | 1; // t_head_bwd's per-wave LDS rows
         const size_t lds = sizeof(float) * (kHeadT / 64) * 64 * (16 * ((g.hid + 15) / 16) + 1 + kXP);
-        // one resident round over the pixel chunks, at most 4 workgroups per CU: the occupancy
-        // query allows 5 (32 KB of LDS each), but 5 per CU measured 399 us against 286 us for 4;
-        // 512 / 768 / 2048 workgroups for the batch 515 / 356 / 333 us (profiles/r4n_*, r4o_*)
+        // one resident round over the pixel chunks (LDS-bound: 5 workgroups per CU at 32,000 B
+        // each, 276 us; at exactly 32 KB the query also allowed 5, but they did not all fit: 399
+        // us against 286 us capped at 4; 512 / 768 / 2048 workgroups for the batch 515 / 356 /
+        // 333 us; profiles/r4n_*, r4o_*, r4y_*)
         const int64_t nchunk = ((int64_t)g.H * g.W + kHeadT - 1) / kHeadT;
 #define CCMI_HB(N)                                                                                                     \
-    hipLaunchKernelGGL((t_head_bwd<CIN, N, true>), resident_grid((const void *)t_head_bwd<CIN, N, true>, kHeadT, lds, nchunk, (int)grid.y, 4), \
+    hipLaunchKernelGGL((t_head_bwd<CIN, N, true>), resident_grid((const void *)t_head_bwd<CIN, N, true>, kHeadT, lds, nchunk, (int)grid.y), \
                        dim3(kHeadT), lds, s, dense, gz0, g, th, ps, z0_or_gdense, gth, gstride)
         switch ((g.hid + 15) / 16) {
         case 1: CCMI_HB(1); break;
