@@ -2339,7 +2339,7 @@ int make_plan(const ccmi_train_args *a, Plan &pl)
 // workgroups, and each workgroup's flush costs one atomic per value on addresses every
 // workgroup of the frame shares (t_arm16: 227 us with one round of 1024 workgroups, 232 us
 // with 2048, after the flush reduction; before it 293 vs 460 us, profiles/r4l_*, r4m_*).
-static int resident_wgs(const void *fn, int threads, size_t lds, int max_per_cu)
+static int resident_wgs(const void *fn, int threads, size_t lds)
 {
     static std::mutex mu;
     static std::map<std::tuple<const void *, size_t, int>, int> cache;
@@ -2352,12 +2352,12 @@ static int resident_wgs(const void *fn, int threads, size_t lds, int max_per_cu)
     int cus = 0, per = 0;
     if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus < 1) cus = 256;
     if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, fn, threads, lds) != hipSuccess || per < 1) per = 1;
-    return cache[key] = std::min(per, max_per_cu) * cus;
+    return cache[key] = per * cus;
 }
 // grid of a persistent kernel over `units` work units per frame, B frames
-static dim3 resident_grid(const void *fn, int threads, size_t lds, int64_t units, int B, int max_per_cu = 64)
+static dim3 resident_grid(const void *fn, int threads, size_t lds, int64_t units, int B)
 {
-    const int64_t per_frame = std::max<int64_t>(1, resident_wgs(fn, threads, lds, max_per_cu) / B);
+    const int64_t per_frame = std::max<int64_t>(1, resident_wgs(fn, threads, lds) / B);
     return dim3((unsigned)std::max<int64_t>(1, std::min<int64_t>(units, per_frame)), (unsigned)B);
 }
 
