@@ -244,6 +244,9 @@ __global__ __launch_bounds__(kFThreads) __attribute__((amdgpu_waves_per_eu(fused
     // frame reads the same ones); holding them in registers across the upsampling phases
     // cost spill slots at the 80-VGPR budget
     constexpr int kHeadRegs = (kMaxHid * 16 + kFThreads - 1) / kFThreads;
+    // scaled ReLU for the unrolled VALU head (HID > 0, !MH; launched only with a first-layer ReLU)
+    constexpr bool kScaledRelu = HID > 0 && !MH;
+    constexpr float kW0Scale = kScaledRelu ? 0x1p-32f : 1.f, kW1Scale = kScaledRelu ? 0x1p32f : 1.f;
     auto stage_head = [&]() {
         const int tid = threadIdx.x;
         float hv[kHeadRegs];
@@ -252,9 +255,11 @@ __global__ __launch_bounds__(kFThreads) __attribute__((amdgpu_waves_per_eu(fused
             const int i = tid + k * kFThreads, j = i >> 4, f = i & 15;
             float v = 0.f;
             if (i < kMaxHid * 16 && A.n_head == 2 && j < A.hid) {
-                if (f < CIN) v = prm[A.w0_off + j * CIN + f];
-                else if (f == CIN) v = prm[A.b0_off + j];
-                else if (f <= CIN + CMID) v = prm[A.w1_off + (f - CIN - 1) * A.hid + j];
+                // the unrolled VALU head's records carry the scaled-ReLU exponents (see unit()):
+                // hidden weights / bias x 2^-32, output weights x 2^32 -- exact power-of-two scalings
+                if (f < CIN) v = prm[A.w0_off + j * CIN + f] * kW0Scale;
+                else if (f == CIN) v = prm[A.b0_off + j] * kW0Scale;
+                else if (f <= CIN + CMID) v = prm[A.w1_off + (f - CIN - 1) * A.hid + j] * kW1Scale;
             }
             hv[k] = v;
         }
@@ -614,8 +619,6 @@ __global__ __launch_bounds__(kFThreads) __attribute__((amdgpu_waves_per_eu(fused
             }
         } else if (A.n_head == 2) {
             const int hid = HID > 0 ? HID : A.hid;
-            // fmaxf(acc, lo0) is the optional ReLU without a per-element select
-            const f2 lo0 = f2(A.relu0 ? 0.f : -INFINITY);
             f2 xp[NR / 2][CIN], op[NR / 2][CMID];
 #pragma unroll
             for (int q = 0; q < NR / 2; ++q) {
@@ -637,15 +640,35 @@ __global__ __launch_bounds__(kFThreads) __attribute__((amdgpu_waves_per_eu(fused
                 const lds_f4 p = hb + 4 * (j < hid ? j : hid - 1);
                 return Rec{{p[0], p[1], p[2], p[3]}};
             };
+            // Scaled ReLU: the records hold w0, b0 x 2^-32 and w1 x 2^32 (stage_head), so the
+            // hidden pre-activation arrives as h 2^-32 -- every fma of the chain rounds exactly as
+            // the unscaled one (power-of-two scaling, far from the subnormal / overflow range) --
+            // and max(h, 0) is the last fma's clamp-to-[0, 1] modifier (h <= 2^32): no v_max_f32
+            // per pixel and unit (gfx950 has no packed f32 max; they were 1 in 6 of the head's
+            // VALU instructions).  w1 2^32 x (h 2^-32) = w1 h exactly.
+            const f2 lo0 = f2(A.relu0 ? 0.f : -INFINITY); // the generic head's ReLU (max)
             auto unit = [&](const Rec &r) {
+                constexpr bool RELU = kScaledRelu;
                 const float *u = reinterpret_cast<const float *>(r.v);
                 const f2 bj = f2(u[hr(CIN)]);
+                constexpr int kl = hr(CIN - 1), kp = kl & ~1; // the last hidden weight and its aligned pair
+                const f2 wl = f2{u[kp], u[kp + 1]};
 #pragma unroll
                 for (int q = 0; q < NR / 2; ++q) {
                     f2 acc = bj;
 #pragma unroll
-                    for (int k = 0; k < CIN; ++k) acc = __builtin_elementwise_fma(f2(u[hr(k)]), xp[q][k], acc);
-                    acc = __builtin_elementwise_max(acc, lo0);
+                    for (int k = 0; k < CIN - 1; ++k) acc = __builtin_elementwise_fma(f2(u[hr(k)]), xp[q][k], acc);
+                    if constexpr (RELU) {
+                        f2 h;
+                        if constexpr ((kl & 1) == 0)
+                            asm("v_pk_fma_f32 %0, %1, %2, %3 op_sel_hi:[0,1,1] clamp" : "=v"(h) : "v"(wl), "v"(xp[q][CIN - 1]), "v"(acc));
+                        else
+                            asm("v_pk_fma_f32 %0, %1, %2, %3 op_sel:[1,0,0] op_sel_hi:[1,1,1] clamp" : "=v"(h) : "v"(wl), "v"(xp[q][CIN - 1]), "v"(acc));
+                        acc = h;
+                    } else {
+                        acc = __builtin_elementwise_fma(f2(u[kl]), xp[q][CIN - 1], acc);
+                        acc = __builtin_elementwise_max(acc, lo0);
+                    }
 #pragma unroll
                     for (int m = 0; m < CMID; ++m) op[q][m] = __builtin_elementwise_fma(f2(u[hr(CIN + 1 + m)]), acc, op[q][m]);
                 }
@@ -886,7 +909,7 @@ template <int CMID, bool UPS>
 void launch_fused(dim3 grid, hipStream_t s, const FusedArgs &fa, const LevelArgs &u)
 {
     // the presets' 7-grid decoders with a 48-wide head (hop and its relatives): unrolled head
-    if (fa.cin == 7 && fa.n_head == 2 && fa.hid == 48) {
+    if (fa.cin == 7 && fa.n_head == 2 && fa.hid == 48 && fa.relu0) { // (its scaled ReLU assumes one)
         hipLaunchKernelGGL((syn_fused_kernel<7, CMID, UPS, false, 48>), grid, dim3(kFThreads), 0, s, fa, u);
         return;
     }
