@@ -2106,19 +2106,20 @@ __global__ void t_zero_rows(float *__restrict__ p, int64_t n, int64_t stride)
 
 // dL/dy of the latents (G[0, N) = dL/dyhat * dyhat/dy) and the squared norm of the whole
 // gradient row (latents + parameters, clip_grad_norm_) in one pass
-__global__ __launch_bounds__(kT) void t_latgrad_sumsq(const float *__restrict__ gq, const float *__restrict__ dq, int N,
-                                                      float *__restrict__ G, int64_t n, int64_t gstride,
-                                                      float *__restrict__ acc4)
+__global__ __launch_bounds__(kT) void t_latgrad_sumsq(const float *__restrict__ gq, const float *__restrict__ gq2,
+                                                      const float *__restrict__ dq, int N, float *__restrict__ G,
+                                                      int64_t n, int64_t gstride, float *__restrict__ acc4)
 {
     __shared__ float s_red[8];
     const int b = blockIdx.y;
     float *g = G + (int64_t)b * gstride;
     const float *gqb = gq + (int64_t)b * N, *dqb = dq + (int64_t)b * N;
+    const float *gq2b = gq2 ? gq2 + (int64_t)b * N : nullptr; // the ARM's part (side-stream form)
     float s = 0.f;
     for (int64_t i = (int64_t)blockIdx.x * kT + threadIdx.x; i < n; i += (int64_t)gridDim.x * kT) {
         float v;
         if (i < N) {
-            v = gqb[i] * dqb[i];
+            v = (gq2b ? gq2b[i] + gqb[i] : gqb[i]) * dqb[i];
             g[i] = v;
         } else {
             v = g[i];
@@ -2192,11 +2193,21 @@ __global__ void t_finish(const float *__restrict__ acc4, float inv_total, float 
 // ------------------------------------------------------------------ host planning
 size_t align256(size_t v) { return (v + 255) / 256 * 256; }
 
+// CCMI_ARM_OVERLAP = k > 0: the ARM forward + backward runs on a side stream, concurrently with
+// the synthesis / upsampling forward and backward, with at most k workgroups per CU (its latent
+// gradients in their own buffer, summed by t_latgrad_sumsq).  k = 1: the latency-bound ARM
+// fills what the chain's kernels leave of each CU (8-frame 512x768 step 1.112 / 1.117 ->
+// 1.049 / 1.050 ms; k = 2: 1.067 / 1.072, k = 3: 1.084 / 1.076; profiles/r4ah_*).  With the
+// full resident grid (round 4, earlier) it took every CU's LDS and the chain queued behind it.
+#ifndef CCMI_ARM_OVERLAP
+#define CCMI_ARM_OVERLAP 1
+#endif
 struct Plan {
     Geo g;
     ArmTiles at;
     int B, nblk_arm;
     // workspace offsets (bytes)
+    size_t gq_arm = 0; // the ARM's latent gradients when it runs on the side stream (CCMI_ARM_OVERLAP)
     size_t yq, dq, gq, kf, stacks, stacks_bytes, dense, z[kMaxSp + 1], graw, gbuf[2], gdense, gstack, tmpU, tmpG, G,
         acc4, bc, slots, total;
     int64_t gstack_off[CCMI_MAX_GRIDS]; // per level k (1..L-2) inside gstack, elements per frame
@@ -2330,6 +2341,7 @@ int make_plan(const ccmi_train_args *a, Plan &pl)
     pl.acc4 = take(4 * B * 4);
     pl.bc = take(4 * B * 2);
     pl.slots = take(4 * B * kDwSlots * (size_t)(g.syn_off - g.up_off));
+    if (CCMI_ARM_OVERLAP) pl.gq_arm = take(4 * B * g.N); // after acc4: zeroed with it
     pl.total = o;
     return CCMI_OK;
 }
@@ -2339,30 +2351,30 @@ int make_plan(const ccmi_train_args *a, Plan &pl)
 // workgroups, and each workgroup's flush costs one atomic per value on addresses every
 // workgroup of the frame shares (t_arm16: 227 us with one round of 1024 workgroups, 232 us
 // with 2048, after the flush reduction; before it 293 vs 460 us, profiles/r4l_*, r4m_*).
-static int resident_wgs(const void *fn, int threads, size_t lds)
+static int resident_wgs(const void *fn, int threads, size_t lds, int max_per_cu)
 {
     static std::mutex mu;
-    static std::map<std::tuple<const void *, size_t, int>, int> cache;
+    static std::map<std::tuple<const void *, size_t, int, int>, int> cache;
     int dev = 0;
     if (hipGetDevice(&dev) != hipSuccess) dev = 0;
     std::lock_guard<std::mutex> lk(mu);
-    const auto key = std::make_tuple(fn, lds, dev);
+    const auto key = std::make_tuple(fn, lds, dev, max_per_cu);
     auto it = cache.find(key);
     if (it != cache.end()) return it->second;
     int cus = 0, per = 0;
     if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus < 1) cus = 256;
     if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, fn, threads, lds) != hipSuccess || per < 1) per = 1;
-    return cache[key] = per * cus;
+    return cache[key] = std::min(per, max_per_cu) * cus;
 }
 // grid of a persistent kernel over `units` work units per frame, B frames
-static dim3 resident_grid(const void *fn, int threads, size_t lds, int64_t units, int B)
+static dim3 resident_grid(const void *fn, int threads, size_t lds, int64_t units, int B, int max_per_cu = 1 << 20)
 {
-    const int64_t per_frame = std::max<int64_t>(1, resident_wgs(fn, threads, lds) / B);
+    const int64_t per_frame = std::max<int64_t>(1, resident_wgs(fn, threads, lds, max_per_cu) / B);
     return dim3((unsigned)std::max<int64_t>(1, std::min<int64_t>(units, per_frame)), (unsigned)B);
 }
 
 template <int D>
-int launch_arm_d(int nh, int64_t nblk, int B, hipStream_t s, const float *yq, const Geo &g, const ArmTiles &at, const float *th,
+int launch_arm_d(int nh, int64_t nblk, int B, int cap, hipStream_t s, const float *yq, const Geo &g, const ArmTiles &at, const float *th,
                  int64_t ps, float lam_px, float *gq, float *gth, int64_t gstride, float *acc4, const float *grate,
                  float *rate_out)
 {
@@ -2371,19 +2383,19 @@ int launch_arm_d(int nh, int64_t nblk, int B, hipStream_t s, const float *yq, co
         // the VALU kernel's tile loop (606 -> 499 us per 8-frame iteration)
         {
             switch (nh) {
-            case 0: hipLaunchKernelGGL((t_arm16<0>), resident_grid((const void *)t_arm16<0>, kT, 0, nblk, B), dim3(kT), 0, s, yq, g, at, th, ps, lam_px, gq, gth, gstride, acc4, grate, rate_out); break;
-            case 1: hipLaunchKernelGGL((t_arm16<1>), resident_grid((const void *)t_arm16<1>, kT, 0, nblk, B), dim3(kT), 0, s, yq, g, at, th, ps, lam_px, gq, gth, gstride, acc4, grate, rate_out); break;
-            case 2: hipLaunchKernelGGL((t_arm16<2>), resident_grid((const void *)t_arm16<2>, kT, 0, nblk, B), dim3(kT), 0, s, yq, g, at, th, ps, lam_px, gq, gth, gstride, acc4, grate, rate_out); break;
-            default: hipLaunchKernelGGL((t_arm16<3>), resident_grid((const void *)t_arm16<3>, kT, 0, nblk, B), dim3(kT), 0, s, yq, g, at, th, ps, lam_px, gq, gth, gstride, acc4, grate, rate_out); break;
+            case 0: hipLaunchKernelGGL((t_arm16<0>), resident_grid((const void *)t_arm16<0>, kT, 0, nblk, B, cap), dim3(kT), 0, s, yq, g, at, th, ps, lam_px, gq, gth, gstride, acc4, grate, rate_out); break;
+            case 1: hipLaunchKernelGGL((t_arm16<1>), resident_grid((const void *)t_arm16<1>, kT, 0, nblk, B, cap), dim3(kT), 0, s, yq, g, at, th, ps, lam_px, gq, gth, gstride, acc4, grate, rate_out); break;
+            case 2: hipLaunchKernelGGL((t_arm16<2>), resident_grid((const void *)t_arm16<2>, kT, 0, nblk, B, cap), dim3(kT), 0, s, yq, g, at, th, ps, lam_px, gq, gth, gstride, acc4, grate, rate_out); break;
+            default: hipLaunchKernelGGL((t_arm16<3>), resident_grid((const void *)t_arm16<3>, kT, 0, nblk, B, cap), dim3(kT), 0, s, yq, g, at, th, ps, lam_px, gq, gth, gstride, acc4, grate, rate_out); break;
             }
             return CCMI_OK;
         }
     }
     switch (nh) {
-    case 0: hipLaunchKernelGGL((t_arm<D, 0>), resident_grid((const void *)t_arm<D, 0>, kT, 0, nblk, B), dim3(kT), 0, s, yq, g, at, th, ps, lam_px, gq, gth, gstride, acc4, grate, rate_out); break;
-    case 1: hipLaunchKernelGGL((t_arm<D, 1>), resident_grid((const void *)t_arm<D, 1>, kT, 0, nblk, B), dim3(kT), 0, s, yq, g, at, th, ps, lam_px, gq, gth, gstride, acc4, grate, rate_out); break;
-    case 2: hipLaunchKernelGGL((t_arm<D, 2>), resident_grid((const void *)t_arm<D, 2>, kT, 0, nblk, B), dim3(kT), 0, s, yq, g, at, th, ps, lam_px, gq, gth, gstride, acc4, grate, rate_out); break;
-    default: hipLaunchKernelGGL((t_arm<D, 3>), resident_grid((const void *)t_arm<D, 3>, kT, 0, nblk, B), dim3(kT), 0, s, yq, g, at, th, ps, lam_px, gq, gth, gstride, acc4, grate, rate_out); break;
+    case 0: hipLaunchKernelGGL((t_arm<D, 0>), resident_grid((const void *)t_arm<D, 0>, kT, 0, nblk, B, cap), dim3(kT), 0, s, yq, g, at, th, ps, lam_px, gq, gth, gstride, acc4, grate, rate_out); break;
+    case 1: hipLaunchKernelGGL((t_arm<D, 1>), resident_grid((const void *)t_arm<D, 1>, kT, 0, nblk, B, cap), dim3(kT), 0, s, yq, g, at, th, ps, lam_px, gq, gth, gstride, acc4, grate, rate_out); break;
+    case 2: hipLaunchKernelGGL((t_arm<D, 2>), resident_grid((const void *)t_arm<D, 2>, kT, 0, nblk, B, cap), dim3(kT), 0, s, yq, g, at, th, ps, lam_px, gq, gth, gstride, acc4, grate, rate_out); break;
+    default: hipLaunchKernelGGL((t_arm<D, 3>), resident_grid((const void *)t_arm<D, 3>, kT, 0, nblk, B, cap), dim3(kT), 0, s, yq, g, at, th, ps, lam_px, gq, gth, gstride, acc4, grate, rate_out); break;
     }
     return CCMI_OK;
 }
@@ -2480,6 +2492,33 @@ extern "C" size_t ccmi_train_workspace_bytes(const ccmi_train_args *a)
     return pl.total;
 }
 
+// a side stream and its fork / join events, one per host thread and device (CCMI_ARM_OVERLAP)
+struct SideStream {
+    int device = -1;
+    hipStream_t st = nullptr;
+    hipEvent_t fork = nullptr, join = nullptr;
+};
+static SideStream *side_stream()
+{
+    static thread_local SideStream ss;
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess) return nullptr;
+    if (ss.device != dev) {
+        if (ss.st) {
+            (void)hipStreamDestroy(ss.st);
+            (void)hipEventDestroy(ss.fork);
+            (void)hipEventDestroy(ss.join);
+        }
+        ss = SideStream{};
+        if (hipStreamCreateWithFlags(&ss.st, hipStreamNonBlocking) != hipSuccess ||
+            hipEventCreateWithFlags(&ss.fork, hipEventDisableTiming) != hipSuccess ||
+            hipEventCreateWithFlags(&ss.join, hipEventDisableTiming) != hipSuccess)
+            return nullptr;
+        ss.device = dev;
+    }
+    return &ss;
+}
+
 extern "C" int ccmi_train_step(const ccmi_train_args *a, void *stream)
 {
     if (!a || !a->latent || !a->params || !a->target) return ccmi_set_error(CCMI_ERR_ARG, "train: null argument");
@@ -2520,15 +2559,30 @@ extern "C" int ccmi_train_step(const ccmi_train_args *a, void *stream)
     hipLaunchKernelGGL(t_quant, grid1(g.N, B), dim3(kT), 0, s, a->latent, a->latent_stride, g.N, a->gain, a->quantizer,
                        a->noise, quant_args(a->temperature, a->noise_param), (uint64_t)a->seed, a->step, a->noise_in, yq,
                        dq, gq);
+    SideStream *side = nullptr;
     {
-        // persistent over the latent tiles: one resident round of workgroups for the batch
+        // persistent over the latent tiles: one resident round of workgroups for the batch (or,
+        // with CCMI_ARM_OVERLAP, at most that many per CU, on the side stream)
+        hipStream_t sa = s;
+        float *gqa = gq;
+        int cap = 1 << 20;
+        if (CCMI_ARM_OVERLAP > 0) {
+            side = side_stream();
+            if (!side) return ccmi_set_error(CCMI_ERR_HIP, "train: side stream");
+            CCMI_HIP_CHECK(hipEventRecord(side->fork, s));
+            CCMI_HIP_CHECK(hipStreamWaitEvent(side->st, side->fork, 0));
+            sa = side->st;
+            gqa = F(pl.gq_arm);
+            cap = CCMI_ARM_OVERLAP;
+        }
         switch (g.d) {
-        case 8: launch_arm_d<8>(g.nh, pl.nblk_arm, B, s, yq, g, pl.at, a->params, a->param_stride, lam_px, gq, Gth, GS, acc4, a->grad_rate, a->rate_out); break;
-        case 16: launch_arm_d<16>(g.nh, pl.nblk_arm, B, s, yq, g, pl.at, a->params, a->param_stride, lam_px, gq, Gth, GS, acc4, a->grad_rate, a->rate_out); break;
-        case 24: launch_arm_d<24>(g.nh, pl.nblk_arm, B, s, yq, g, pl.at, a->params, a->param_stride, lam_px, gq, Gth, GS, acc4, a->grad_rate, a->rate_out); break;
-        default: launch_arm_d<32>(g.nh, pl.nblk_arm, B, s, yq, g, pl.at, a->params, a->param_stride, lam_px, gq, Gth, GS, acc4, a->grad_rate, a->rate_out); break;
+        case 8: launch_arm_d<8>(g.nh, pl.nblk_arm, B, cap, sa, yq, g, pl.at, a->params, a->param_stride, lam_px, gqa, Gth, GS, acc4, a->grad_rate, a->rate_out); break;
+        case 16: launch_arm_d<16>(g.nh, pl.nblk_arm, B, cap, sa, yq, g, pl.at, a->params, a->param_stride, lam_px, gqa, Gth, GS, acc4, a->grad_rate, a->rate_out); break;
+        case 24: launch_arm_d<24>(g.nh, pl.nblk_arm, B, cap, sa, yq, g, pl.at, a->params, a->param_stride, lam_px, gqa, Gth, GS, acc4, a->grad_rate, a->rate_out); break;
+        default: launch_arm_d<32>(g.nh, pl.nblk_arm, B, cap, sa, yq, g, pl.at, a->params, a->param_stride, lam_px, gqa, Gth, GS, acc4, a->grad_rate, a->rate_out); break;
         }
         CCMI_HIP_CHECK(hipGetLastError());
+        if (side) CCMI_HIP_CHECK(hipEventRecord(side->join, side->st));
     }
     {
         ccmi_ups_args u{};
@@ -2675,7 +2729,9 @@ extern "C" int ccmi_train_step(const ccmi_train_args *a, void *stream)
     // ---- latent gradients, norm, Adam
     // about eight workgroups per CU over the batch, 4+ elements per thread
     const unsigned nls = (unsigned)std::max<int64_t>(1, std::min<int64_t>(ccmi_div_up(GS, 4 * kT), std::max(1, 2048 / B)));
-    hipLaunchKernelGGL(t_latgrad_sumsq, dim3(nls, B), dim3(kT), 0, s, gq, dq, g.N, G, GS, GS, acc4);
+    if (side) CCMI_HIP_CHECK(hipStreamWaitEvent(s, side->join, 0));
+    hipLaunchKernelGGL(t_latgrad_sumsq, dim3(nls, B), dim3(kT), 0, s, gq, side ? F(pl.gq_arm) : nullptr, dq, g.N, G, GS,
+                       GS, acc4);
     const float total = a->yuv420 ? (float)(npx + 2 * (int64_t)(g.H / 2) * (g.W / 2)) : (float)(3 * npx);
     if (a->loss_out) hipLaunchKernelGGL(t_finish, dim3(1), dim3(std::max(64, B)), 0, s, acc4, 1.f / total, lam_px, a->loss_out, B);
     if (a->update) {
