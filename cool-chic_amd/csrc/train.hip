@@ -2606,7 +2606,10 @@ extern "C" int ccmi_train_step(const ccmi_train_args *a, void *stream)
         u.workspace = F(pl.stacks);
         u.workspace_bytes = pl.stacks_bytes + 4;
         u.batch = B;
-        if (int rc = ccmi_launch_ups_f32(&u, s)) return rc;
+        if (int rc = ccmi_launch_ups_f32(&u, s)) {
+            if (side) (void)hipStreamWaitEvent(s, side->join, 0); // the side stream's work stays ordered
+            return rc;
+        }
     }
     head_dispatch(g.L, false, dim3((unsigned)((npx + 2 * kT - 1) / (2 * kT)), (unsigned)B), s, dense, nullptr, g, a->params,
                   a->param_stride, F(pl.z[0]), nullptr, 0); // two pixels per thread
@@ -2616,6 +2619,8 @@ extern "C" int ccmi_train_step(const ccmi_train_args *a, void *stream)
     if (a->raw_out)
         CCMI_HIP_CHECK(hipMemcpyAsync(a->raw_out, F(pl.z[g.n_sp]), sizeof(float) * 3 * npx * B, hipMemcpyDeviceToDevice, s));
     if (a->forward_only) {
+        // the ARM's rate (rate_out, the rate sums in acc4) comes from the side stream
+        if (side) CCMI_HIP_CHECK(hipStreamWaitEvent(s, side->join, 0));
         if (a->loss_out) {
             // with a real target (target_stride > 0) the loss row holds the built-in MSE too;
             // otherwise (autograd: the loss lives in torch) MSE reads 0 and loss = lmbda-rate
