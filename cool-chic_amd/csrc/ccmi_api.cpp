@@ -5,6 +5,8 @@
 #include <stdarg.h>
 #include <stdio.h>
 
+#include <mutex>
+
 #include "ccmi_internal.h"
 
 static thread_local char g_err[512] = "";
@@ -16,6 +18,52 @@ int ccmi_set_error(int code, const char *fmt, ...)
     vsnprintf(g_err, sizeof g_err, fmt, ap);
     va_end(ap);
     return code;
+}
+
+static std::mutex g_pool_mu;
+static std::vector<StreamSet *> g_pool; // free sets
+
+StreamSet *ccmi_streamset_acquire(int nst, int nev, bool timing)
+{
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess) {
+        ccmi_set_error(CCMI_ERR_HIP, "stream pool: hipGetDevice failed");
+        return nullptr;
+    }
+    {
+        std::lock_guard<std::mutex> lk(g_pool_mu);
+        for (size_t i = 0; i < g_pool.size(); ++i) {
+            StreamSet *s = g_pool[i];
+            if (s->device == dev && s->timing == timing && (int)s->st.size() >= nst && (int)s->ev.size() >= nev) {
+                g_pool.erase(g_pool.begin() + (long)i);
+                return s;
+            }
+        }
+    }
+    StreamSet *s = new StreamSet;
+    s->device = dev;
+    s->timing = timing;
+    s->st.assign(nst, nullptr);
+    s->ev.assign(nev, nullptr);
+    bool ok = true;
+    for (auto &x : s->st) ok = ok && hipStreamCreateWithFlags(&x, hipStreamNonBlocking) == hipSuccess;
+    for (auto &x : s->ev) ok = ok && (timing ? hipEventCreate(&x) : hipEventCreateWithFlags(&x, hipEventDisableTiming)) == hipSuccess;
+    if (!ok) {
+        ccmi_set_error(CCMI_ERR_HIP, "stream pool: stream / event creation failed");
+        for (auto x : s->st)
+            if (x) (void)hipStreamDestroy(x);
+        for (auto x : s->ev)
+            if (x) (void)hipEventDestroy(x);
+        delete s;
+        return nullptr;
+    }
+    return s;
+}
+
+void ccmi_streamset_release(StreamSet *set)
+{
+    std::lock_guard<std::mutex> lk(g_pool_mu);
+    g_pool.push_back(set);
 }
 
 extern "C" const char *ccmi_last_error(void) { return g_err; }

@@ -5,6 +5,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <vector>
+
 #include "../../include/ccmi.h"
 
 #define CCMI_MAX_GRIDS 8
@@ -37,3 +39,29 @@ int ccmi_launch_arm_f32(const ccmi_arm_args *a, hipStream_t s);
 int ccmi_launch_ups_f32(const ccmi_ups_args *a, hipStream_t s);
 int ccmi_launch_syn_f32(const ccmi_syn_args *a, hipStream_t s);
 int ccmi_launch_post_f32(const ccmi_post_args *a, hipStream_t s);
+
+// Process-wide pool of side streams and events, one set per concurrent user and device
+// (train.hip's ARM side stream, dec_host.cpp's chunk streams).  A set is leased for one call
+// and returned to the pool afterwards, so threads that come and go (thread pools) reuse the
+// same few streams instead of leaking one per thread; sets are never destroyed (the runtime
+// may be gone at process exit).
+struct StreamSet {
+    int device = -1;
+    bool timing = false;
+    std::vector<hipStream_t> st;
+    std::vector<hipEvent_t> ev;
+};
+// A set on the current device with >= nst streams and >= nev events (timing events when
+// `timing`), nullptr with the error message set on failure.
+StreamSet *ccmi_streamset_acquire(int nst, int nev, bool timing);
+void ccmi_streamset_release(StreamSet *set);
+struct StreamSetLease {
+    StreamSet *set = nullptr;
+    StreamSetLease() = default;
+    StreamSetLease(const StreamSetLease &) = delete;
+    StreamSetLease &operator=(const StreamSetLease &) = delete;
+    ~StreamSetLease()
+    {
+        if (set) ccmi_streamset_release(set);
+    }
+};

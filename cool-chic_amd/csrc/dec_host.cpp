@@ -676,30 +676,19 @@ int decode_many(const uint8_t *const *streams, const size_t *lens, int n, uint8_
         return CCMI_OK;
     };
     // K > 1: streams forked from s after the uploads; each chunk runs ARM -> tail -> download on
-    // its stream, and s waits for every chunk before it returns.  The extra stream and the
-    // events are created once per thread and device, and kept (never destroyed at exit, when
-    // the runtime may be gone).
-    struct ForkCache {
-        int device = -1;
-        std::vector<hipStream_t> st;
-        std::vector<hipEvent_t> ev; // [0] fork; per chunk c: [1 + 4c] start, [2 + 4c] ARM done, [3 + 4c] tail done, [4 + 4c] done
-    };
-    static thread_local ForkCache fk;
+    // its stream, and s waits for every chunk before it returns.  The extra streams and the
+    // events are leased from the process-wide pool (ccmi_api.cpp) for this call: st[c] for
+    // chunks c >= 1 (chunk 0 runs on s), ev[0] fork; per chunk c: [1 + 4c] start, [2 + 4c] ARM
+    // done, [3 + 4c] tail done, [4 + 4c] done.
+    StreamSetLease lease;
     if (K == 1) {
         if (int rc = launch_chunk(0, s, ev.ok ? ev.e[2] : nullptr)) return rc;
         ev.rec(3, s);
         if (int rc = download_chunk(0, s)) return rc;
     } else {
-        int device = 0;
-        CCMI_HIP_CHECK(hipGetDevice(&device));
-        if (fk.device != device || (int)fk.st.size() < K || fk.ev.size() < (size_t)(1 + 4 * K)) {
-            fk.device = -1; // rebuilt below; the old ones are left to the runtime
-            fk.st.assign(K, nullptr);
-            fk.ev.assign(1 + 4 * K, nullptr);
-            for (int c = 1; c < K; ++c) CCMI_HIP_CHECK(hipStreamCreateWithFlags(&fk.st[c], hipStreamNonBlocking));
-            for (auto &x : fk.ev) CCMI_HIP_CHECK(hipEventCreate(&x));
-            fk.device = device;
-        }
+        lease.set = ccmi_streamset_acquire(K, 1 + 4 * K, true);
+        if (!lease.set) return CCMI_ERR_HIP;
+        StreamSet &fk = *lease.set;
         // an error after some chunks were queued: s still waits for them before the caller can
         // reuse or free the workspace (the chunks' own streams never outlive it unjoined)
         int started = 0;
@@ -709,10 +698,9 @@ int decode_many(const uint8_t *const *streams, const size_t *lens, int n, uint8_
                 (void)hipStreamWaitEvent(s, fk.ev[4 + 4 * c], 0);
             }
         };
-        fk.st[0] = s;
         CCMI_HIP_CHECK(hipEventRecord(fk.ev[0], s));
         for (int c = K - 1; c >= 0; --c) { // the most expensive chunk first
-            hipStream_t cs = fk.st[c];
+            hipStream_t cs = c == 0 ? s : fk.st[c];
             if (c > 0) {
                 if (hipStreamWaitEvent(cs, fk.ev[0], 0) != hipSuccess) {
                     join();
@@ -761,6 +749,7 @@ int decode_many(const uint8_t *const *streams, const size_t *lens, int n, uint8_
             float span = 0.f, arm = 0.f, all = 0.f;
             (void)hipEventElapsedTime(&g_last_ms[0], ev.e[0], ev.e[1]);
             (void)hipEventElapsedTime(&all, ev.e[1], ev.e[4]);
+            const StreamSet &fk = *lease.set;
             for (int c = 0; c < K; ++c) {
                 float t = 0.f;
                 if (hipEventElapsedTime(&t, fk.ev[1 + 4 * c], fk.ev[2 + 4 * c]) == hipSuccess) arm = std::max(arm, t);

@@ -2492,32 +2492,38 @@ extern "C" size_t ccmi_train_workspace_bytes(const ccmi_train_args *a)
     return pl.total;
 }
 
-// a side stream and its fork / join events, one per host thread and device (CCMI_ARM_OVERLAP)
-struct SideStream {
-    int device = -1;
-    hipStream_t st = nullptr;
-    hipEvent_t fork = nullptr, join = nullptr;
-};
-static SideStream *side_stream()
-{
-    static thread_local SideStream ss;
-    int dev = 0;
-    if (hipGetDevice(&dev) != hipSuccess) return nullptr;
-    if (ss.device != dev) {
-        if (ss.st) {
-            (void)hipStreamDestroy(ss.st);
-            (void)hipEventDestroy(ss.fork);
-            (void)hipEventDestroy(ss.join);
-        }
-        ss = SideStream{};
-        if (hipStreamCreateWithFlags(&ss.st, hipStreamNonBlocking) != hipSuccess ||
-            hipEventCreateWithFlags(&ss.fork, hipEventDisableTiming) != hipSuccess ||
-            hipEventCreateWithFlags(&ss.join, hipEventDisableTiming) != hipSuccess)
-            return nullptr;
-        ss.device = dev;
+// The ARM's side stream (CCMI_ARM_OVERLAP): leased from the process-wide pool for one call
+// (ccmi_api.cpp; st[0], events ev[0] fork and ev[1] join).  SideJoin orders the side stream
+// back into the caller's stream on EVERY exit after the fork: the explicit waits (forward-only
+// return, before t_latgrad_sumsq) and, through its destructor, every error return in between,
+// so no ARM kernel can still be writing gq_arm / acc4 / Gth / rate_out once the call returned.
+struct SideJoin {
+    hipStream_t s = nullptr, side = nullptr;
+    hipEvent_t ev = nullptr;
+    bool recorded = false, pending = false;
+    void record()
+    {
+        if (pending && !recorded) recorded = hipEventRecord(ev, side) == hipSuccess;
     }
-    return &ss;
+    hipError_t wait()
+    {
+        if (!pending) return hipSuccess;
+        record();
+        pending = false;
+        return recorded ? hipStreamWaitEvent(s, ev, 0) : hipStreamSynchronize(side);
+    }
+    ~SideJoin() { (void)wait(); }
+};
+
+#if defined(CCMI_DIAG_SIDE_SPIN)
+// Diagnostic build only (make spin): ~5 ms of spinning queued on the side stream before the
+// ARM, so a consumer that reads the ARM's outputs without the join sees stale data every time.
+__global__ void t_diag_spin(uint64_t ticks)
+{
+    const uint64_t t0 = __builtin_amdgcn_s_memrealtime(); // 100 MHz constant clock
+    while (__builtin_amdgcn_s_memrealtime() - t0 < ticks) __builtin_amdgcn_s_sleep(8);
 }
+#endif
 
 extern "C" int ccmi_train_step(const ccmi_train_args *a, void *stream)
 {
@@ -2559,7 +2565,9 @@ extern "C" int ccmi_train_step(const ccmi_train_args *a, void *stream)
     hipLaunchKernelGGL(t_quant, grid1(g.N, B), dim3(kT), 0, s, a->latent, a->latent_stride, g.N, a->gain, a->quantizer,
                        a->noise, quant_args(a->temperature, a->noise_param), (uint64_t)a->seed, a->step, a->noise_in, yq,
                        dq, gq);
-    SideStream *side = nullptr;
+    StreamSetLease lease; // declared before the join: released after it
+    SideJoin join;
+    bool side = false;
     {
         // persistent over the latent tiles: one resident round of workgroups for the batch (or,
         // with CCMI_ARM_OVERLAP, at most that many per CU, on the side stream)
@@ -2567,13 +2575,21 @@ extern "C" int ccmi_train_step(const ccmi_train_args *a, void *stream)
         float *gqa = gq;
         int cap = 1 << 20;
         if (CCMI_ARM_OVERLAP > 0) {
-            side = side_stream();
-            if (!side) return ccmi_set_error(CCMI_ERR_HIP, "train: side stream");
-            CCMI_HIP_CHECK(hipEventRecord(side->fork, s));
-            CCMI_HIP_CHECK(hipStreamWaitEvent(side->st, side->fork, 0));
-            sa = side->st;
+            lease.set = ccmi_streamset_acquire(1, 2, false);
+            if (!lease.set) return CCMI_ERR_HIP;
+            CCMI_HIP_CHECK(hipEventRecord(lease.set->ev[0], s));
+            CCMI_HIP_CHECK(hipStreamWaitEvent(lease.set->st[0], lease.set->ev[0], 0));
+            side = true;
+            sa = lease.set->st[0];
+            join.s = s;
+            join.side = sa;
+            join.ev = lease.set->ev[1];
+            join.pending = true; // from here on every return joins
             gqa = F(pl.gq_arm);
             cap = CCMI_ARM_OVERLAP;
+#if defined(CCMI_DIAG_SIDE_SPIN)
+            hipLaunchKernelGGL(t_diag_spin, dim3(1), dim3(64), 0, sa, (uint64_t)500000);
+#endif
         }
         switch (g.d) {
         case 8: launch_arm_d<8>(g.nh, pl.nblk_arm, B, cap, sa, yq, g, pl.at, a->params, a->param_stride, lam_px, gqa, Gth, GS, acc4, a->grad_rate, a->rate_out); break;
@@ -2582,7 +2598,7 @@ extern "C" int ccmi_train_step(const ccmi_train_args *a, void *stream)
         default: launch_arm_d<32>(g.nh, pl.nblk_arm, B, cap, sa, yq, g, pl.at, a->params, a->param_stride, lam_px, gqa, Gth, GS, acc4, a->grad_rate, a->rate_out); break;
         }
         CCMI_HIP_CHECK(hipGetLastError());
-        if (side) CCMI_HIP_CHECK(hipEventRecord(side->join, side->st));
+        join.record();
     }
     {
         ccmi_ups_args u{};
@@ -2606,10 +2622,7 @@ extern "C" int ccmi_train_step(const ccmi_train_args *a, void *stream)
         u.workspace = F(pl.stacks);
         u.workspace_bytes = pl.stacks_bytes + 4;
         u.batch = B;
-        if (int rc = ccmi_launch_ups_f32(&u, s)) {
-            if (side) (void)hipStreamWaitEvent(s, side->join, 0); // the side stream's work stays ordered
-            return rc;
-        }
+        if (int rc = ccmi_launch_ups_f32(&u, s)) return rc; // joined by ~SideJoin
     }
     head_dispatch(g.L, false, dim3((unsigned)((npx + 2 * kT - 1) / (2 * kT)), (unsigned)B), s, dense, nullptr, g, a->params,
                   a->param_stride, F(pl.z[0]), nullptr, 0); // two pixels per thread
@@ -2620,7 +2633,7 @@ extern "C" int ccmi_train_step(const ccmi_train_args *a, void *stream)
         CCMI_HIP_CHECK(hipMemcpyAsync(a->raw_out, F(pl.z[g.n_sp]), sizeof(float) * 3 * npx * B, hipMemcpyDeviceToDevice, s));
     if (a->forward_only) {
         // the ARM's rate (rate_out, the rate sums in acc4) comes from the side stream
-        if (side) CCMI_HIP_CHECK(hipStreamWaitEvent(s, side->join, 0));
+        CCMI_HIP_CHECK(join.wait());
         if (a->loss_out) {
             // with a real target (target_stride > 0) the loss row holds the built-in MSE too;
             // otherwise (autograd: the loss lives in torch) MSE reads 0 and loss = lmbda-rate
@@ -2734,7 +2747,7 @@ extern "C" int ccmi_train_step(const ccmi_train_args *a, void *stream)
     // ---- latent gradients, norm, Adam
     // about eight workgroups per CU over the batch, 4+ elements per thread
     const unsigned nls = (unsigned)std::max<int64_t>(1, std::min<int64_t>(ccmi_div_up(GS, 4 * kT), std::max(1, 2048 / B)));
-    if (side) CCMI_HIP_CHECK(hipStreamWaitEvent(s, side->join, 0));
+    CCMI_HIP_CHECK(join.wait());
     hipLaunchKernelGGL(t_latgrad_sumsq, dim3(nls, B), dim3(kT), 0, s, gq, side ? F(pl.gq_arm) : nullptr, dq, g.N, G, GS,
                        GS, acc4);
     const float total = a->yuv420 ? (float)(npx + 2 * (int64_t)(g.H / 2) * (g.W / 2)) : (float)(3 * npx);

@@ -105,6 +105,23 @@ def test_gpu_gradients_match_reference(f, gpu):
         o += n
 
 
+@pytest.mark.parametrize("f", FILES, ids=lambda f: f.stem)
+def test_forward_only_rate_read_right_after_the_call(f, gpu):
+    """forward_only (the autograd forward) returns the ARM's rate, which is computed on the
+    training side stream: values read right after the call, ordered only by the caller's
+    stream, must be the final ones.  Against the diagnostic spin build (make -C cool-chic_amd
+    spin; CCMI_LIB=.../libccmi_spin.so) a missing side-stream join reads stale values here."""
+    from ccmi.autograd import TrainForward
+    z = np.load(f)
+    of, st, target, meta = _setup(z, gpu)
+    cfg = dict(arch=of.arch, quantizer=meta["quantizer_type"], temperature=float(meta["temperature"]),
+               yuv420=bool(meta["yuv420"]))
+    raw, rate = TrainForward.apply(of.latents, of.params, cfg)
+    got = float(rate.double().sum().item())  # stream-ordered read, no device synchronize before it
+    assert abs(got - float(z["rate_bit"])) <= 2e-5 * float(z["rate_bit"]), (got, float(z["rate_bit"]))
+    assert torch.isfinite(raw).all()
+
+
 @pytest.mark.parametrize("f", [f for f in FILES if "g1/latent_grids.0.data" in np.load(f).files],
                          ids=lambda f: f.stem)
 def test_gpu_gradients_at_step1_parameters_match_reference(f, gpu):

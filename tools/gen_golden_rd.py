@@ -93,15 +93,20 @@ def load_targets() -> dict:
     oracle = ROOT / "oracle" / "_build" / "ccdec_oracle"
     if not oracle.exists():
         subprocess.run(["make", "-s", "-C", str(ROOT / "oracle")], check=True)
-    with tempfile.TemporaryDirectory() as td:
-        ppm = Path(td) / "k01.ppm"
-        subprocess.run([str(oracle), str(GOLD / "cool" / "kodim01-lmbda-00001.cool"), str(ppm)], check=True,
-                       stdout=subprocess.DEVNULL)
-        k, bd = cio.read_ppm(ppm)
-    assert bd == 8
-    k = k[0].float()  # [3, 512, 768]
+    def dec(stream: str):
+        with tempfile.TemporaryDirectory() as td:
+            ppm = Path(td) / "k.ppm"
+            subprocess.run([str(oracle), str(GOLD / "cool" / stream), str(ppm)], check=True,
+                           stdout=subprocess.DEVNULL)
+            k, bd = cio.read_ppm(ppm)
+        assert bd == 8
+        return k[0].float()
+
+    k = dec("kodim01-lmbda-00001.cool")  # [3, 512, 768]
     out["kodim01_768x512"] = k.contiguous()                      # Kodak geometry (config 4 content)
     out["kodim01_crop512"] = k[:, :512, :512].contiguous()
+    # the portrait Kodak geometry (config 4's second geometry batch: kodim04/09/10/17/18/19)
+    out["kodim04_512x768"] = dec("kodim04-lmbda-00001.cool").contiguous()  # [3, 768, 512]
     return out
 
 
@@ -377,10 +382,13 @@ if __name__ == "__main__":
     what = sys.argv[1] if len(sys.argv) > 1 else "all"
     if what == "one":
         # one (image, preset scale, lambda, seed) point into its own file, so several can run
-        # side by side: python tools/gen_golden_rd.py one IMAGE SCALE LAMBDA SEED THREADS OUT
+        # side by side: python tools/gen_golden_rd.py one IMAGE SCALE LAMBDA SEED THREADS OUT [ARCH]
+        # (SEED may be a comma list, run in order into the same file)
         img, sc, lm, sd, th, out = sys.argv[2:8]
+        arch = sys.argv[8] if len(sys.argv) > 8 else "hop"
         torch.set_num_threads(int(th))
-        run_rd("c3x", Path(out), images=[img], lambdas=[float(lm)], seeds=[int(sd)], scale=float(sc))
+        run_rd("c3x", Path(out), images=[img], lambdas=[float(x) for x in lm.split(",")],
+               seeds=[int(x) for x in sd.split(",")], scale=float(sc), arch=arch)
         sys.exit(0)
     if what in ("bd", "all"):
         gen_bd(GOLD / "bd_reference.json")
