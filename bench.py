@@ -529,6 +529,42 @@ def encoder_shard(rank: int, lambdas=None):
     return [REF_LAMBDAS[rank % len(REF_LAMBDAS)]], rank // len(REF_LAMBDAS)
 
 
+# Per-kernel rooflines of the encoder's training step, from a committed rocprofv3 kernel trace
+# of tools/prof_train.sh (8 frames of 512 x 768, hop, c3x; one launch per iteration each).
+TRAIN_PROFILE = "profiles/r4y_train_kernel_stats.csv"
+TRAIN_FRAMES, TRAIN_H, TRAIN_W = 8, 512, 768
+
+
+def train_kernel_rooflines(csv_path: str = TRAIN_PROFILE) -> list:
+    """FLOPs per launch / average launch duration for the two largest training kernels.
+    t_head_bwd<7, 3>: per pixel the hidden-layer recompute (48 x 7 MAC), g_h (48 x 3), g_x (7 x 48),
+    dW1 (3 x 48) and dW0 (48 x 7): 1,296 MAC = 2,592 FLOP.  t_arm16<2>: per latent 3 x the ARM
+    forward (dim 16, 2 hidden layers + the 2-wide output: 544 MAC) = 3,264 FLOP (forward +
+    input and weight gradients)."""
+    import csv
+    npx = TRAIN_H * TRAIN_W
+    nlat = sum((TRAIN_H >> k) * (TRAIN_W >> k) for k in range(7))
+    flops = {"t_head_bwd<7, 3": 2592 * npx * TRAIN_FRAMES, "t_arm16<2>": 3264 * nlat * TRAIN_FRAMES}
+    out = []
+    path = ROOT / csv_path
+    if not path.exists():
+        return out
+    rows = list(csv.DictReader(path.open()))
+    for key, fl in flops.items():
+        r = next((r for r in rows if key in r["Name"]), None)
+        if r is None:
+            continue
+        us = float(r["AverageNs"]) / 1e3
+        ach = fl / (us * 1e-6) / 1e12
+        name = r["Name"].replace("void (anonymous namespace)::", "")
+        out.append({"kernel": name[:name.index(">") + 1] if ">" in name else name.split("(")[0],
+                    "flop_per_launch": fl, "avg_us": round(us, 2), "achieved": round(ach, 3),
+                    "peak": PEAK_FP32_TFLOPS, "unit": "TFLOP/s", "frac": round(ach / PEAK_FP32_TFLOPS, 4),
+                    "launch": f"{TRAIN_FRAMES} frames {TRAIN_H}x{TRAIN_W}, one per iteration",
+                    "source": csv_path})
+    return out
+
+
 def bench_encoder(images: int, scale: float, lambdas, rank: int, world: int, dist, dev):
     """Encoder overfit (BASELINE config 4): the c3x schedule (warm-up candidates + 3 phases +
     quantize_model, ccmi.train.overfit) on the first `images` Kodak proxies, RGB, hop decoder.
@@ -885,7 +921,8 @@ def main():
             "roofline": {"bound": "valu-fp32", "kernel": "whole overfit (all training kernels + host loop)",
                          "achieved": round(ach, 3), "peak": PEAK_FP32_TFLOPS, "unit": "TFLOP/s",
                          "frac": round(ach / PEAK_FP32_TFLOPS, 4),
-                         "note": "algorithmic FLOPs = 3 x forward (ARM + upsampling + synthesis) per iteration"},
+                         "note": "algorithmic FLOPs = 3 x forward (ARM + upsampling + synthesis) per iteration",
+                         "kernels": train_kernel_rooflines()},
             "data": "Kodak-24 proxies: the reference's own lambda=1e-4 Kodak .cool streams (35-46 dB) decoded "
                     "bit-exactly (the originals are not in the reference tree); PSNR is measured against the "
                     "proxy, results.tsv against the original"}

@@ -598,23 +598,10 @@ __global__ __launch_bounds__(64) void dec_arm_spec_kernel(const ArmStreamDesc *_
 #endif
 }
 
-// ------------------------------------------------------------------ latency-optimised ARM decode (d <= 16, >= 1 hidden layer)
-// dec_arm_spec_kernel's speculation (DPP row g = latent x + g, undecoded same-row latents
-// guessed 0), with the serial chain of a pass shortened:
-//  * the first hidden layer's above-row part (every context but the D_S = 3 same-row ones,
-//    plus the bias and the residual of the above-row neurons) is computed off the chain,
-//    64 latents at a time with lane = latent once the rows above are decoded, into an LDS
-//    ring of two 64-latent chunks; a pass adds the three same-row products to it.  Exact:
-//    the reference accumulates every product in int32 before its single rounding
-//    (arm_cpu.cpp:65-80), and int32 addition wraps identically in any order (-fwrapv);
-//  * the next pass's above-row sums are read for all four outcomes (x + 1 .. x + 4) before
-//    the CABAC of the current pass, so the chain never waits on LDS for them;
-//  * the CABAC bin uses a count-leading-zeros renormalisation and selects instead of
-//    the branchy lps_renorm ladder (same state transitions as TDecBinCABAC::decodeBin).
+// ------------------------------------------------------------------ chain kernel support
 constexpr int kDS = 3; // same-row contexts (0, -3), (0, -2), (0, -1): the last three context indices
-constexpr int kChunk = 64;
 
-// Byte source of the latency kernel: the stream's words come through wave-uniform VECTOR
+// Byte source of the chain kernel: the stream's words come through wave-uniform VECTOR
 // loads issued one word ahead (the scalar-load reader's fetch is counted in lgkmcnt with
 // the LDS reads, so every LDS wait of a pass also waited for it).  Word indices clamp to the
 // zero padding after the stream (>= 64 bytes, dec_host.cpp), which reads as zeros.
@@ -651,77 +638,142 @@ struct DevBytesV {
     }
 };
 
-// A static context's model state st (0..255) as the bin decode uses it: the MPS in bit 7,
-// the LPS-side state's top bits (st ^ 0xFF when the MPS is 1, then >> 2) in bits 0..4.
-__host__ __device__ constexpr uint32_t bin_code(uint32_t st)
+// ------------------------------------------------------------------ chain kernel (d <= 16, >= 1 hidden layer)
+// The serial decode chain of one latent-layer stream, built around what one wavefront can
+// issue (one instruction per ~4 cycles, SALU and VALU alike): every instruction on the chain
+// is one the decode needs.  Speculation as in round 3 (DPP row g evaluates latent x + g,
+// its undecoded same-row neighbours guessed equal to the latent above) with:
+//  * layer 0 in GUESS-ERROR form: the chunk precompute folds the above-row contexts AND the
+//    guessed same-row contexts (the latents above, up[x - 3 .. x - 1]) into one sum per latent
+//    and neuron, preG; a pass adds C1 e1 + C2 e2 + C3 e3, where e_j = (decoded - guessed value)
+//    of latent x - j (wave-uniform, SGPR) and C_j the per-lane constant weight of that context
+//    for the lane's row (0 when the row guessed it).  Exact: int32 sums wrap identically in any
+//    order (-fwrapv) and the reference rounds once per layer (arm_cpu.cpp:65-80);
+//  * coded RUNS: the block map is turned into runs of coded latents once per run (lanes read
+//    the block flags, one ballot), so a pass's only control flow is its CABAC;
+//  * the next pass's inputs read ahead at constant LDS offsets: the preG ring (two 64-latent
+//    chunks) mirrors its first 8 entries after its end, so latents x + 1 .. x + 7 never wrap;
+//  * decoded values collected in a VGPR (v_writelane) and stored 60 at a time;
+//  * the CABAC state left-aligned (range << 23, value << 16): the renormalisation shift of
+//    both outcomes is one s_flbit of the new range; the five static bin codes of a context
+//    (4 unary bins + sign, 6 bits each) in one LDS word;
+//  * the multiply forms (24-bit / 32-bit) as instantiations of the pass loop, switched at a
+//    pass boundary when a decoded latent leaves the 24-bit range.
+constexpr int kPreRing = 128; // two 64-latent chunks of preG
+constexpr int kPreMir = 8;    // ring entries [0, 8) mirrored at [128, 136)
+constexpr uint32_t kQ24 = 16383; // |q| <= kQ24 keeps contexts and guess errors inside 24 signed bits
+
+// 6-bit code of a static context's model state st: bit 5 the MPS, bits 0..4 the LPS class
+// ((st or its complement) >> 2; TDecBinCABAC::decodeBin's LPS-range index)
+__host__ __device__ constexpr uint32_t code6(uint32_t st)
 {
-    return (st & 0x80u) | ((((st >> 7) ? st ^ 0xFFu : st) & 0xFFu) >> 2);
+    return ((st >> 7) << 5) | ((((st >> 7) ? st ^ 0xFFu : st) & 0xFFu) >> 2);
 }
 
-// one bin of a static context given as bin_code(state) (TDecBinCABAC::decodeBin): the state
-// update as one SALU sequence with a single compare whose SCC drives four selects (the
-// compiled C form rebuilt the decision as a 64-bit lane mask ANDed with exec per select:
-// ~30 instead of 19 instructions on the serial chain).  LPS iff value >= (range - lps) << 7;
-// the renormalisation shift is clz(lps) - 23 after an LPS (Contexts.cpp's table for lps in
-// [4, 236]) and 1 after an MPS that left the range below 256.
-__device__ __forceinline__ uint32_t bin_fast(Cabac<DevBytesV> &c, uint32_t code)
-{
-    uint32_t range = c.range, value = c.value, nb, lp, t0, t1, lps, rm, sc, nl, nm;
-    asm("s_and_b32 %[t0], %[code], 31\n\t"
-        "s_lshr_b32 %[t1], %[range], 5\n\t"
-        "s_mul_i32 %[t0], %[t0], %[t1]\n\t"
-        "s_lshr_b32 %[t0], %[t0], 1\n\t"
-        "s_add_u32 %[lps], %[t0], 4\n\t"
-        "s_sub_u32 %[rm], %[range], %[lps]\n\t"
-        "s_lshl_b32 %[sc], %[rm], 7\n\t"
-        "s_flbit_i32_b32 %[nl], %[lps]\n\t"
-        "s_sub_u32 %[nl], %[nl], 23\n\t"
-        "s_lshr_b32 %[nm], %[rm], 8\n\t"
-        "s_xor_b32 %[nm], %[nm], 1\n\t"
-        "s_cmp_ge_u32 %[value], %[sc]\n\t"
-        "s_cselect_b32 %[range], %[lps], %[rm]\n\t"
-        "s_cselect_b32 %[nb], %[nl], %[nm]\n\t"
-        "s_cselect_b32 %[sc], %[sc], 0\n\t"
-        "s_cselect_b32 %[lp], 1, 0\n\t"
-        "s_sub_u32 %[value], %[value], %[sc]\n\t"
-        "s_lshl_b32 %[value], %[value], %[nb]\n\t"
-        "s_lshl_b32 %[range], %[range], %[nb]"
-        : [range] "+s"(range), [value] "+s"(value), [nb] "=&s"(nb), [lp] "=&s"(lp), [t0] "=&s"(t0), [t1] "=&s"(t1),
-          [lps] "=&s"(lps), [rm] "=&s"(rm), [sc] "=&s"(sc), [nl] "=&s"(nl), [nm] "=&s"(nm)
-        : [code] "s"(code)
-        : "scc");
-    c.range = range;
-    c.value = value;
-    c.bits_needed += (int32_t)nb;
-    if (c.bits_needed >= 0) {
-        c.value += c.src.next() << c.bits_needed;
-        c.bits_needed -= 8;
+struct Cab6 {
+    DevBytesV src;
+    uint32_t R, V; // TDecBinCABAC's m_uiRange << 23 and m_uiValue << 16
+    int32_t bn;    // bits_needed
+    __device__ __forceinline__ void from(const Cabac<DevBytesV> &c)
+    {
+        src = c.src;
+        R = c.range << 23;
+        V = c.value << 16;
+        bn = c.bits_needed;
     }
-    return (code >> 7) ^ lp;
+    __device__ __forceinline__ void to(Cabac<DevBytesV> &c) const
+    {
+        c.src = src;
+        c.range = R >> 23;
+        c.value = V >> 16;
+        c.bits_needed = bn;
+    }
+};
+
+// One bin of a static context, k-th 6-bit code of the word st (TDecBinCABAC::decodeBin):
+// LPS iff value >= (range - lps) << 7; after either outcome the new range is renormalised to
+// [256, 511) by one left shift of clz(range << 23) (1 or 0 after an MPS, clz(lps) - 23 after an
+// LPS, = the reference's renorm table for lps in [4, 236]).
+template <int K>
+__device__ __forceinline__ uint32_t bin6(Cab6 &c, uint32_t st)
+{
+    const uint32_t q5 = (st >> (6 * K)) & 31u, mps = (st >> (6 * K + 5)) & 1u;
+    uint32_t R = c.R, V = c.V, t, lps, rm, nb, lp;
+    asm("s_lshr_b32 %[t], %[R], 28\n\t"
+        "s_mul_i32 %[t], %[t], %[q5]\n\t"
+        "s_lshr_b32 %[t], %[t], 1\n\t"
+        "s_add_u32 %[t], %[t], 4\n\t"
+        "s_lshl_b32 %[lps], %[t], 23\n\t"
+        "s_sub_u32 %[rm], %[R], %[lps]\n\t"
+        "s_cmp_ge_u32 %[V], %[rm]\n\t"
+        "s_cselect_b32 %[R], %[lps], %[rm]\n\t"
+        "s_cselect_b32 %[t], %[rm], 0\n\t"
+        "s_cselect_b32 %[lp], 1, 0\n\t"
+        "s_sub_u32 %[V], %[V], %[t]\n\t"
+        "s_flbit_i32_b32 %[nb], %[R]\n\t"
+        "s_lshl_b32 %[R], %[R], %[nb]\n\t"
+        "s_lshl_b32 %[V], %[V], %[nb]"
+        : [R] "+s"(R), [V] "+s"(V), [t] "=&s"(t), [lps] "=&s"(lps), [rm] "=&s"(rm), [nb] "=&s"(nb), [lp] "=&s"(lp)
+        : [q5] "s"(q5)
+        : "scc");
+    c.R = R;
+    c.V = V;
+    c.bn += (int32_t)nb;
+    if (c.bn >= 0) {
+        c.V += c.src.next() << (c.bn + 16);
+        c.bn -= 8;
+    }
+    return lp ^ mps;
 }
+
+// decode_single (cc-bac.h:192-231) with the static codes of one context
+__device__ __forceinline__ int32_t decode_val(Cab6 &c, uint32_t st)
+{
+    int32_t val = 0;
+    if (bin6<0>(c, st)) {
+        if (!bin6<1>(c, st)) val = 1;
+        else if (!bin6<2>(c, st)) val = 2;
+        else if (!bin6<3>(c, st)) val = 3;
+        else {
+            Cabac<DevBytesV> t;
+            c.to(t);
+            val = t.expgolomb(0) + 4;
+            c.from(t);
+        }
+        if (bin6<4>(c, st)) val = -val;
+    }
+    return val;
+}
+
+// ReLU + rounding of a hidden layer, arm_cpu.cpp:76-81 as written (a sum within 127 of INT_MAX
+// wraps negative there too)
+// v_writelane_b32 (no clang builtin in this toolchain: the LLVM intrinsic by its asm label)
+extern "C" __device__ int32_t ccmi_writelane(int32_t v, int32_t lane, int32_t old) __asm("llvm.amdgcn.writelane.i32");
+
+__device__ __forceinline__ int32_t relu_rnd8(int32_t acc) { return acc < 0 ? 0 : (acc + 128) >> 8; }
 
 template <int D, int NH>
-__global__ __launch_bounds__(64) void dec_arm_lat_kernel(const ArmStreamDesc *__restrict__ streams, int pitch)
+__global__ __launch_bounds__(64) void dec_arm_chain_kernel(const ArmStreamDesc *__restrict__ streams, int pitch)
 {
     static_assert(D <= 16 && D > kDS && NH >= 1, "one neuron per lane of a DPP row, >= 1 hidden layer");
     constexpr int DA = D - kDS; // above-row contexts
 #if defined(CCMI_ARM_STAMPS)
-    // [0] ARM pass (same-row products + MLP + output sums)  [1] index + table  [2] CABAC
-    // [3] ARM passes  [4] coded latents  [5] setup  [6] latent loop  [7] chunk precompute
-    // [8] block fills  [9] row copy-out  [10] blocks visited
-    // counters in a VGPR (lane k = counter k, 32-bit cycles): SGPR accumulators pushed the
-    // kernel's wave-uniform state out to VGPR lanes and distorted what they measured
+    // [0] ARM + index (to the table read)  [1] table wait  [2] CABAC  [3] passes  [4] coded latents
+    // [5] setup  [6] latent loop  [7] chunk precompute  [8] run starts (fills, block scan)
+    // [9] row copy-out  [10] runs  [11] after the CABAC (pass end)
     uint32_t st_v = 0;
 #define LACC(k, d) st_v += (threadIdx.x == (k)) ? (uint32_t)(d) : 0u
-#undef ACC
-#define ACC(k, a, b) LACC(k, (b) - (a))
+#define CSTAMP(var) const uint64_t var = __builtin_amdgcn_s_memtime()
     const uint64_t t_begin = __builtin_amdgcn_s_memtime();
+#else
+#define LACC(k, d)
+#define CSTAMP(var)
 #endif
     extern __shared__ int32_t smem[];
-    uint32_t *ctab = reinterpret_cast<uint32_t *>(smem);               // 17 x 50 x 2
-    int32_t *w0s = smem + 17 * 50 * 2;                                  // [16][16] layer-0 weights, [16] biases
-    int32_t *pre = w0s + 16 * 16 + 16;                                  // [2][kChunk][16] above-row sums
-    int32_t *ring = pre + 2 * kChunk * 16;                              // kRingS x pitch
+    uint32_t *ctab = reinterpret_cast<uint32_t *>(smem);               // 17 x 50 packed bin codes
+    int32_t *w0s = smem + 17 * 50;                                      // [16][16] layer-0 weights, [16] biases
+    int32_t *pre = w0s + 16 * 16 + 16;                                  // [kPreRing + kPreMir][16] preG
+    int32_t *ring = pre + (kPreRing + kPreMir) * 16;                    // kRingS x pitch
     uint8_t *bmap = reinterpret_cast<uint8_t *>(ring + kRingS * pitch); // block sig/flat map
 
     const ArmStreamDesc S = streams[blockIdx.x];
@@ -731,30 +783,35 @@ __global__ __launch_bounds__(64) void dec_arm_lat_kernel(const ArmStreamDesc *__
     const int h = S.h, w = S.w;
     const bool w24 = (S.flags & 1) != 0;
 
-    // context table with every static-context index turned into its bin code (model state:
-    // Model::init + state(), then bin_code) once here instead of per bin
-    for (int i = lane; i < 17 * 50 * 2; i += 64) {
-        const uint32_t v = c_ctx.v[i];
-        uint32_t st = 0;
+    for (int i = lane; i < 17 * 50; i += 64) {
+        const uint32_t v = c_ctx.v[2 * i], vs = c_ctx.v[2 * i + 1];
+        uint32_t e = 0;
         for (int k = 0; k < 4; ++k) {
             Model m;
             m.init((int)((v >> (8 * k)) & 0xFF));
-            st |= bin_code(m.state()) << (8 * k);
+            e |= code6(m.state()) << (6 * k);
         }
-        ctab[i] = (i & 1) ? (st & 0xFF) : st;
+        Model m;
+        m.init((int)(vs & 0xFF));
+        ctab[i] = e | (code6(m.state()) << 24);
     }
     for (int i = lane; i < kRingS * pitch; i += 64) ring[i] = 0;
-    // layer 0 in LDS for the chunk precompute (broadcast reads: as scalar operands its 16 x 13
-    // above-row weights pushed the kernel's other wave-uniform state out to VGPR lanes)
     for (int i = lane; i < 16 * 16 + 16; i += 64) {
         const int r = i >> 4, cc = i & 15;
         w0s[i] = i < 256 ? (r < D && cc < D ? S.weights[r * D + cc] : 0) : (cc < D ? S.weights[D * D + cc] : 0);
     }
-
-    // layer 0: same-row weights of neuron o (its own residual folded into the matching one)
-    int32_t Ws[kDS];
+    // guess-error coefficients: latent x - j is a decoded (not guessed) neighbour of row g's
+    // latent x + g iff g + j <= 3, at context dx = -(g + j), index DA + 3 - (g + j); the weight
+    // carries the neuron's own residual when that index is its own
+    int32_t C1, C2, C3;
+    {
+        int32_t Ws[kDS];
 #pragma unroll
-    for (int j = 0; j < kDS; ++j) Ws[j] = live ? S.weights[o * D + DA + j] + (o == DA + j ? 256 : 0) : 0;
+        for (int j = 0; j < kDS; ++j) Ws[j] = live ? S.weights[o * D + DA + j] + (o == DA + j ? 256 : 0) : 0;
+        C1 = grp == 0 ? Ws[2] : grp == 1 ? Ws[1] : grp == 2 ? Ws[0] : 0;
+        C2 = grp == 0 ? Ws[1] : grp == 1 ? Ws[0] : 0;
+        C3 = grp == 0 ? Ws[0] : 0;
+    }
     int32_t Wh[NH][16], Bh[NH];
 #pragma unroll
     for (int l = 1; l < NH; ++l) {
@@ -765,13 +822,13 @@ __global__ __launch_bounds__(64) void dec_arm_lat_kernel(const ArmStreamDesc *__
     }
     const int32_t *ob = S.weights + NH * (D * D + D);
     const int32_t Wo0 = live ? ob[o] : 0, Wo1 = live ? ob[D + o] : 0;
-    const int32_t bo0 = __builtin_amdgcn_readfirstlane(ob[2 * D]);
-    const int32_t bo1 = __builtin_amdgcn_readfirstlane(ob[2 * D + 1]);
+    // the output biases ride in neuron 0's product (the row sums add them once)
+    const int32_t Bo0 = o == 0 ? ob[2 * D] : 0, Bo1 = o == 0 ? ob[2 * D + 1] : 0;
 
     // ---- CABAC start + block significance / flat maps (BACContext::set_layer, cc-bac.h:24-130)
-    Cabac<DevBytesV> cab;
-    cab.src.init(S.bytes, S.nbytes);
-    cab.start();
+    Cabac<DevBytesV> cab0;
+    cab0.src.init(S.bytes, S.nbytes);
+    cab0.start();
     const int updated = S.sig_blk < 0;
     const int blk = S.sig_blk < 0 ? -S.sig_blk : S.sig_blk;
     int shift = 0;
@@ -786,62 +843,87 @@ __global__ __launch_bounds__(64) void dec_arm_lat_kernel(const ArmStreamDesc *__
     for (int i = lane; i < nblk; i += 64) bmap[i] = 1; // bit0 sig, bit1 flat
     __syncthreads();
     if (nblk > 1) {
-        if (cab.ep()) {
+        if (cab0.ep()) {
             Model m;
             m.init(65);
             for (int i = 0; i < nblk; ++i) {
-                const uint32_t b = updated ? cab.bin_adaptive(m) : cab.ep();
+                const uint32_t b = updated ? cab0.bin_adaptive(m) : cab0.ep();
                 if (lane == 0) bmap[i] = (uint8_t)b;
             }
         }
         __syncthreads();
-        if (cab.ep()) {
+        if (cab0.ep()) {
             Model m;
             m.init(65);
             for (int i = 0; i < nblk; ++i) {
                 const int sig = __builtin_amdgcn_readfirstlane((int)bmap[i]);
                 if (sig) {
-                    const uint32_t f = updated ? cab.bin_adaptive(m) : cab.ep();
+                    const uint32_t f = updated ? cab0.bin_adaptive(m) : cab0.ep();
                     if (lane == 0) bmap[i] = (uint8_t)(sig | (f << 1));
                 }
             }
         }
     }
     __syncthreads();
+    Cab6 cab;
+    cab.from(cab0);
 
-    // context offsets of the above-row contexts (rows y-3 .. y-1), for the chunk precompute
-    // sticky 24-bit guard: the largest (q + 32767) as unsigned, >= 65535 once a decoded latent
-    // has |q| >= 32768 (an s_max per latent; the bool form went through a VGPR and back)
+    // 24-bit guard: max over the decoded q of (q + kQ24) as unsigned, < 2 kQ24 + 1 while every
+    // |q| <= kQ24 (contexts < 2^22, guess errors < 2^23)
     uint32_t qspan = 0;
+    // 0: 24-bit layer 0 + 24-bit hidden / output layers; 1: 32-bit layer 0; 2: all 32-bit
+    int mode = w24 ? 0 : 2;
+    auto lds_order = []() __attribute__((always_inline)) { // this wave's LDS stores before its later loads (other lanes read them)
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    };
 #if defined(CCMI_ARM_STAMPS)
     LACC(5, __builtin_amdgcn_s_memtime() - t_begin);
     const uint64_t t_loop = __builtin_amdgcn_s_memtime();
 #endif
 
     for (int y = 0; y < h; ++y) {
-        int32_t *row = ring + (y % kRingS) * pitch + kPad;
-        const int32_t *up = ring + ((y + kRingS - 1) % kRingS) * pitch + kPad;
-        int32_t r1 = 0, r2 = 0, r3 = 0, r4 = 0; // decoded values at x-1 .. x-4 (this row)
+        int32_t *row = ring + (y & 3) * pitch + kPad;
+        const int32_t *up = ring + ((y + 3) & 3) * pitch + kPad;
         const int brow = blk > 0 ? (y >> shift) * nbx : 0;
-        int have0 = -1, have1 = -1; // chunk held by pre slot 0 / 1
-        // above-row sums of chunk c (latents 64 c .. 64 c + 63), lane = latent; contexts of
-        // rows y-3 .. y-1 from the ring (their zero rows above the image, zero pad columns)
-        auto chunk = [&](int c) {
-#if defined(CCMI_ARM_STAMPS)
-            const uint64_t tc0 = __builtin_amdgcn_s_memtime();
-#endif
-            const int x = c * kChunk + lane;
-            const bool in = x < w; // lanes past the row end compute zeros nobody reads
-            int32_t ctx[DA];
+        int pre_next = 0;        // next 64-latent chunk of preG to compute for this row
+        int pre_lim = 0;         // a pass at x needs x + 8 <= pre_lim (INT_MAX once the row is covered)
+        int32_t vrow = 0;        // lane i < x - xb: decoded value of latent xb + i, not stored yet
+        int xb = 0;
+        int32_t e1 = 0, e2 = 0, e3 = 0; // guess errors of latents x - 1, x - 2, x - 3
+        int32_t pfa = 0;         // preG of this lane's latent x + grp, neuron o
+        int32_t upv = 0;         // lane i < 8: up[x - ub + i]
+        int ub = 0;
+        int x = 0;
+
+        auto flush = [&]() __attribute__((always_inline)) {
+            if (lane < x - xb) row[xb + lane] = vrow;
+            xb = x;
+        };
+        // preG of chunk c (latents 64 c .. 64 c + 63, lane = latent)
+        auto chunk = [&](int c) __attribute__((always_inline)) {
+            CSTAMP(tc0);
+            const int xx = c * 64 + lane;
+            const bool in = xx < w; // lanes past the row end compute sums nobody reads
+            int32_t ctx[D];
 #pragma unroll
             for (int i = 0; i < DA; ++i) {
                 int dy, dx;
                 ctx_dydx<D>(i, dy, dx);
-                ctx[i] = in ? ring[((y + dy + kRingS) % kRingS) * pitch + kPad + x + dx] : 0;
+                ctx[i] = in ? ring[((y + dy) & 3) * pitch + kPad + xx + dx] : 0;
             }
-            int32_t *dst = pre + ((c & 1) * kChunk + lane) * 16;
-            // the 24-bit form chosen once per chunk (a per-product select doubled the work)
-            auto sums = [&](auto F24) {
+#pragma unroll
+            for (int j = 0; j < kDS; ++j) ctx[DA + j] = in ? up[xx - kDS + j] : 0; // the guesses
+            // the weights re-read per chunk: loop-invariant LDS loads hoisted out of the row loop
+            // held all 272 of them in VGPRs (occupancy 1); an opaque offset keeps them here
+            int woff = 0;
+            asm volatile("" : "+s"(woff));
+            const int32_t *wl = w0s + woff;
+            const int ri = xx & (kPreRing - 1);
+            int32_t *dst = pre + ri * 16;
+            int32_t *mir = pre + (kPreRing + ri) * 16;
+            auto sums = [&](auto F24) __attribute__((always_inline)) {
                 constexpr bool f24 = decltype(F24)::value;
 #pragma unroll
                 for (int n = 0; n < 16; n += 4) {
@@ -853,218 +935,187 @@ __global__ __launch_bounds__(64) void dec_arm_lat_kernel(const ArmStreamDesc *__
                             acc[q] = 0;
                             continue;
                         }
-                        int32_t a = w0s[256 + nn] + (nn < DA ? ctx[nn < DA ? nn : 0] * 256 : 0); // bias + own residual
-                        const int4 *wr = reinterpret_cast<const int4 *>(w0s + 16 * nn);
+                        int32_t a = wl[256 + nn] + ctx[nn] * 256; // bias + own residual
+                        const int4 *wr = reinterpret_cast<const int4 *>(wl + 16 * nn);
 #pragma unroll
-                        for (int i4 = 0; i4 < (DA + 3) / 4; ++i4) {
+                        for (int i4 = 0; i4 < (D + 3) / 4; ++i4) {
                             const int4 wv = wr[i4];
                             const int32_t wk[4] = {wv.x, wv.y, wv.z, wv.w};
 #pragma unroll
                             for (int k = 0; k < 4; ++k)
-                                if (4 * i4 + k < DA) a += imul<f24>(wk[k], ctx[4 * i4 + k]);
+                                if (4 * i4 + k < D) a += imul<f24>(wk[k], ctx[4 * i4 + k]);
                         }
                         acc[q] = a;
                     }
-                    *reinterpret_cast<int4 *>(dst + n) = int4{acc[0], acc[1], acc[2], acc[3]};
+                    const int4 v4{acc[0], acc[1], acc[2], acc[3]};
+                    *reinterpret_cast<int4 *>(dst + n) = v4;
+                    if (ri < kPreMir) *reinterpret_cast<int4 *>(mir + n) = v4;
                 }
             };
-            if (w24 && qspan < 65535u) sums(std::true_type{});
+            if (mode == 0) sums(std::true_type{});
             else sums(std::false_type{});
-            if (c & 1) have1 = c;
-            else have0 = c;
-            // other lanes read these sums next: order this wave's LDS stores before its loads
-            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-            __builtin_amdgcn_wave_barrier();
-            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 #if defined(CCMI_ARM_STAMPS)
             __builtin_amdgcn_s_waitcnt(0);
             LACC(7, __builtin_amdgcn_s_memtime() - tc0);
 #endif
         };
-        auto push = [&](int32_t v, int x) {
-            r4 = r3;
-            r3 = r2;
-            r2 = r1;
-            r1 = v;
-            if (lane == 0) row[x] = v;
+        // preG for latents up to x + 7 (the chunks of [x, x + 8) not computed yet)
+        auto ensure = [&]() __attribute__((always_inline)) {
+            const int hi = (min(x + 8, w) - 1) >> 6;
+            for (int c = max(pre_next, x >> 6); c <= hi; ++c) chunk(c);
+            pre_next = max(pre_next, hi + 1);
+            pre_lim = pre_next * 64 >= w ? 0x7FFFFFFF : pre_next * 64;
+            lds_order();
         };
-        auto fill = [&](int x, int n, int kind /*0 zero, 1 = r1, 2 = up*/) {
-            const int32_t c1 = r1;
-            for (int i = lane; i < n; i += 64) row[x + i] = kind == 0 ? 0 : kind == 1 ? c1 : up[x + i];
-            if (kind == 2) {
-                __builtin_amdgcn_s_waitcnt(0);
-                __builtin_amdgcn_wave_barrier();
-                auto at = [&](int j) { return __builtin_amdgcn_readfirstlane(row[j]); };
-                r4 = n >= 4 ? at(x + n - 4) : n == 3 ? r1 : n == 2 ? r2 : r3;
-                r3 = n >= 3 ? at(x + n - 3) : n == 2 ? r1 : r2;
-                r2 = n >= 2 ? at(x + n - 2) : r1;
-                r1 = at(x + n - 1);
-            } else {
-                const int32_t v = kind == 0 ? 0 : c1;
-                r4 = n >= 4 ? v : n == 3 ? r1 : n == 2 ? r2 : r3;
-                r3 = n >= 3 ? v : n == 2 ? r1 : r2;
-                r2 = n >= 2 ? v : r1;
-                r1 = v;
+
+        // one mode's pass loop over the current run [x, cend): returns at the run end, when the
+        // next pass needs preG not computed yet or a flush of vrow, or when the 24-bit guard
+        // trips (mode 0 only); one compare per pass against the bound of all three
+        auto passes = [&](int cend, auto F1, auto FW) __attribute__((always_inline)) {
+            constexpr bool f1 = decltype(F1)::value, fw = decltype(FW)::value;
+            const int stop = min(min(cend, pre_lim - 7), xb + 61);
+            while (x < stop) {
+                CSTAMP(t0);
+                // ---- ARM of latents x .. x + 3 (row g = latent x + g)
+                int32_t a = relu_rnd8(pfa + imul<f1>(C1, e1) + imul<f1>(C2, e2) + imul<f1>(C3, e3));
+#pragma unroll
+                for (int l = 1; l < NH; ++l)
+                    a = relu_rnd8(Bh[l] + a * 256 + row_dot<fw>(Wh[l], a, std::make_integer_sequence<int, D>{}));
+                const int32_t m0 = row_sum16(imul<fw>(Wo0, a) + Bo0), m1 = row_sum16(imul<fw>(Wo1, a) + Bo1);
+                // ---- mu / scale -> context-table entry (lane 16 g + 15 holds row g's sums).  The
+                // reference's symmetric rounding m < 0 ? -((-m + 128) >> 8) : (m + 128) >> 8 equals
+                // (m + 128 + (m >> 31)) >> 8 (|m| < 2^31 - 128), get_val_mu_indicies cc-contexts.h:20-48
+                auto rnd8 = [](int32_t m) __attribute__((always_inline)) { return (m + 128 + (m >> 31)) >> 8; };
+                const int32_t mu = rnd8(m0), ls = rnd8(m1);
+                const int32_t mr = (mu + 128 + (mu >> 31)) & ~255; // rnd8(mu) << 8
+                const int32_t mi = rnd8((mu - mr) * 16) + 8;       // [0, 16]
+                const int32_t si = min(max((ls * 5 + 1408) >> 8, 0), 49);
+                const uint32_t ent = ctab[__mul24(mi, 50) + si];
+                const int32_t mq = mr >> 8;
+                // ---- the next pass's inputs, read ahead (it starts at x + nd, nd = 1 .. 4)
+                const int32_t *pp = pre + ((x & (kPreRing - 1)) + grp) * 16 + o;
+                const int32_t nx0 = pp[16], nx1 = pp[32], nx2 = pp[48], nx3 = pp[64];
+                const int32_t upn = up[x + (lane & 7)];
+                CSTAMP(t1);
+#if defined(CCMI_ARM_STAMPS)
+                __builtin_amdgcn_s_waitcnt(0xc07f); // lgkmcnt(0): the table entry
+#endif
+                CSTAMP(t2);
+                // ---- CABAC, in order, until a latent differs from its guess or the run ends
+                const int lim = min(cend - x, 4);
+                int nd = 0;
+#pragma unroll
+                for (int j = 0; j < 4; ++j) {
+                    const uint32_t st = (uint32_t)__builtin_amdgcn_readlane((int)ent, 16 * j + 15);
+                    const int32_t q = __builtin_amdgcn_readlane(mq, 16 * j + 15) + decode_val(cab, st);
+                    const int32_t g = __builtin_amdgcn_readlane(upv, ub + j);
+                    if (f1) qspan = max(qspan, (uint32_t)(q + (int32_t)kQ24));
+                    const int32_t v = (int32_t)((uint32_t)q << kArmPrec);
+                    vrow = ccmi_writelane(v, x - xb + j, vrow);
+                    e3 = e2;
+                    e2 = e1;
+                    e1 = v - g;
+                    pfa = j == 0 ? nx0 : j == 1 ? nx1 : j == 2 ? nx2 : nx3;
+                    nd = j + 1;
+                    if (e1 != 0 || j + 1 >= lim) break;
+                }
+                CSTAMP(t3);
+                x += nd;
+                ub = nd;
+                upv = upn;
+                CSTAMP(t4);
+                LACC(0, t1 - t0);
+                LACC(1, t2 - t1);
+                LACC(2, t3 - t2);
+                LACC(3, 1);
+                LACC(4, nd);
+                LACC(11, t4 - t3);
+                if (f1 && qspan > 2 * kQ24) return;
             }
         };
-        int bm = 1, bend = 0;
-        // above-row sums of this lane's latent (x + grp) for the next pass, read ahead
-        int pf_x = -1;
-        int32_t pf_a = 0;
-        int up_base = 0;   // up_v lane i < 8: the latent above position up_base + i (read ahead)
-        int32_t up_v = 0;
-        for (int x = 0; x < w;) {
-            int L;
+
+        while (x < w) {
+            CSTAMP(tr0);
+            // ---- the run of coded latents starting at x (uncoded blocks before it filled)
+            int cend = w;
             if (blk > 0) {
-                if (x >= bend) {
-                    bm = __builtin_amdgcn_readfirstlane((int)bmap[brow + (x >> shift)]);
-                    bend = min((x | mask) + 1, w);
-                }
-                if (!(bm & 1) || ((bm & 2) && ((y & mask) || (x & mask)))) {
-                    STAMP(tf0);
-                    fill(x, bend - x, !(bm & 1) ? 0 : (y & mask) ? 2 : 1);
+                const int bx = x >> shift;
+                const int bm = __builtin_amdgcn_readfirstlane((int)bmap[brow + bx]);
+                const int bend = min((x | mask) + 1, w);
+                const bool flat = (bm & 2) != 0;
+                if (!(bm & 1) || (flat && ((y & mask) || (x & mask)))) {
+                    // zero block, flat block below its first row (copy of the row above), or the
+                    // rest of a flat block's first row (copy of its decoded corner)
+                    flush();
+                    lds_order();
+                    const int kind = !(bm & 1) ? 0 : (y & mask) ? 2 : 1;
+                    const int32_t c1 = kind == 1 ? __builtin_amdgcn_readfirstlane(row[x - 1]) : 0;
+                    for (int i = lane; i < bend - x; i += 64) row[x + i] = kind == 0 ? 0 : kind == 1 ? c1 : up[x + i];
                     x = bend;
-                    STAMP(tf1);
-                    ACC(8, tf0, tf1);
-#if defined(CCMI_ARM_STAMPS)
-                    LACC(10, 1);
-#endif
+                    xb = x;
+                    LACC(8, __builtin_amdgcn_s_memtime() - tr0);
                     continue;
                 }
-                if (bm & 2) {
-                    L = 1; // the coded corner of a flat block
+                if (flat) {
+                    cend = x + 1; // the coded corner of a flat block
                 } else {
-                    L = min(kSpec, bend - x);
+                    // consecutive coded, non-flat blocks: the first other block ends the run
+                    int b = bx + 1;
+                    cend = bend;
+                    while (b < nbx) {
+                        const int bb = b + lane;
+                        const int f = bb < nbx ? (int)bmap[brow + bb] : 0;
+                        const uint64_t stop = __ballot(bb < nbx && f != 1);
+                        if (stop) {
+                            b += __builtin_ctzll(stop);
+                            break;
+                        }
+                        b += 64;
+                    }
+                    cend = min(b << shift, w);
                 }
-            } else {
-                L = min(kSpec, w - x);
             }
-            STAMP(tp);
-            // the chunks this pass and the next pass's read-ahead use (latents x .. x + 7), from
-            // one call site: the chunk body is large, and a copy per use overflowed the
-            // instruction cache
+            // run start: guess errors of latents x - 1 .. x - 3 from the stored row (fills)
+            flush();
+            lds_order();
             {
-                const int c_hi = min(x + 2 * kSpec - 1, w - 1) >> 6;
-                for (int c = x >> 6; c <= c_hi; ++c)
-                    if ((c & 1 ? have1 : have0) != c) chunk(c);
+                const int32_t d = lane < kDS ? row[x - 1 - lane] - up[x - 1 - lane] : 0;
+                e1 = __builtin_amdgcn_readlane(d, 0);
+                e2 = __builtin_amdgcn_readlane(d, 1);
+                e3 = __builtin_amdgcn_readlane(d, 2);
             }
-            if (x != pf_x) { // the read-ahead missed (a block boundary or a fill moved x)
-                const int xg = x + grp;
-                pf_a = pre[(((xg >> 6) & 1) * kChunk + (xg & 63)) * 16 + o];
-                up_base = x;
-                up_v = up[x + (lane & 7)];
-            }
-            // the guesses for the undecoded latents x .. x + 2 of the speculative rows: the
-            // latents directly above (hit 75-79 % on the coded blocks of the high-rate class-E
-            // streams, against 24-37 % for a zero guess, tools/latent_stats.py)
-            const int ub = x - up_base;
-            const int32_t g0 = __builtin_amdgcn_readlane(up_v, ub), g1 = __builtin_amdgcn_readlane(up_v, ub + 1),
-                          g2 = __builtin_amdgcn_readlane(up_v, ub + 2);
-            STAMP(t0);
-            // layer 0: above-row sums + the same-row products; lane (g, o) = latent x + g, whose
-            // neighbours at or right of x are the speculative zeros
-            const int32_t s1 = grp == 0 ? r1 : grp == 1 ? g0 : grp == 2 ? g1 : g2;
-            const int32_t s2 = grp == 0 ? r2 : grp == 1 ? r1 : grp == 2 ? g0 : g1;
-            const int32_t s3 = grp == 0 ? r3 : grp == 1 ? r2 : grp == 2 ? r1 : g0;
-            // the multiplies' form fixed per instantiation: with a runtime select per product
-            // the compiler folded both forms into the quarter-rate v_mul_lo_u32
-            auto mlp = [&](auto F1, auto W24) {
-                constexpr bool f1 = decltype(F1)::value, f24 = decltype(W24)::value;
-                const int32_t acc = pf_a + imul<f1>(Ws[0], s3) + imul<f1>(Ws[1], s2) + imul<f1>(Ws[2], s1);
-                int32_t a = acc < 0 ? 0 : (acc + 128) >> 8;
-#pragma unroll
-                for (int l = 1; l < NH; ++l) a = arm_hidden_rows<D, f24>(Wh[l], Bh[l], a);
-                return int2{row_sum16(imul<f24>(Wo0, a)) + bo0, row_sum16(imul<f24>(Wo1, a)) + bo1};
-            };
-            int2 ms;
-            if (w24 && qspan < 65535u) ms = mlp(std::true_type{}, std::true_type{});
-            else if (w24) ms = mlp(std::false_type{}, std::true_type{});
-            else ms = mlp(std::false_type{}, std::false_type{});
-#if defined(CCMI_ARM_STAMPS)
-            __builtin_amdgcn_s_waitcnt(0);
-#endif
-            STAMP(t1);
-            // mu / scale -> context-table entry (lane 16 g + 15 holds row g's sums).  The
-            // reference's symmetric rounding m < 0 ? -((-m + 128) >> 8) : (m + 128) >> 8 equals
-            // (m + 127 + [m >= 0]) >> 8 (arithmetic shift; |m| < 2^31 - 128): branch-free, where the
-            // ternary form compiled to exec-mask branches
-            auto rnd8 = [](int32_t m) { return (m + 128 + (m >> 31)) >> 8; };
-            const int32_t mu = rnd8(ms.x);
-            const int32_t ls = rnd8(ms.y);
-            // get_val_mu_indicies (cc-contexts.h:20-48)
-            const int32_t mr = rnd8(mu) << 8;
-            const int32_t mi = rnd8((mu - mr) * 16) + 8; // in [0, 16]
-            // (lsp * 5 + 128) >> 8 is <= 0 for every lsp < 0, so one clamp covers both bounds
-            const int32_t lsp = ls + 256;
-            const int32_t si = min(max((lsp * 4 + lsp + 128) >> 8, 0), 49);
-            const uint2 e = *reinterpret_cast<const uint2 *>(ctab + (uint32_t)(__mul24(mi, 50) + si) * 2u);
-            // the next pass starts at x + nd, nd = 1 .. kSpec: its above-row sums for every nd
-            int32_t nxt[kSpec];
-#pragma unroll
-            for (int k = 1; k <= kSpec; ++k) {
-                const int xg = x + k + grp;
-                nxt[k - 1] = pre[(((xg >> 6) & 1) * kChunk + (xg & 63)) * 16 + o];
-            }
-            const int32_t up_nxt = up[x + (lane & 7)]; // lane i: above x + i; the next pass reads lanes nd .. nd + 2
-            const uint32_t pk = (uint32_t)mr | e.y; // mu rounded (a multiple of 256), sign-bin state
-            STAMP(t2);
-            // decode_single (cc-bac.h:192-231), in order, until the first non-zero latent
-            // unrolled: constant lanes for the readlanes and a constant guess per latent
-            int nd = 0;
-#pragma unroll
-            for (int j = 0; j < kSpec; ++j) {
-                if (j >= L) break;
-                const int src_lane = 16 * j + 15;
-                const uint32_t st = __builtin_amdgcn_readlane(e.x, src_lane);
-                const uint32_t pkj = __builtin_amdgcn_readlane(pk, src_lane);
-                int32_t val = 0;
-                if (bin_fast(cab, st & 0xFF)) {
-                    if (!bin_fast(cab, (st >> 8) & 0xFF)) val = 1;
-                    else if (!bin_fast(cab, (st >> 16) & 0xFF)) val = 2;
-                    else if (!bin_fast(cab, st >> 24)) val = 3;
-                    else val = cab.expgolomb(0) + 4;
-                    if (bin_fast(cab, pkj & 0xFF)) val = -val;
+            if (x + 8 > pre_lim) ensure();
+            pfa = pre[((x & (kPreRing - 1)) + grp) * 16 + o];
+            upv = up[x + (lane & 7)];
+            ub = 0;
+            LACC(8, __builtin_amdgcn_s_memtime() - tr0);
+            LACC(10, 1);
+            while (x < cend) {
+                if (x + 8 > pre_lim) ensure();
+                if (x - xb > 60) flush();
+                if (mode == 0) {
+                    passes(cend, std::true_type{}, std::true_type{});
+                    if (qspan > 2 * kQ24) mode = 1;
+                } else if (mode == 1) {
+                    passes(cend, std::false_type{}, std::true_type{});
+                } else {
+                    passes(cend, std::false_type{}, std::false_type{});
                 }
-                const int32_t q = ((int32_t)pkj >> 8) + val;
-                qspan = max(qspan, (uint32_t)(q + 32767));
-                const int32_t v = (int32_t)((uint32_t)q << kArmPrec);
-                push(v, x + j);
-                ++nd;
-                // the next row assumed this latent equal to its guess
-                if (v != (j == 0 ? g0 : j == 1 ? g1 : g2)) break;
             }
-            STAMP(t3);
-            ACC(12, tp, t0);
-            ACC(0, t0, t1);
-            ACC(1, t1, t2);
-            ACC(2, t2, t3);
-#if defined(CCMI_ARM_STAMPS)
-            LACC(3, 1);
-            LACC(4, nd);
-#endif
-            x += nd;
-            pf_x = x;
-            pf_a = nd == 1 ? nxt[0] : nd == 2 ? nxt[1] : nd == 3 ? nxt[2] : nxt[3];
-            up_base = x - nd;
-            up_v = up_nxt;
-            STAMP(t4);
-            ACC(11, t3, t4);
         }
-        STAMP(tr0);
-        __syncthreads();
+        CSTAMP(tw0);
+        flush();
+        lds_order();
         int32_t *dst = S.out + (int64_t)y * w;
-        for (int x = lane; x < w; x += 64) dst[x] = row[x];
-        __syncthreads();
-        STAMP(tr1);
-        ACC(9, tr0, tr1);
+        for (int i = lane; i < w; i += 64) dst[i] = row[i];
+        LACC(9, __builtin_amdgcn_s_memtime() - tw0);
     }
 #if defined(CCMI_ARM_STAMPS)
     LACC(6, __builtin_amdgcn_s_memtime() - t_loop);
     if (lane < 16 && S.dbg) S.dbg[lane] = st_v;
-#undef LACC
-#undef ACC
-#define ACC(k, a, b) st_acc[k] += (b) - (a)
 #endif
+#undef LACC
+#undef CSTAMP
 }
 
 // ------------------------------------------------------------------ upsampling (integer)
@@ -1485,12 +1536,13 @@ int launch_dec_arm(const ArmStreamDesc *d_streams, int n_streams, int max_w, int
 #else
     constexpr bool spec_off = false;
 #endif
-    // the latency-optimised kernel: + two 64-latent chunks of above-row sums in LDS
-    const size_t lds_lat = lds_spec + sizeof(int32_t) * (2 * kChunk * 16 + 16 * 16 + 16);
+    // the chain kernel: packed context table, layer-0 weights, the preG ring (+ mirror), ring
+    const size_t lds_lat = sizeof(int32_t) * (17 * 50 + 16 * 16 + 16 + (kPreRing + kPreMir) * 16 + kRingS * pitch) +
+                           ((size_t)max_blocks + 16);
     if (!spec_off && d <= 16 && d > kDS && nh >= 1 && lds_lat <= 160 * 1024) {
 #define CCMI_ARM_LAT(DD, NN)                                                                                    \
         if (d == DD && nh == NN) {                                                                              \
-            hipLaunchKernelGGL((dec_arm_lat_kernel<DD, NN>), dim3(n_streams), dim3(64), lds_lat, s, d_streams, pitch); \
+            hipLaunchKernelGGL((dec_arm_chain_kernel<DD, NN>), dim3(n_streams), dim3(64), lds_lat, s, d_streams, pitch); \
             CCMI_HIP_CHECK(hipGetLastError());                                                                  \
             return CCMI_OK;                                                                                     \
         }

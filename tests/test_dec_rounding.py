@@ -1,5 +1,5 @@
 """Integer identities the path-B latency kernel relies on (dec_kernels.hip,
-dec_arm_lat_kernel), checked on the CPU in int32 arithmetic with wraparound:
+dec_arm_chain_kernel), checked on the CPU in int32 arithmetic with wraparound:
 
 * the reference's symmetric rounding of a /256 (arm_cpu.cpp:94-97, cc-contexts.h:25-29),
   m < 0 ? -((-m + 128) >> 8) : (m + 128) >> 8, equals the branch-free (m + 128 + (m >> 31)) >> 8

@@ -30,6 +30,11 @@ BUDGET = {
     "ups_level_fixed<8, 7>": (64, 0, 0),                    # upsampling pyramid
     "dec_arm_kernel<16, 2>": (128, 0, 0),                   # path B ARM + CABAC
     "dec_arm_spec_kernel<16, 2>": (128, 0, 0),
+    # path B chain kernel: one wave per stream, 4-5 streams per CU in a batch (LDS-bound); the
+    # chunk precompute's 272 layer-0 weights are re-read per chunk (hoisted, they took the
+    # kernel to 256 + 146 VGPRs at occupancy 1)
+    "dec_arm_chain_kernel<16, 2>": (128, 0, 0),
+    "dec_arm_chain_kernel<8, 2>": (128, 0, 0),
     "dec_ups_level_batch": (64, 0, 0),
     # training step (3 waves / SIMD).  t_arm16<2>: round 3 spilled 13 VGPRs across its tile
     # loop (their reloads' vmcnt(0) waited for the previous tile's gradient atomics); since
