@@ -659,8 +659,8 @@ struct DevBytesV {
 //    (4 unary bins + sign, 6 bits each) in one LDS word;
 //  * the multiply forms (24-bit / 32-bit) as instantiations of the pass loop, switched at a
 //    pass boundary when a decoded latent leaves the 24-bit range.
-constexpr int kPreRing = 128; // two 64-latent chunks of preG
-constexpr int kPreMir = 8;    // ring entries [0, 8) mirrored at [128, 136)
+constexpr int kPreRing = 256; // four 64-latent chunks of preG (ring slot = chunk sequence number & 3)
+constexpr int kPreMir = 8;    // ring entries [0, 8) mirrored at [256, 264)
 constexpr uint32_t kQ24 = 16383; // |q| <= kQ24 keeps contexts and guess errors inside 24 signed bits
 
 // 6-bit code of a static context's model state st: bit 5 the MPS, bits 0..4 the LPS class
@@ -719,7 +719,7 @@ __device__ __forceinline__ uint32_t bin6(Cab6 &c, uint32_t st)
     c.R = R;
     c.V = V;
     c.bn += (int32_t)nb;
-    if (c.bn >= 0) {
+    if (__builtin_expect(c.bn >= 0, 0)) { // the byte refill off the fall-through path
         c.V += c.src.next() << (c.bn + 16);
         c.bn -= 8;
     }
@@ -753,16 +753,18 @@ extern "C" __device__ int32_t ccmi_writelane(int32_t v, int32_t lane, int32_t ol
 __device__ __forceinline__ int32_t relu_rnd8(int32_t acc) { return acc < 0 ? 0 : (acc + 128) >> 8; }
 
 template <int D, int NH>
-__global__ __launch_bounds__(64) void dec_arm_chain_kernel(const ArmStreamDesc *__restrict__ streams, int pitch)
+__global__ __launch_bounds__(128) void dec_arm_chain_kernel(const ArmStreamDesc *__restrict__ streams, int pitch)
 {
     static_assert(D <= 16 && D > kDS && NH >= 1, "one neuron per lane of a DPP row, >= 1 hidden layer");
     constexpr int DA = D - kDS; // above-row contexts
 #if defined(CCMI_ARM_STAMPS)
-    // [0] ARM + index (to the table read)  [1] table wait  [2] CABAC  [3] passes  [4] coded latents
-    // [5] setup  [6] latent loop  [7] chunk precompute  [8] run starts (fills, block scan)
-    // [9] row copy-out  [10] runs  [11] after the CABAC (pass end)
+    // chain wave: [0] ARM + index (to the table read)  [1] table wait  [2] CABAC  [3] passes
+    // [4] coded latents  [5] setup  [6] latent loop  [7] waits for the helper's preG
+    // [8] run starts (fills, block scan)  [9] row copy-out  [10] runs  [11] after the CABAC
+    // helper wave (lanes 12..15 of the dump): [12] busy (chunk precompute)  [13] chunks computed
+    // [14] chunks skipped (no coded latent)  [15] waiting
     uint32_t st_v = 0;
-#define LACC(k, d) st_v += (threadIdx.x == (k)) ? (uint32_t)(d) : 0u
+#define LACC(k, d) st_v += (lane == (k)) ? (uint32_t)(d) : 0u
 #define CSTAMP(var) const uint64_t var = __builtin_amdgcn_s_memtime()
     const uint64_t t_begin = __builtin_amdgcn_s_memtime();
 #else
@@ -770,20 +772,22 @@ __global__ __launch_bounds__(64) void dec_arm_chain_kernel(const ArmStreamDesc *
 #define CSTAMP(var)
 #endif
     extern __shared__ int32_t smem[];
-    uint32_t *ctab = reinterpret_cast<uint32_t *>(smem);               // 17 x 50 packed bin codes
-    int32_t *w0s = smem + 17 * 50;                                      // [16][16] layer-0 weights, [16] biases
+    volatile int32_t *ctl = smem;                                       // [0] ready seq [1] chain seq [2] done
+    uint32_t *ctab = reinterpret_cast<uint32_t *>(smem + 4);            // 17 x 50 packed bin codes
+    int32_t *w0s = smem + 4 + 17 * 50 + 2;                              // [16][16] layer-0 weights, [16] biases (16 B aligned)
     int32_t *pre = w0s + 16 * 16 + 16;                                  // [kPreRing + kPreMir][16] preG
     int32_t *ring = pre + (kPreRing + kPreMir) * 16;                    // kRingS x pitch
     uint8_t *bmap = reinterpret_cast<uint8_t *>(ring + kRingS * pitch); // block sig/flat map
 
     const ArmStreamDesc S = streams[blockIdx.x];
-    const int lane = threadIdx.x;
+    const int tid = threadIdx.x, wid = tid >> 6, lane = tid & 63;
     const int grp = lane >> 4, o = lane & 15;
     const bool live = o < D;
     const int h = S.h, w = S.w;
     const bool w24 = (S.flags & 1) != 0;
+    const int nch = (w + 63) >> 6; // 64-latent chunks per row
 
-    for (int i = lane; i < 17 * 50; i += 64) {
+    for (int i = tid; i < 17 * 50; i += 128) {
         const uint32_t v = c_ctx.v[2 * i], vs = c_ctx.v[2 * i + 1];
         uint32_t e = 0;
         for (int k = 0; k < 4; ++k) {
@@ -795,11 +799,158 @@ __global__ __launch_bounds__(64) void dec_arm_chain_kernel(const ArmStreamDesc *
         m.init((int)(vs & 0xFF));
         ctab[i] = e | (code6(m.state()) << 24);
     }
-    for (int i = lane; i < kRingS * pitch; i += 64) ring[i] = 0;
-    for (int i = lane; i < 16 * 16 + 16; i += 64) {
+    for (int i = tid; i < kRingS * pitch; i += 128) ring[i] = 0;
+    for (int i = tid; i < 16 * 16 + 16; i += 128) {
         const int r = i >> 4, cc = i & 15;
         w0s[i] = i < 256 ? (r < D && cc < D ? S.weights[r * D + cc] : 0) : (cc < D ? S.weights[D * D + cc] : 0);
     }
+    if (tid < 4) ctl[tid] = 0;
+
+    // ---- CABAC start + block significance / flat maps (BACContext::set_layer, cc-bac.h:24-130);
+    // both waves run it (the map is written by thread 0), the chain wave keeps the CABAC state
+    Cabac<DevBytesV> cab0;
+    cab0.src.init(S.bytes, S.nbytes);
+    cab0.start();
+    const int updated = S.sig_blk < 0;
+    const int blk = S.sig_blk < 0 ? -S.sig_blk : S.sig_blk;
+    int shift = 0;
+    while ((1 << shift) < blk) ++shift;
+    const int mask = (1 << shift) - 1;
+    int nby = 1, nbx = 1;
+    if (blk > 0) {
+        nby = (h + blk - 1) >> shift;
+        nbx = (w + blk - 1) >> shift;
+    }
+    const int nblk = nby * nbx;
+    for (int i = tid; i < nblk; i += 128) bmap[i] = 1; // bit0 sig, bit1 flat
+    __syncthreads();
+    if (nblk > 1) {
+        if (cab0.ep()) {
+            Model m;
+            m.init(65);
+            for (int i = 0; i < nblk; ++i) {
+                const uint32_t b = updated ? cab0.bin_adaptive(m) : cab0.ep();
+                if (tid == 0) bmap[i] = (uint8_t)b;
+            }
+        }
+        __syncthreads();
+        if (cab0.ep()) {
+            Model m;
+            m.init(65);
+            for (int i = 0; i < nblk; ++i) {
+                const int sig = __builtin_amdgcn_readfirstlane((int)bmap[i]);
+                if (sig) {
+                    const uint32_t f = updated ? cab0.bin_adaptive(m) : cab0.ep();
+                    if (tid == 0) bmap[i] = (uint8_t)(sig | (f << 1));
+                }
+            }
+        }
+    }
+    __syncthreads();
+    auto lds_order = []() __attribute__((always_inline)) { // this wave's LDS stores before its later loads
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    };
+
+    if (wid == 1) {
+        // ================= helper wave: preG of every chunk with a coded latent, in (row, chunk)
+        // order, into ring slot seq & 3 (4 slots + the mirror of slot 0's first 8 entries), as
+        // soon as (a) the chain wave has left the chunk that held the slot (chain seq >= seq - 3)
+        // and (b) the row above is final under the chunk's contexts (done >= its last column)
+        const int dmax = blk > 0 ? 0 : 1; // no block map: every latent coded
+        int seq = 0;
+        for (int y = 0; y < h; ++y) {
+            const int brow = blk > 0 ? (y >> shift) * nbx : 0;
+            for (int c = 0; c < nch; ++c, ++seq) {
+                CSTAMP(tw0);
+                // is any latent of [64 c, 64 c + 64) coded (the ARM evaluated there)?
+                bool coded = dmax != 0;
+                if (!coded) {
+                    const int b0 = (c * 64) >> shift, b1 = (min(c * 64 + 64, w) - 1) >> shift;
+                    const int bb = b0 + lane;
+                    const int f = bb <= b1 ? (int)bmap[brow + bb] : 0;
+                    // sig and not flat: every latent; sig and flat: the corner, in the block's first row
+                    coded = __ballot(bb <= b1 && (f == 1 || (f == 3 && !(y & mask)))) != 0;
+                }
+                const int need = y == 0 ? 0 : (y - 1) * w + min(c * 64 + 66, w);
+                // bounded: a synchronisation bug ends in a wrong decode (caught by the md5 tests), not
+                // in a wave that never retires
+                for (int spin = 0; spin < (1 << 24); ++spin) {
+                    if (__builtin_amdgcn_readfirstlane(ctl[1]) >= seq - 3 && __builtin_amdgcn_readfirstlane(ctl[2]) >= need)
+                        break;
+                    __builtin_amdgcn_s_sleep(1);
+                }
+                CSTAMP(tw1);
+                LACC(15, tw1 - tw0);
+                if (coded) {
+                    const int slot = seq & 3;
+                    const int xx = min(c * 64 + lane, w - 1); // lanes past the row end: a copy nobody reads
+                    const int32_t *up = ring + ((y + 3) & 3) * pitch + kPad;
+                    int32_t ctx[D];
+#pragma unroll
+                    for (int i = 0; i < DA; ++i) {
+                        int dy, dx;
+                        ctx_dydx<D>(i, dy, dx);
+                        ctx[i] = ring[((y + dy) & 3) * pitch + kPad + xx + dx];
+                    }
+#pragma unroll
+                    for (int j = 0; j < kDS; ++j) ctx[DA + j] = up[xx - kDS + j]; // the guesses
+                    // 24-bit products when the weights and every context fit (|v| < 2^22)
+                    bool small = w24;
+#pragma unroll
+                    for (int i = 0; i < D; ++i) small = small && (uint32_t)(ctx[i] + (1 << 22)) < (1u << 23);
+                    const bool f24 = __ballot(!small) == 0;
+                    int32_t *dst = pre + (slot * 64 + lane) * 16;
+                    int32_t *mir = pre + (kPreRing + lane) * 16;
+                    auto sums = [&](auto F24) __attribute__((always_inline)) {
+                        constexpr bool fz = decltype(F24)::value;
+#pragma unroll
+                        for (int n = 0; n < 16; n += 4) {
+                            int32_t acc[4];
+#pragma unroll
+                            for (int q = 0; q < 4; ++q) {
+                                const int nn = n + q;
+                                if (nn >= D) {
+                                    acc[q] = 0;
+                                    continue;
+                                }
+                                int32_t a = w0s[256 + nn] + ctx[nn] * 256; // bias + own residual
+                                const int4 *wr = reinterpret_cast<const int4 *>(w0s + 16 * nn);
+#pragma unroll
+                                for (int i4 = 0; i4 < (D + 3) / 4; ++i4) {
+                                    const int4 wv = wr[i4];
+                                    const int32_t wk[4] = {wv.x, wv.y, wv.z, wv.w};
+#pragma unroll
+                                    for (int k = 0; k < 4; ++k)
+                                        if (4 * i4 + k < D) a += imul<fz>(wk[k], ctx[4 * i4 + k]);
+                                }
+                                acc[q] = a;
+                            }
+                            const int4 v4{acc[0], acc[1], acc[2], acc[3]};
+                            *reinterpret_cast<int4 *>(dst + n) = v4;
+                            if (slot == 0 && lane < kPreMir) *reinterpret_cast<int4 *>(mir + n) = v4;
+                        }
+                    };
+                    if (f24) sums(std::true_type{});
+                    else sums(std::false_type{});
+                    LACC(13, 1);
+                } else {
+                    LACC(14, 1);
+                }
+                lds_order();
+                if (lane == 0) ctl[0] = seq + 1;
+                CSTAMP(tw2);
+                LACC(12, tw2 - tw1);
+            }
+        }
+#if defined(CCMI_ARM_STAMPS)
+        if (lane >= 12 && lane < 16 && S.dbg) S.dbg[lane] = st_v;
+#endif
+        return;
+    }
+
+    // ================= chain wave
     // guess-error coefficients: latent x - j is a decoded (not guessed) neighbour of row g's
     // latent x + g iff g + j <= 3, at context dx = -(g + j), index DA + 3 - (g + j); the weight
     // carries the neuron's own residual when that index is its own
@@ -824,47 +975,6 @@ __global__ __launch_bounds__(64) void dec_arm_chain_kernel(const ArmStreamDesc *
     const int32_t Wo0 = live ? ob[o] : 0, Wo1 = live ? ob[D + o] : 0;
     // the output biases ride in neuron 0's product (the row sums add them once)
     const int32_t Bo0 = o == 0 ? ob[2 * D] : 0, Bo1 = o == 0 ? ob[2 * D + 1] : 0;
-
-    // ---- CABAC start + block significance / flat maps (BACContext::set_layer, cc-bac.h:24-130)
-    Cabac<DevBytesV> cab0;
-    cab0.src.init(S.bytes, S.nbytes);
-    cab0.start();
-    const int updated = S.sig_blk < 0;
-    const int blk = S.sig_blk < 0 ? -S.sig_blk : S.sig_blk;
-    int shift = 0;
-    while ((1 << shift) < blk) ++shift;
-    const int mask = (1 << shift) - 1;
-    int nby = 1, nbx = 1;
-    if (blk > 0) {
-        nby = (h + blk - 1) >> shift;
-        nbx = (w + blk - 1) >> shift;
-    }
-    const int nblk = nby * nbx;
-    for (int i = lane; i < nblk; i += 64) bmap[i] = 1; // bit0 sig, bit1 flat
-    __syncthreads();
-    if (nblk > 1) {
-        if (cab0.ep()) {
-            Model m;
-            m.init(65);
-            for (int i = 0; i < nblk; ++i) {
-                const uint32_t b = updated ? cab0.bin_adaptive(m) : cab0.ep();
-                if (lane == 0) bmap[i] = (uint8_t)b;
-            }
-        }
-        __syncthreads();
-        if (cab0.ep()) {
-            Model m;
-            m.init(65);
-            for (int i = 0; i < nblk; ++i) {
-                const int sig = __builtin_amdgcn_readfirstlane((int)bmap[i]);
-                if (sig) {
-                    const uint32_t f = updated ? cab0.bin_adaptive(m) : cab0.ep();
-                    if (lane == 0) bmap[i] = (uint8_t)(sig | (f << 1));
-                }
-            }
-        }
-    }
-    __syncthreads();
     Cab6 cab;
     cab.from(cab0);
 
@@ -873,11 +983,6 @@ __global__ __launch_bounds__(64) void dec_arm_chain_kernel(const ArmStreamDesc *
     uint32_t qspan = 0;
     // 0: 24-bit layer 0 + 24-bit hidden / output layers; 1: 32-bit layer 0; 2: all 32-bit
     int mode = w24 ? 0 : 2;
-    auto lds_order = []() __attribute__((always_inline)) { // this wave's LDS stores before its later loads (other lanes read them)
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-        __builtin_amdgcn_wave_barrier();
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-    };
 #if defined(CCMI_ARM_STAMPS)
     LACC(5, __builtin_amdgcn_s_memtime() - t_begin);
     const uint64_t t_loop = __builtin_amdgcn_s_memtime();
@@ -887,7 +992,8 @@ __global__ __launch_bounds__(64) void dec_arm_chain_kernel(const ArmStreamDesc *
         int32_t *row = ring + (y & 3) * pitch + kPad;
         const int32_t *up = ring + ((y + 3) & 3) * pitch + kPad;
         const int brow = blk > 0 ? (y >> shift) * nbx : 0;
-        int pre_next = 0;        // next 64-latent chunk of preG to compute for this row
+        const int rseq = y * nch;            // chunk sequence number of (y, 0)
+        const int rring = (rseq * 64) & 255; // preG ring index of latent (y, 0); latent x at (rring + x) & 255
         int pre_lim = 0;         // a pass at x needs x + 8 <= pre_lim (INT_MAX once the row is covered)
         int32_t vrow = 0;        // lane i < x - xb: decoded value of latent xb + i, not stored yet
         int xb = 0;
@@ -897,79 +1003,29 @@ __global__ __launch_bounds__(64) void dec_arm_chain_kernel(const ArmStreamDesc *
         int ub = 0;
         int x = 0;
 
+        // stores the collected values and publishes the row's progress (the helper's
+        // chunks of row y + 1 read this row)
         auto flush = [&]() __attribute__((always_inline)) {
             if (lane < x - xb) row[xb + lane] = vrow;
             xb = x;
-        };
-        // preG of chunk c (latents 64 c .. 64 c + 63, lane = latent)
-        auto chunk = [&](int c) __attribute__((always_inline)) {
-            CSTAMP(tc0);
-            const int xx = c * 64 + lane;
-            const bool in = xx < w; // lanes past the row end compute sums nobody reads
-            int32_t ctx[D];
-#pragma unroll
-            for (int i = 0; i < DA; ++i) {
-                int dy, dx;
-                ctx_dydx<D>(i, dy, dx);
-                ctx[i] = in ? ring[((y + dy) & 3) * pitch + kPad + xx + dx] : 0;
-            }
-#pragma unroll
-            for (int j = 0; j < kDS; ++j) ctx[DA + j] = in ? up[xx - kDS + j] : 0; // the guesses
-            // the weights re-read per chunk: loop-invariant LDS loads hoisted out of the row loop
-            // held all 272 of them in VGPRs (occupancy 1); an opaque offset keeps them here
-            int woff = 0;
-            asm volatile("" : "+s"(woff));
-            const int32_t *wl = w0s + woff;
-            const int ri = xx & (kPreRing - 1);
-            int32_t *dst = pre + ri * 16;
-            int32_t *mir = pre + (kPreRing + ri) * 16;
-            auto sums = [&](auto F24) __attribute__((always_inline)) {
-                constexpr bool f24 = decltype(F24)::value;
-#pragma unroll
-                for (int n = 0; n < 16; n += 4) {
-                    int32_t acc[4];
-#pragma unroll
-                    for (int q = 0; q < 4; ++q) {
-                        const int nn = n + q;
-                        if (nn >= D) {
-                            acc[q] = 0;
-                            continue;
-                        }
-                        int32_t a = wl[256 + nn] + ctx[nn] * 256; // bias + own residual
-                        const int4 *wr = reinterpret_cast<const int4 *>(wl + 16 * nn);
-#pragma unroll
-                        for (int i4 = 0; i4 < (D + 3) / 4; ++i4) {
-                            const int4 wv = wr[i4];
-                            const int32_t wk[4] = {wv.x, wv.y, wv.z, wv.w};
-#pragma unroll
-                            for (int k = 0; k < 4; ++k)
-                                if (4 * i4 + k < D) a += imul<f24>(wk[k], ctx[4 * i4 + k]);
-                        }
-                        acc[q] = a;
-                    }
-                    const int4 v4{acc[0], acc[1], acc[2], acc[3]};
-                    *reinterpret_cast<int4 *>(dst + n) = v4;
-                    if (ri < kPreMir) *reinterpret_cast<int4 *>(mir + n) = v4;
-                }
-            };
-            if (mode == 0) sums(std::true_type{});
-            else sums(std::false_type{});
-#if defined(CCMI_ARM_STAMPS)
-            __builtin_amdgcn_s_waitcnt(0);
-            LACC(7, __builtin_amdgcn_s_memtime() - tc0);
-#endif
-        };
-        // preG for latents up to x + 7 (the chunks of [x, x + 8) not computed yet)
-        auto ensure = [&]() __attribute__((always_inline)) {
-            const int hi = (min(x + 8, w) - 1) >> 6;
-            for (int c = max(pre_next, x >> 6); c <= hi; ++c) chunk(c);
-            pre_next = max(pre_next, hi + 1);
-            pre_lim = pre_next * 64 >= w ? 0x7FFFFFFF : pre_next * 64;
             lds_order();
+            if (lane == 0) ctl[2] = y * w + x;
+        };
+        // preG for latents up to x + 7: publish the chain's chunk (frees the slots before it) and
+        // wait for the helper
+        auto wait_pre = [&]() __attribute__((always_inline)) {
+            CSTAMP(tq0);
+            const int need = (min(x + 8, w) - 1) >> 6;
+            if (lane == 0) ctl[1] = rseq + (x >> 6);
+            for (int spin = 0; spin < (1 << 24) && __builtin_amdgcn_readfirstlane(ctl[0]) <= rseq + need; ++spin)
+                __builtin_amdgcn_s_sleep(1); // bounded, as the helper's wait
+            pre_lim = (need + 1) * 64 >= w ? 0x7FFFFFFF : (need + 1) * 64;
+            CSTAMP(tq1);
+            LACC(7, tq1 - tq0);
         };
 
         // one mode's pass loop over the current run [x, cend): returns at the run end, when the
-        // next pass needs preG not computed yet or a flush of vrow, or when the 24-bit guard
+        // next pass needs preG not waited for yet or a flush of vrow, or when the 24-bit guard
         // trips (mode 0 only); one compare per pass against the bound of all three
         auto passes = [&](int cend, auto F1, auto FW) __attribute__((always_inline)) {
             constexpr bool f1 = decltype(F1)::value, fw = decltype(FW)::value;
@@ -993,7 +1049,7 @@ __global__ __launch_bounds__(64) void dec_arm_chain_kernel(const ArmStreamDesc *
                 const uint32_t ent = ctab[__mul24(mi, 50) + si];
                 const int32_t mq = mr >> 8;
                 // ---- the next pass's inputs, read ahead (it starts at x + nd, nd = 1 .. 4)
-                const int32_t *pp = pre + ((x & (kPreRing - 1)) + grp) * 16 + o;
+                const int32_t *pp = pre + (((rring + x) & (kPreRing - 1)) + grp) * 16 + o;
                 const int32_t nx0 = pp[16], nx1 = pp[32], nx2 = pp[48], nx3 = pp[64];
                 const int32_t upn = up[x + (lane & 7)];
                 CSTAMP(t1);
@@ -1047,12 +1103,12 @@ __global__ __launch_bounds__(64) void dec_arm_chain_kernel(const ArmStreamDesc *
                     // zero block, flat block below its first row (copy of the row above), or the
                     // rest of a flat block's first row (copy of its decoded corner)
                     flush();
-                    lds_order();
                     const int kind = !(bm & 1) ? 0 : (y & mask) ? 2 : 1;
                     const int32_t c1 = kind == 1 ? __builtin_amdgcn_readfirstlane(row[x - 1]) : 0;
                     for (int i = lane; i < bend - x; i += 64) row[x + i] = kind == 0 ? 0 : kind == 1 ? c1 : up[x + i];
                     x = bend;
                     xb = x;
+                    flush(); // nothing to store: publishes the filled block
                     LACC(8, __builtin_amdgcn_s_memtime() - tr0);
                     continue;
                 }
@@ -1061,7 +1117,6 @@ __global__ __launch_bounds__(64) void dec_arm_chain_kernel(const ArmStreamDesc *
                 } else {
                     // consecutive coded, non-flat blocks: the first other block ends the run
                     int b = bx + 1;
-                    cend = bend;
                     while (b < nbx) {
                         const int bb = b + lane;
                         const int f = bb < nbx ? (int)bmap[brow + bb] : 0;
@@ -1077,21 +1132,20 @@ __global__ __launch_bounds__(64) void dec_arm_chain_kernel(const ArmStreamDesc *
             }
             // run start: guess errors of latents x - 1 .. x - 3 from the stored row (fills)
             flush();
-            lds_order();
             {
                 const int32_t d = lane < kDS ? row[x - 1 - lane] - up[x - 1 - lane] : 0;
                 e1 = __builtin_amdgcn_readlane(d, 0);
                 e2 = __builtin_amdgcn_readlane(d, 1);
                 e3 = __builtin_amdgcn_readlane(d, 2);
             }
-            if (x + 8 > pre_lim) ensure();
-            pfa = pre[((x & (kPreRing - 1)) + grp) * 16 + o];
+            if (x + 8 > pre_lim) wait_pre();
+            pfa = pre[(((rring + x) & (kPreRing - 1)) + grp) * 16 + o];
             upv = up[x + (lane & 7)];
             ub = 0;
             LACC(8, __builtin_amdgcn_s_memtime() - tr0);
             LACC(10, 1);
             while (x < cend) {
-                if (x + 8 > pre_lim) ensure();
+                if (x + 8 > pre_lim) wait_pre();
                 if (x - xb > 60) flush();
                 if (mode == 0) {
                     passes(cend, std::true_type{}, std::true_type{});
@@ -1104,15 +1158,17 @@ __global__ __launch_bounds__(64) void dec_arm_chain_kernel(const ArmStreamDesc *
             }
         }
         CSTAMP(tw0);
-        flush();
-        lds_order();
+        flush(); // done = (y + 1) w: the whole row is final
+        // the chain is past every chunk of this row: without this, rows with no coded run (no
+        // wait_pre) left the helper waiting for slots forever (the decode's last rows, uncoded)
+        if (lane == 0) ctl[1] = (y + 1) * nch;
         int32_t *dst = S.out + (int64_t)y * w;
         for (int i = lane; i < w; i += 64) dst[i] = row[i];
         LACC(9, __builtin_amdgcn_s_memtime() - tw0);
     }
 #if defined(CCMI_ARM_STAMPS)
     LACC(6, __builtin_amdgcn_s_memtime() - t_loop);
-    if (lane < 16 && S.dbg) S.dbg[lane] = st_v;
+    if (lane < 12 && S.dbg) S.dbg[lane] = st_v;
 #endif
 #undef LACC
 #undef CSTAMP
@@ -1537,12 +1593,12 @@ int launch_dec_arm(const ArmStreamDesc *d_streams, int n_streams, int max_w, int
     constexpr bool spec_off = false;
 #endif
     // the chain kernel: packed context table, layer-0 weights, the preG ring (+ mirror), ring
-    const size_t lds_lat = sizeof(int32_t) * (17 * 50 + 16 * 16 + 16 + (kPreRing + kPreMir) * 16 + kRingS * pitch) +
+    const size_t lds_lat = sizeof(int32_t) * (4 + 17 * 50 + 2 + 16 * 16 + 16 + (kPreRing + kPreMir) * 16 + kRingS * pitch) +
                            ((size_t)max_blocks + 16);
     if (!spec_off && d <= 16 && d > kDS && nh >= 1 && lds_lat <= 160 * 1024) {
 #define CCMI_ARM_LAT(DD, NN)                                                                                    \
         if (d == DD && nh == NN) {                                                                              \
-            hipLaunchKernelGGL((dec_arm_chain_kernel<DD, NN>), dim3(n_streams), dim3(64), lds_lat, s, d_streams, pitch); \
+            hipLaunchKernelGGL((dec_arm_chain_kernel<DD, NN>), dim3(n_streams), dim3(128), lds_lat, s, d_streams, pitch); \
             CCMI_HIP_CHECK(hipGetLastError());                                                                  \
             return CCMI_OK;                                                                                     \
         }
