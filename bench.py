@@ -530,21 +530,22 @@ def encoder_shard(rank: int, lambdas=None):
 
 
 # Per-kernel rooflines of the encoder's training step, from a committed rocprofv3 kernel trace
-# of tools/prof_train.sh (8 frames of 512 x 768, hop, c3x; one launch per iteration each).
-TRAIN_PROFILE = "profiles/r4y_train_kernel_stats.csv"
+# of tools/bench_train.py 8 with CCMI_ARM_OVERLAP=0 (every kernel alone; 8 frames of 512 x 768,
+# hop, c3x; one launch per iteration each; tools/gpu_r5e.sh)
+TRAIN_PROFILE = "profiles/r5e_train_kernel_stats.csv"
 TRAIN_FRAMES, TRAIN_H, TRAIN_W = 8, 512, 768
 
 
 def train_kernel_rooflines(csv_path: str = TRAIN_PROFILE) -> list:
     """FLOPs per launch / average launch duration for the two largest training kernels.
-    t_head_bwd<7, 3>: per pixel the hidden-layer recompute (48 x 7 MAC), g_h (48 x 3), g_x (7 x 48),
+    t_head_bwd(_t)<7, 3>: per pixel the hidden-layer recompute (48 x 7 MAC), g_h (48 x 3), g_x (7 x 48),
     dW1 (3 x 48) and dW0 (48 x 7): 1,296 MAC = 2,592 FLOP.  t_arm16<2>: per latent 3 x the ARM
     forward (dim 16, 2 hidden layers + the 2-wide output: 544 MAC) = 3,264 FLOP (forward +
     input and weight gradients)."""
     import csv
     npx = TRAIN_H * TRAIN_W
     nlat = sum((TRAIN_H >> k) * (TRAIN_W >> k) for k in range(7))
-    flops = {"t_head_bwd<7, 3": 2592 * npx * TRAIN_FRAMES, "t_arm16<2>": 3264 * nlat * TRAIN_FRAMES}
+    flops = {"t_head_bwd": 2592 * npx * TRAIN_FRAMES, "t_arm16<2>": 3264 * nlat * TRAIN_FRAMES}
     out = []
     path = ROOT / csv_path
     if not path.exists():

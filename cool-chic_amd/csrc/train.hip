@@ -1580,6 +1580,193 @@ __global__ __launch_bounds__(kHeadT) void t_head_bwd(const float *__restrict__ d
     }
 }
 
+// Tiled form (the one launched): the hidden layer stays in registers (pairs of units, packed
+// FMAs, as the PAIR form), and the LDS rows that feed the weight-gradient MFMAs hold ONE
+// 16-unit tile at a time (pitch 17) next to a per-pixel row gp | 0 | x | 1 | 0 shared by both
+// MFMA loops: 7.7 KB of LDS per wave instead of 14.8 KB (LDS had capped the full-width form at
+// 2.5 waves / SIMD with 55 % of its wave cycles in WAIT_ANY; profiles/r4w_train_pmc.txt).
+// Per tile q: h rows -> dW1 tile (M = k < 3, N = the tile's units) -> g_h rows (the ReLU mask
+// from the registers) -> dW0 tile (M = the tile's units, N = i <= CIN) and this pixel's g_x.
+// The output layer must be linear (g.r1 == 0, every reference architecture's "X-1-linear-none"):
+// then g_out needs no pass over all units first, and a tile's units are computed just in time.
+template <int CIN, int NT>
+__global__ __launch_bounds__(kHeadT, 4) void t_head_bwd_t(const float *__restrict__ dense, const float *__restrict__ gz0,
+                                                       Geo g, const float *__restrict__ th, int64_t ps,
+                                                       float *__restrict__ gdense, float *__restrict__ gth, int64_t gstride)
+{
+    extern __shared__ float s_dyn[];
+    constexpr int kTP = 17;            // tile row pitch: 16 units + 1 (odd: conflict-free row writes)
+    constexpr int kSW = (CIN + 6) | 1; // pixel row: gp[0..3) | 0 | x[0..CIN) | 1 | 0, odd pitch
+    constexpr int kGX = 4;             // first x column
+    __shared__ __attribute__((aligned(16))) float s_rec[16 * NT][12];
+    static_assert(CIN + 4 <= 12, "hidden-unit record");
+    constexpr int kPR = 2 * (CIN + 4) <= 24 ? 24 : 32;
+    static_assert(8 * NT * kPR <= 16 * NT * 12, "pair records fit in the record area");
+    float(*s_rec2)[kPR] = reinterpret_cast<float(*)[kPR]>(&s_rec[0][0]);
+    const int b = blockIdx.y, t = threadIdx.x, lane = t & 63, w = t >> 6;
+    const int hid = g.hid;
+    const int64_t npx = (int64_t)g.H * g.W;
+    const float *P = th + (int64_t)b * ps;
+    // pair records: unit pair jp = units 2jp, 2jp + 1, field f interleaved as [2f + parity];
+    // units >= hid are zero records (h = 0: no contribution anywhere)
+    for (int e = t; e < 8 * NT * kPR; e += kHeadT) {
+        const int jp = e / kPR, r = e - jp * kPR, f = r >> 1, j = 2 * jp + (r & 1);
+        float v = 0.f;
+        if (j < hid) {
+            if (f < CIN) v = P[g.w0 + j * CIN + f];
+            else if (f == CIN) v = P[g.b0 + j];
+            else if (f <= CIN + 3) v = P[g.w1 + (f - CIN - 1) * hid + j];
+        }
+        s_rec2[jp][r] = v;
+    }
+    const float bo0 = P[g.b1], bo1 = P[g.b1 + 1], bo2 = P[g.b1 + 2];
+    float *sv = s_dyn + w * 64 * (kTP + kSW), *sw = sv + 64 * kTP;
+    const int ln = lane & 15, lk = lane >> 4;
+    const int ia = ln < 3 ? ln : 3, ib = kGX + (ln <= CIN ? ln : CIN + 1); // operand columns (pads read 0)
+    v4f a1[NT], a0[NT];
+#pragma unroll
+    for (int q = 0; q < NT; ++q) a1[q] = a0[q] = v4f{0.f, 0.f, 0.f, 0.f};
+    float db1[3] = {0.f, 0.f, 0.f};
+    __syncthreads(); // records staged
+    const int64_t nchunk = (npx + kHeadT - 1) / kHeadT;
+    float nx[CIN], ng[3];
+    auto load_chunk = [&](int64_t ch) {
+        const int64_t p = ch * kHeadT + t;
+        const bool valid = p < npx;
+        const float *x = dense + (int64_t)b * CIN * npx + p;
+        const float *G = gz0 + (int64_t)b * 3 * npx + p;
+#pragma unroll
+        for (int i = 0; i < CIN; ++i) nx[i] = valid ? x[i * npx] : 0.f;
+#pragma unroll
+        for (int k = 0; k < 3; ++k) ng[k] = valid ? G[k * npx] : 0.f;
+    };
+    using ccmi_fwd::f2;
+    const f2 lo0 = f2(g.r0 ? 0.f : -INFINITY);
+    if ((int64_t)blockIdx.x < nchunk) load_chunk(blockIdx.x);
+    for (int64_t ch = blockIdx.x; ch < nchunk; ch += gridDim.x) {
+        const int64_t p = ch * kHeadT + t;
+        const bool valid = p < npx;
+        float xv[CIN], gp1[3];
+#pragma unroll
+        for (int i = 0; i < CIN; ++i) xv[i] = nx[i];
+#pragma unroll
+        for (int k = 0; k < 3; ++k) gp1[k] = ng[k];
+        if (ch + gridDim.x < nchunk) load_chunk(ch + gridDim.x);
+#pragma unroll
+        for (int k = 0; k < 3; ++k) db1[k] += gp1[k];
+        // ---- this pixel's row: gp | 0 | x | 1 | 0 (invalid pixels: gp = 0, x = 0)
+#pragma unroll
+        for (int k = 0; k < 3; ++k) sw[lane * kSW + k] = gp1[k];
+        sw[lane * kSW + 3] = 0.f;
+#pragma unroll
+        for (int i = 0; i < CIN; ++i) sw[lane * kSW + kGX + i] = xv[i];
+        sw[lane * kSW + kGX + CIN] = 1.f;
+        sw[lane * kSW + kGX + CIN + 1] = 0.f;
+        f2 gxp[CIN];
+#pragma unroll
+        for (int i = 0; i < CIN; ++i) gxp[i] = f2(0.f);
+#pragma unroll
+        for (int q = 0; q < NT; ++q) {
+            // the tile's records through an opaque base: the compiler must not keep them (or the
+            // other tiles') loaded across the chunk
+            int roff = 0;
+            asm volatile("" : "+s"(roff));
+            const float(*rec)[kPR] = s_rec2 + 8 * q + roff;
+            float *row = sv + lane * kTP;
+            // ---- the tile's hidden units h (pairs, packed FMAs) -> this lane's row; only the
+            // ReLU mask stays in a register (bit 2u + parity)
+            uint32_t hmask = 0;
+#pragma unroll 2
+            for (int u = 0; u < 8; ++u) {
+                const f2 *r = reinterpret_cast<const f2 *>(rec[u]);
+                f2 a = r[CIN];
+#pragma unroll
+                for (int i = 0; i < CIN; ++i) a = __builtin_elementwise_fma(r[i], f2(xv[i]), a);
+                a = __builtin_elementwise_max(a, lo0);
+                row[2 * u] = a.x;
+                row[2 * u + 1] = a.y;
+                hmask |= ((a.x > 0.f ? 1u : 0u) | (a.y > 0.f ? 2u : 0u)) << (2 * u);
+            }
+            wave_lds_sync();
+            // ---- dW1 tile q += gp^T h; K = pixels px = s + 16 (lane >> 4): the two 16-lane groups
+            // of each 32-lane half read rows 16 apart, 16 banks apart (odd pitches)
+#pragma unroll
+            for (int s = 0; s < 16; ++s) {
+                const int px = s + 16 * lk;
+                a1[q] = mfma4(sw[px * kSW + ia], sv[px * kTP + ln], a1[q]);
+            }
+            wave_lds_sync(); // every lane has read the h rows before g_h replaces them
+            // ---- g_h of the tile (replaces h in this lane's row) and g_x
+            const uint32_t keep = g.r0 ? hmask : 0xFFFFu;
+#pragma unroll 2
+            for (int u = 0; u < 8; ++u) {
+                const f2 *r = reinterpret_cast<const f2 *>(rec[u]);
+                f2 gh = r[CIN + 1] * f2(gp1[0]);
+                gh = __builtin_elementwise_fma(r[CIN + 2], f2(gp1[1]), gh);
+                gh = __builtin_elementwise_fma(r[CIN + 3], f2(gp1[2]), gh);
+                gh.x = (keep >> (2 * u)) & 1u ? gh.x : 0.f; // selects, not exec-mask branches
+                gh.y = (keep >> (2 * u + 1)) & 1u ? gh.y : 0.f;
+                row[2 * u] = gh.x;
+                row[2 * u + 1] = gh.y;
+#pragma unroll
+                for (int i = 0; i < CIN; ++i) gxp[i] = __builtin_elementwise_fma(r[i], gh, gxp[i]);
+            }
+            wave_lds_sync();
+            // ---- dW0 | db0 tile q += g_h^T [x | 1]
+#pragma unroll
+            for (int s = 0; s < 16; ++s) {
+                const int px = s + 16 * lk;
+                a0[q] = mfma4(sv[px * kTP + ln], sw[px * kSW + ib], a0[q]);
+            }
+            wave_lds_sync(); // before the next tile's h (or the next chunk's rows) overwrite these
+        }
+        if (valid) {
+            float *gd = gdense + (int64_t)b * CIN * npx + p;
+#pragma unroll
+            for (int i = 0; i < CIN; ++i) gd[i * npx] = gxp[i].x + gxp[i].y;
+        }
+    }
+    // ---- flush (t_head_bwd's): the waves' partial rows meet in LDS, one atomic per value
+    const int nred = hid * (CIN + 4) + 3;
+    float *red = s_dyn + w * 64 * (kTP + kSW);
+    static_assert(64 * (kTP + kSW) >= 16 * NT * (CIN + 4) + 3, "a wave's partial row fits its LDS rows");
+    __syncthreads();
+#pragma unroll
+    for (int q = 0; q < NT; ++q) {
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            const int m = 4 * lk + r;
+            if (m < 3) { // dW1[k = m][j]
+                const int j = 16 * q + ln;
+                if (j < hid) red[hid * (CIN + 1) + m * hid + j] = a1[q][r];
+            }
+            const int j = 16 * q + m; // dW0[j][i = ln]
+            if (j < hid) {
+                if (ln < CIN) red[j * CIN + ln] = a0[q][r];
+                else if (ln == CIN) red[hid * CIN + j] = a0[q][r];
+            }
+        }
+    }
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {
+        const float v = wave_sum(db1[k]);
+        if (lane == 0) red[hid * (CIN + 4) + k] = v;
+    }
+    __syncthreads();
+    float *Gp = gth + (int64_t)b * gstride;
+    constexpr int kW = kHeadT / 64;
+    for (int e = t; e < nred; e += kHeadT) {
+        float v = 0.f;
+#pragma unroll
+        for (int ww = 0; ww < kW; ++ww) v += s_dyn[ww * 64 * (kTP + kSW) + e];
+        const int dst = e < hid * CIN ? g.w0 + e
+                        : e < hid * (CIN + 1) ? g.b0 + (e - hid * CIN)
+                        : e < hid * (CIN + 4) ? g.w1 + (e - hid * (CIN + 1))
+                                              : g.b1 + (e - hid * (CIN + 4));
+        atomicAdd(&Gp[dst], v);
+    }
+}
+
 // ------------------------------------------------------------------ upsampling backward
 // Polyphase taps of the 2x transposed conv: destination 2j + a reads source clamp(j + d)
 // with tap a + K/2 - 1 - 2d (fwd_ups.hip).
@@ -2202,6 +2389,17 @@ size_t align256(size_t v) { return (v + 255) / 256 * 256; }
 #ifndef CCMI_ARM_OVERLAP
 #define CCMI_ARM_OVERLAP 1
 #endif
+// the compile-time default, or the environment's CCMI_ARM_OVERLAP (0 .. 3) read once per process
+// (0 runs the ARM in line: kernel traces where every kernel runs alone)
+static int arm_overlap()
+{
+    static const int v = [] {
+        const char *e = getenv("CCMI_ARM_OVERLAP");
+        if (e && e[0] >= '0' && e[0] <= '3' && !e[1]) return e[0] - '0';
+        return (int)CCMI_ARM_OVERLAP;
+    }();
+    return v;
+}
 struct Plan {
     Geo g;
     ArmTiles at;
@@ -2341,7 +2539,7 @@ int make_plan(const ccmi_train_args *a, Plan &pl)
     pl.acc4 = take(4 * B * 4);
     pl.bc = take(4 * B * 2);
     pl.slots = take(4 * B * kDwSlots * (size_t)(g.syn_off - g.up_off));
-    if (CCMI_ARM_OVERLAP) pl.gq_arm = take(4 * B * g.N); // after acc4: zeroed with it
+    if (arm_overlap()) pl.gq_arm = take(4 * B * g.N); // after acc4: zeroed with it
     pl.total = o;
     return CCMI_OK;
 }
@@ -2406,16 +2604,27 @@ void launch_head(bool bwd, dim3 grid, hipStream_t s, const float *dense, const f
 {
     if (!bwd) hipLaunchKernelGGL((t_head_fwd<CIN>), grid, dim3(kT), 0, s, dense, g, th, ps, z0_or_gdense);
     else {
+        // the tiled form for a linear output layer (every reference architecture); the full-width
+        // form otherwise (and in -DCCMI_HEAD_BWD_FULL A/B builds)
+#if defined(CCMI_HEAD_BWD_FULL)
+        const bool tiled = false;
+#else
+        const bool tiled = !g.r1;
+#endif
         constexpr int kXP = (CIN + 2 > 5 ? CIN + 2 : 5) | 1; // t_head_bwd's per-wave LDS rows
-        const size_t lds = sizeof(float) * (kHeadT / 64) * 64 * (16 * ((g.hid + 15) / 16) + 1 + kXP);
-        // one resident round over the pixel chunks (LDS-bound: 5 workgroups per CU at 32,000 B
-        // each, 276 us; at exactly 32 KB the query also allowed 5, but they did not all fit: 399
-        // us against 286 us capped at 4; 512 / 768 / 2048 workgroups for the batch 515 / 356 /
-        // 333 us; profiles/r4n_*, r4o_*, r4y_*)
+        const size_t lds = tiled ? sizeof(float) * (kHeadT / 64) * 64 * (17 + ((CIN + 6) | 1))
+                                 : sizeof(float) * (kHeadT / 64) * 64 * (16 * ((g.hid + 15) / 16) + 1 + kXP);
+        // one resident round over the pixel chunks (full-width form LDS-bound: 5 workgroups per CU
+        // at 32,000 B each, 276 us; at exactly 32 KB the query also allowed 5, but they did not all
+        // fit: 399 us against 286 us capped at 4; profiles/r4n_*, r4o_*, r4y_*)
         const int64_t nchunk = ((int64_t)g.H * g.W + kHeadT - 1) / kHeadT;
 #define CCMI_HB(N)                                                                                                     \
-    hipLaunchKernelGGL((t_head_bwd<CIN, N, true>), resident_grid((const void *)t_head_bwd<CIN, N, true>, kHeadT, lds, nchunk, (int)grid.y), \
-                       dim3(kHeadT), lds, s, dense, gz0, g, th, ps, z0_or_gdense, gth, gstride)
+    if (tiled)                                                                                                         \
+        hipLaunchKernelGGL((t_head_bwd_t<CIN, N>), resident_grid((const void *)t_head_bwd_t<CIN, N>, kHeadT, lds, nchunk, (int)grid.y), \
+                           dim3(kHeadT), lds, s, dense, gz0, g, th, ps, z0_or_gdense, gth, gstride);                    \
+    else                                                                                                               \
+        hipLaunchKernelGGL((t_head_bwd<CIN, N, true>), resident_grid((const void *)t_head_bwd<CIN, N, true>, kHeadT, lds, nchunk, (int)grid.y), \
+                           dim3(kHeadT), lds, s, dense, gz0, g, th, ps, z0_or_gdense, gth, gstride)
         switch ((g.hid + 15) / 16) {
         case 1: CCMI_HB(1); break;
         case 2: CCMI_HB(2); break;
@@ -2574,7 +2783,7 @@ extern "C" int ccmi_train_step(const ccmi_train_args *a, void *stream)
         hipStream_t sa = s;
         float *gqa = gq;
         int cap = 1 << 20;
-        if (CCMI_ARM_OVERLAP > 0) {
+        if (arm_overlap() > 0) {
             lease.set = ccmi_streamset_acquire(1, 2, false);
             if (!lease.set) return CCMI_ERR_HIP;
             CCMI_HIP_CHECK(hipEventRecord(lease.set->ev[0], s));
@@ -2586,7 +2795,7 @@ extern "C" int ccmi_train_step(const ccmi_train_args *a, void *stream)
             join.ev = lease.set->ev[1];
             join.pending = true; // from here on every return joins
             gqa = F(pl.gq_arm);
-            cap = CCMI_ARM_OVERLAP;
+            cap = arm_overlap();
 #if defined(CCMI_DIAG_SIDE_SPIN)
             hipLaunchKernelGGL(t_diag_spin, dim3(1), dim3(64), 0, sa, (uint64_t)500000);
 #endif

@@ -43,7 +43,9 @@ BUDGET = {
     # that live only in the prologue / epilogue, outside the tile loop (477 -> 448 us per
     # launch against the 3-wave build, profiles/r4j_train_ab.txt)
     "t_arm16<2>": (128, 2, 12),
-    "t_head_bwd<7, 3, true>": (168, 0, 0),  # unit-pair packed form (default)
+    "t_head_bwd<7, 3, true>": (168, 0, 0),  # unit-pair packed form (output-ReLU architectures)
+    # the tiled form (linear output layer, every reference architecture): 4 waves / SIMD
+    "t_head_bwd_t<7, 3>": (128, 0, 0),
     "t_sp_bwd<1>": (128, 0, 0),  # 3x3 backward, input gradient
     "t_sp_bwd<2>": (128, 0, 0),  # 3x3 backward, weight gradients (4 waves / SIMD)
 }
