@@ -94,7 +94,7 @@ class DecodeArgs(C.Structure):
     ]
 
 
-HEAD_DEFAULT, HEAD_VALU, HEAD_MFMA = 0, 1, 2  # ccmi_decode_args.head (CCMI_HEAD_*)
+HEAD_DEFAULT, HEAD_VALU, HEAD_MFMA, HEAD_GENERIC = 0, 1, 2, 3  # ccmi_decode_args.head (CCMI_HEAD_*)
 
 
 _lib = None

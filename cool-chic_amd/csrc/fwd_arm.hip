@@ -147,19 +147,20 @@ __global__ __launch_bounds__(kThreads) void arm_fwd_kernel(
         f2 o[kNP][D];
 #pragma unroll
         for (int j = 0; j < D; ++j) {
+            // F.linear(x) + x, then ReLU: the accumulator starts at bias + residual (one packed
+            // add instead of two after the products; a different fp32 summation order, inside
+            // the forward's tolerance)
             f2 acc[kNP];
 #pragma unroll
-            for (int q = 0; q < kNP; ++q) acc[q] = f2(0.f);
+            for (int q = 0; q < kNP; ++q) acc[q] = a[q][j] + f2(bl[j]);
 #pragma unroll
             for (int i = 0; i < D; ++i) {
                 const f2 wji = f2(Wl[j * D + i]);
 #pragma unroll
                 for (int q = 0; q < kNP; ++q) acc[q] = __builtin_elementwise_fma(wji, a[q][i], acc[q]);
             }
-            // F.linear(x) + x, then ReLU
 #pragma unroll
-            for (int q = 0; q < kNP; ++q)
-                o[q][j] = __builtin_elementwise_max((acc[q] + f2(bl[j])) + a[q][j], f2(0.f));
+            for (int q = 0; q < kNP; ++q) o[q][j] = __builtin_elementwise_max(acc[q], f2(0.f));
         }
 #pragma unroll
         for (int q = 0; q < kNP; ++q)
@@ -171,8 +172,8 @@ __global__ __launch_bounds__(kThreads) void arm_fwd_kernel(
     f2 m[kNP], ls[kNP];
 #pragma unroll
     for (int q = 0; q < kNP; ++q) {
-        m[q] = f2(0.f);
-        ls[q] = f2(0.f);
+        m[q] = f2(Wo[2 * D]);
+        ls[q] = f2(Wo[2 * D + 1]);
     }
 #pragma unroll
     for (int i = 0; i < D; ++i) {
@@ -182,11 +183,6 @@ __global__ __launch_bounds__(kThreads) void arm_fwd_kernel(
             m[q] = __builtin_elementwise_fma(w0, a[q][i], m[q]);
             ls[q] = __builtin_elementwise_fma(w1, a[q][i], ls[q]);
         }
-    }
-#pragma unroll
-    for (int q = 0; q < kNP; ++q) {
-        m[q] += f2(Wo[2 * D]);
-        ls[q] += f2(Wo[2 * D + 1]);
     }
 #pragma unroll
     for (int n = 0; n < kNL; ++n) {

@@ -641,11 +641,16 @@ __global__ __launch_bounds__(kFThreads) __attribute__((amdgpu_waves_per_eu(fused
                 return Rec{{p[0], p[1], p[2], p[3]}};
             };
             // Scaled ReLU: the records hold w0, b0 x 2^-32 and w1 x 2^32 (stage_head), so the
-            // hidden pre-activation arrives as h 2^-32 -- every fma of the chain rounds exactly as
-            // the unscaled one (power-of-two scaling, far from the subnormal / overflow range) --
-            // and max(h, 0) is the last fma's clamp-to-[0, 1] modifier (h <= 2^32): no v_max_f32
-            // per pixel and unit (gfx950 has no packed f32 max; they were 1 in 6 of the head's
-            // VALU instructions).  w1 2^32 x (h 2^-32) = w1 h exactly.
+            // hidden pre-activation arrives as h 2^-32 and max(h, 0) is the last fma's
+            // clamp-to-[0, 1] modifier: no v_max_f32 per pixel and unit (gfx950 has no packed f32
+            // max; they were 1 in 6 of the head's VALU instructions).  w1 2^32 x (h 2^-32) = w1 h
+            // exactly.  A power-of-two scaling commutes with every rounding of the chain as long
+            // as no operand or partial sum leaves the normal range after scaling, so the result
+            // is bitwise the unscaled head's (CCMI_HEAD_GENERIC, test_forward.py's
+            // test_unrolled_head_bitwise_generic) only while every hidden weight, bias and
+            // partial pre-activation h has |h| >= 2^-94 or is 0, and h <= 2^32: a tinier value
+            // loses bits as a subnormal (its term is below 2^-94 |w1|), a larger positive h is
+            // clamped to 2^32.  Decoder weights and activations are far inside both limits.
             const f2 lo0 = f2(A.relu0 ? 0.f : -INFINITY); // the generic head's ReLU (max)
             auto unit = [&](const Rec &r) {
                 constexpr bool RELU = kScaledRelu;
@@ -909,7 +914,7 @@ template <int CMID, bool UPS>
 void launch_fused(dim3 grid, hipStream_t s, const FusedArgs &fa, const LevelArgs &u)
 {
     // the presets' 7-grid decoders with a 48-wide head (hop and its relatives): unrolled head
-    if (fa.cin == 7 && fa.n_head == 2 && fa.hid == 48 && fa.relu0) { // (its scaled ReLU assumes one)
+    if (fa.cin == 7 && fa.n_head == 2 && fa.hid == 48 && fa.relu0 && !fa.head_generic) { // (its scaled ReLU assumes one)
         hipLaunchKernelGGL((syn_fused_kernel<7, CMID, UPS, false, 48>), grid, dim3(kFThreads), 0, s, fa, u);
         return;
     }
@@ -1115,8 +1120,9 @@ extern "C" int ccmi_decode_forward_f32(const ccmi_decode_args *a, void *stream)
     P.fa.out_stride = a->out_stride;
     P.fa.qmax = a->bitdepth > 0 ? (float)((1 << a->bitdepth) - 1) : 0.f;
     P.fa.yuv420 = a->yuv420;
-    if (a->head < CCMI_HEAD_DEFAULT || a->head > CCMI_HEAD_MFMA) return ccmi_set_error(CCMI_ERR_ARG, "decode: head %d", a->head);
+    if (a->head < CCMI_HEAD_DEFAULT || a->head > CCMI_HEAD_GENERIC) return ccmi_set_error(CCMI_ERR_ARG, "decode: head %d", a->head);
     P.fa.head_mfma = a->head == CCMI_HEAD_MFMA;
+    P.fa.head_generic = a->head == CCMI_HEAD_GENERIC;
     const int halo = P.fa.n_sp;
     P.fa.tiles_x = ccmi_div_up(y.w, kRW - 2 * halo);
     dim3 grid(P.fa.tiles_x * ccmi_div_up(y.h, kRH - 2 * halo), y.batch);

@@ -179,9 +179,12 @@ typedef struct ccmi_decode_args {
     int head;               /* synthesis 1x1 head arithmetic, CCMI_HEAD_*: both are fp32 (the
                                MFMA form's products are exact f32 fmas, summed in another
                                order); MFMA needs 7 inputs, 48 hidden units and >= 1 3x3 layer
-                               and falls back to VALU otherwise */
+                               and falls back to VALU otherwise; GENERIC is a test form: the
+                               runtime-width VALU head without the unrolled 48-wide kernel's
+                               scaled ReLU (bitwise equal to VALU while every hidden
+                               pre-activation h has 2^-94 <= |h| <= 2^32 or h <= 0) */
 } ccmi_decode_args;
-enum { CCMI_HEAD_DEFAULT = 0, CCMI_HEAD_VALU = 1, CCMI_HEAD_MFMA = 2 };
+enum { CCMI_HEAD_DEFAULT = 0, CCMI_HEAD_VALU = 1, CCMI_HEAD_MFMA = 2, CCMI_HEAD_GENERIC = 3 };
 int ccmi_decode_forward_f32(const ccmi_decode_args *args, void *stream);
 
 /* ------------------------------------------------------------------------- */

@@ -275,6 +275,28 @@ def test_fused_decode_matches_reference_golden(path, head, gpu, ccmi_lib):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("path", [p for p in GOLDEN if "hop" in p.stem or "arm32" in p.stem], ids=lambda p: p.stem)
+def test_unrolled_head_bitwise_generic(path, gpu, ccmi_lib):
+    """The unrolled 48-wide head with its scaled ReLU (hidden weights x 2^-32, output weights
+    x 2^32, ReLU as the fma clamp; fwd_syn.hip unit()) against the runtime-width head without
+    the scaling (CCMI_HEAD_GENERIC), bit for bit, on the reference's 48-wide 7-grid decoder weights
+    and a 1080p random hop decoder (both heads sum in the same order)."""
+    import ccmi
+    z = np.load(path)
+    mp = fo.ModelParams.from_npz(z)
+    assert mp.layers[0][0] == 48 and mp.n_grids == 7  # the unrolled head's shape
+    for bd, yuv in ((0, False), (8, False), (10, True)):
+        a = _fused([mp], [_lat(z, mp)], gpu, bd, yuv, ccmi.HEAD_DEFAULT)
+        b = _fused([mp], [_lat(z, mp)], gpu, bd, yuv, ccmi.HEAD_GENERIC)
+        assert torch.equal(a, b)
+    mp = fo.ModelParams.random(1080, 1920, seed=31)
+    g = torch.Generator().manual_seed(31)
+    lat = [0.5 * torch.randn(h, w, generator=g) for h, w in mp.sizes]
+    assert torch.equal(_fused([mp], [lat], gpu, 0, False, ccmi.HEAD_DEFAULT),
+                       _fused([mp], [lat], gpu, 0, False, ccmi.HEAD_GENERIC))
+
+
+@pytest.mark.gpu
 @pytest.mark.parametrize("H,W,seed,layers", [
     (720, 1280, 1, None), (1080, 1920, 11, None), (37, 53, 2, None), (1, 1, 3, None), (2, 130, 4, None), (129, 3, 5, None),
     (1365, 2048, 12, None), (1725, 1145, 13, None),  # CLIC20-pro-valid geometries (config 5 content)
