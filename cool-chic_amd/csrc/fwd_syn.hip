@@ -9,13 +9,13 @@
 // Fast path (every architecture made of a 1x1 "MLP" head followed by 3x3 layers with
 // <= 4 channels -- all the reference presets: hop, mop, lop, ...): ONE fused kernel per
 // launch.  A workgroup owns a 32 x 64 pixel window.  Pass 0 evaluates the per-pixel MLP
-// (c_in -> hid -> c_mid, weights wave-uniform in SGPRs) on the whole window (output tile
-// plus a halo of one pixel per 3x3 layer) and keeps its c_mid outputs in LDS; each 3x3 layer then shrinks
-// the region by one pixel, ping-ponging between two LDS images; the last layer writes
-// to HBM.  Replicate padding is reproduced by evaluating halo pixels at the clamped
-// image coordinate (a pointwise head commutes with clamping; a 3x3 layer reads its
-// input at clamp(clamp(g) + d)).  HBM traffic: c_in planes read once (+ halo), c_out
-// planes written once.
+// (c_in -> hid -> c_mid, weights from LDS records) on the whole window (output tile plus a
+// halo of one pixel per 3x3 layer) and keeps its c_mid outputs in registers; each 3x3 layer
+// then shrinks the valid region by one pixel, in registers (the horizontal taps across lanes
+// by DPP, the vertical ones from the thread's own rows and its neighbours' edge rows through
+// LDS); the last layer writes to HBM.  Replicate padding is reproduced by evaluating halo
+// pixels at the clamped image coordinate.  HBM traffic: c_in planes read once (+ halo),
+// c_out planes written once.
 //
 // Any other architecture runs the generic per-layer kernel (one launch per layer,
 // ping-pong through the caller's workspace).
@@ -36,13 +36,11 @@ constexpr int kThreads = 256;
 // of one pixel per 3x3 layer.  All stages share the window's coordinate frame (pitch
 // 64); stage t is valid on rows/cols [t, 32-t) x [t, 64-t).  Thread (c = tid & 63,
 // g = tid >> 6) owns column c of the 4 consecutive rows 4g .. 4g+3 in every stage.
-//  * head: packed fp32 (v_pk_fma_f32) over pixel pairs, wave-uniform weights from
-//    SGPRs, hidden activations consumed as they are produced (never stored);
-//  * 3x3 layers: the thread slides a 3-row register window down its 4 rows, so a
-//    pixel costs 3*CMID LDS reads instead of 9*CMID.  Window row i maps to image row
-//    clamp(oy + i) (replicate padding); rows whose image row lies outside the image
-//    or outside the stage's valid band are computed but never read or stored, which
-//    keeps control flow uniform.
+//  * head: packed fp32 (v_pk_fma_f32) over pixel pairs, weight records broadcast from LDS,
+//    hidden activations consumed as they are produced (never stored);
+//  * 3x3 layers: in registers (see "3x3 layers, replicate padding" below).  Pixels outside
+//    the image or outside the stage's valid band are computed but never stored, which keeps
+//    control flow uniform.
 // window height (and threads per workgroup) overridable at build time for the window-size
 // A/B of DESIGN.md 7 (tools/ab_fused_window.sh); the product build uses 32 rows, 512 threads
 #ifndef CCMI_FUSED_RH
@@ -151,8 +149,9 @@ constexpr int fused_lds_floats(int cin, int cmid, bool ups)
     const int C = ups ? cin - 1 : 0, GC = (C + fused_groups(cin, ups) - 1) / fused_groups(cin, ups);
     const int raw = ups ? GC * kHsRows * kSW + kHrRows * kTW : 0;
     const int stage = ups ? GC * kHsRows * kRW + kHrRows * kRW : 0;
-    const int b0 = cmid * kPlane > raw ? cmid * kPlane : raw;
-    int b1 = cmid * kPlane > stage ? cmid * kPlane : stage;
+    const int xr = 2 * cmid * kFThreads; // a 3x3 layer's halo-row exchange buffer
+    const int b0 = xr > raw ? xr : raw;
+    int b1 = xr > stage ? xr : stage;
     b1 = b1 > kMaxHid * 16 + 256 ? b1 : kMaxHid * 16 + 256; // head records (+ the MFMA head's weight table)
     return b0 + b1 + 256; // + the 8-bit quotient table
 }
@@ -176,21 +175,18 @@ __global__ __launch_bounds__(kFThreads) __attribute__((amdgpu_waves_per_eu(fused
 {
     constexpr int NR = kRowsPerThread;
     constexpr int C = UPS ? CIN - 1 : 0, NG = fused_groups(CIN, UPS), GC = (C + NG - 1) / NG;
-    // region 0: raw input tiles of a channel group (UPS, phases A-B), then the head output /
-    // 3x3 buffer 0; region 1: the group's horizontal-pass results (UPS), then the head's
-    // weight records, then the 3x3 buffer 1
+    // region 0: raw input tiles of a channel group (UPS, phases A-B), then the 3x3 layers'
+    // halo-row buffer 0; region 1: the group's horizontal-pass results (UPS), then the head's
+    // weight records, then the halo-row buffer 1
     constexpr int kRaw = UPS ? GC * kHsRows * kSW + kHrRows * kTW : 0;
-    constexpr int kBuf0 = CMID * kPlane > kRaw ? CMID * kPlane : kRaw;
+    constexpr int kBuf0 = 2 * CMID * kFThreads > kRaw ? 2 * CMID * kFThreads : kRaw;
     constexpr int kTot = fused_lds_floats(CIN, CMID, UPS);
     __shared__ __attribute__((aligned(16))) float s_pool[kTot];
-    float(*s_buf0)[kPlane] = reinterpret_cast<float(*)[kPlane]>(s_pool);
-    float(*s_buf1)[kPlane] = reinterpret_cast<float(*)[kPlane]>(s_pool + kBuf0);
     float *s_st = s_pool;                      // [GC][kHsRows][kSW] raw source tile (UPS only)
     float *s_yt = s_st + GC * kHsRows * kSW;   // [kHrRows][kTW] raw latent tile (UPS only)
     float *s_hs = s_pool + kBuf0;              // [GC][kHsRows][kRW]   (UPS only)
     float *s_hr = s_hs + GC * kHsRows * kRW;   // [kHrRows][kRW]       (UPS only)
     float *s_lut8 = s_pool + kTot - 256;
-    auto buf = [&](int which) { return which ? s_buf1 : s_buf0; };
 #if defined(CCMI_ARM_STAMPS)
     unsigned long long t_prev = __builtin_amdgcn_s_memtime();
 #endif
@@ -223,7 +219,6 @@ __global__ __launch_bounds__(kFThreads) __attribute__((amdgpu_waves_per_eu(fused
     int rb = (threadIdx.x >> 6) * NR; // first window row of this thread
     int gx = ox + c;
     int cxg = clampi(gx, A.W - 1);
-    int lx[3]; // 3x3 stage: window columns of the clamped horizontal neighbours
     auto reidx = [&]() {
         int t = threadIdx.x;
         asm volatile("" : "+v"(t)); // an opaque copy: the compiler cannot reuse the old values
@@ -231,8 +226,6 @@ __global__ __launch_bounds__(kFThreads) __attribute__((amdgpu_waves_per_eu(fused
         rb = (t >> 6) * NR;
         gx = ox + c;
         cxg = clampi(gx, A.W - 1);
-#pragma unroll
-        for (int d = 0; d < 3; ++d) lx[d] = clampi(cxg + d - 1, A.W - 1) - ox;
     };
 
     const float *lut8 = A.qmax == 255.f ? s_lut8 : nullptr;
@@ -240,16 +233,16 @@ __global__ __launch_bounds__(kFThreads) __attribute__((amdgpu_waves_per_eu(fused
     // head's weight records (region 1: before anything else without fused upsampling, after
     // the gathers with it)
     if (lut8) s_lut8[threadIdx.x & 255] = (float)(threadIdx.x & 255) / 255.f;
-    // the records are fetched right where they are staged (L2-resident: every workgroup of a
-    // frame reads the same ones); holding them in registers across the upsampling phases
-    // cost spill slots at the 80-VGPR budget
+    // the records (L2-resident: every workgroup of a frame reads the same ones) are fetched
+    // into two registers before the last upsampling group, so their latency hides behind its
+    // passes, and staged once region 1 is free
     constexpr int kHeadRegs = (kMaxHid * 16 + kFThreads - 1) / kFThreads;
     // scaled ReLU for the unrolled VALU head (HID > 0, !MH; launched only with a first-layer ReLU)
     constexpr bool kScaledRelu = HID > 0 && !MH;
     constexpr float kW0Scale = kScaledRelu ? 0x1p-32f : 1.f, kW1Scale = kScaledRelu ? 0x1p32f : 1.f;
-    auto stage_head = [&]() {
+    float hv[kHeadRegs];
+    auto load_head = [&]() {
         const int tid = threadIdx.x;
-        float hv[kHeadRegs];
 #pragma unroll
         for (int k = 0; k < kHeadRegs; ++k) {
             const int i = tid + k * kFThreads, j = i >> 4, f = i & 15;
@@ -263,6 +256,9 @@ __global__ __launch_bounds__(kFThreads) __attribute__((amdgpu_waves_per_eu(fused
             }
             hv[k] = v;
         }
+    };
+    auto stage_head = [&]() {
+        const int tid = threadIdx.x;
 #pragma unroll
         for (int k = 0; k < kHeadRegs; ++k) {
             const int i = tid + k * kFThreads, j = i >> 4, f = i & 15;
@@ -281,6 +277,7 @@ __global__ __launch_bounds__(kFThreads) __attribute__((amdgpu_waves_per_eu(fused
         }
     };
     if constexpr (!UPS) {
+        load_head();
         stage_head();
         __syncthreads();
     }
@@ -516,8 +513,14 @@ __global__ __launch_bounds__(kFThreads) __attribute__((amdgpu_waves_per_eu(fused
                 }
             }
         };
-        group(std::integral_constant<int, 0>{});
-        if constexpr (NG > 1) group(std::integral_constant<int, 1>{});
+        if constexpr (NG > 1) {
+            group(std::integral_constant<int, 0>{});
+            load_head(); // in flight behind the last group's passes
+            group(std::integral_constant<int, 1>{});
+        } else {
+            load_head();
+            group(std::integral_constant<int, 0>{});
+        }
     } else {
 #pragma unroll
         for (int p = 0; p < NR; ++p) {
@@ -527,6 +530,8 @@ __global__ __launch_bounds__(kFThreads) __attribute__((amdgpu_waves_per_eu(fused
         }
     }
 
+    // the current stage's image at this thread's 4 rows: row pairs (rb, rb+1), (rb+2, rb+3)
+    f2 img[NR / 2][CMID];
     // ------------------------ pass 0: per-pixel 1x1 head ------------------------
     {
         const cfloat_ptr w0 = prm + A.w0_off, b0 = prm + A.b0_off;
@@ -725,95 +730,165 @@ __global__ __launch_bounds__(kFThreads) __attribute__((amdgpu_waves_per_eu(fused
             return;
         }
 #pragma unroll
-        for (int p = 0; p < NR; ++p)
+        for (int q = 0; q < NR / 2; ++q)
 #pragma unroll
-            for (int m = 0; m < CMID; ++m) s_buf0[m][(rb + p + 1) * kRW + c] = o[p][m];
+            for (int m = 0; m < CMID; ++m) img[q][m] = f2{o[2 * q][m], o[2 * q + 1][m]};
     }
 
     // ------------------------ 3x3 layers, replicate padding ------------------------
-    // Every LDS image is kept "pre-clamped" along rows: a window row outside the image
-    // holds the value of the nearest image row wherever it can be read.  The head computes
-    // all window rows at clamped coordinates; a 3x3 layer stores its in-image rows and the
-    // edge rows again one row further out (the only out-of-image rows an in-image output
-    // reads).  So the vertical neighbours of window row r are simply rows r-1, r+1, and a
-    // thread reads row pairs {r, r+1} straight into packed registers.  Columns are lanes:
-    // the horizontal neighbours use clamped columns lx[].  Each layer and the store pass
-    // re-derive the lane indices (reidx) instead of holding them across the layers.
-    // windows whose rows all lie strictly inside the image write no replicate rows
-    const bool inner = oy > 0 && oy + kRH < A.H;
-    // one 3x3 layer from buf(cur) into buf(cur ^ 1); the last one also lands in LDS (each
-    // thread at its own pixels) and the stores to HBM follow in their own pass, so the FMA
-    // loop carries no output-format branches
-    auto layer = [&](auto LAST, int s, int cur) {
+    // Register form: a stage's image stays in the registers of the thread that computed it
+    // (lane = window column, the thread's 4 rows); only each thread's first and last row go
+    // through LDS, for the threads above and below (one wave each: a wave is 4 whole window
+    // rows).  The horizontal taps never touch LDS: for output channel m the thread forms the
+    // three column partial sums S_dx = sum_{k,dy} w[m][k][dy][dx] x_k(row + dy - 1) of its own
+    // column, and out(c) = S_1(c) + S_0(c - 1) + S_2(c + 1), the neighbours' sums read across
+    // lanes by DPP (v_add_f32 wave_shr:1 / wave_shl:1).  (The LDS form read 3 x 3 x CMID
+    // neighbours per pixel from an LDS image and was LDS-bandwidth bound: 120 ds_read per
+    // thread and layer.)  Replicate padding: every stage is evaluated at all window pixels,
+    // and a value outside the image stands for the nearest image pixel --
+    //  * rows (wave-uniform): a thread reading rows rb-1 .. rb+4 replaces those outside the
+    //    image by the nearest in-image row among them (the only rows an in-image output
+    //    reads: the edge row itself is the thread's own or its neighbour's);
+    //  * columns: the head is evaluated at clamped columns, and each 3x3 layer's output at
+    //    lanes outside the image is replaced by the edge lane's (v_readlane), so the next
+    //    layer's column sums there are the edge column's.
+    // Window rows 0 / kRH-1 and columns 0 / kRW-1 read garbage neighbours (other window or
+    // DPP zero fill); they are outside every later stage's valid band [t, kRW - t).
+    // Halo rows exchange buffers, double-buffered by layer parity: [top, bottom][CMID][thread].
+    float *xb0 = s_pool, *xb1 = s_pool + kBuf0;
+    auto publish = [&](float *xb) __attribute__((always_inline)) {
+        const int tid = threadIdx.x;
+#pragma unroll
+        for (int m = 0; m < CMID; ++m) {
+            xb[m * kFThreads + tid] = img[0][m].x;                      // row rb
+            xb[(CMID + m) * kFThreads + tid] = img[NR / 2 - 1][m].y;   // row rb + 3
+        }
+    };
+    auto shr1 = [](float v) __attribute__((always_inline)) { // lane c <- lane c - 1 (0 at lane 0)
+        return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x138, 0xf, 0xf, true));
+    };
+    auto shl1 = [](float v) __attribute__((always_inline)) { // lane c <- lane c + 1 (0 at lane 63)
+        return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x130, 0xf, 0xf, true));
+    };
+    const bool rows_inner = oy > 0 && oy + kRH < A.H;          // rows -1 .. kRH all in the image
+    const bool cols_inner = ox >= 0 && ox + kRW <= A.W;        // every lane an image column
+    // one 3x3 layer: img (stage s input) -> img (stage s output); the non-last layers publish
+    // their output's halo rows into xout
+    auto layer = [&](auto LAST, int s, const float *xin, float *xout) __attribute__((always_inline)) {
         constexpr bool last = decltype(LAST)::value;
-        __syncthreads();
-        reidx();
+        __syncthreads(); // xin published by every wave (and the previous reads of xout done)
         const cfloat_ptr wt = prm + A.sp[s].w_off;
         const cfloat_ptr bs = prm + A.sp[s].b_off;
         const f2 lo = f2(A.sp[s].relu ? 0.f : -INFINITY);
         const f2 rsd = f2(A.sp[s].residual ? 1.f : 0.f);
-        // plane row of window row (rb - 1) in this thread's column
-        const float *src = &buf(cur)[0][0] + rb * kRW + c;
-        float *dst = &buf(cur ^ 1)[0][0] + (rb + 1) * kRW + c;
+        const int tid = threadIdx.x;
+        const int wrow = __builtin_amdgcn_readfirstlane(tid >> 6) * NR; // rb, wave-uniform
+        const int tup = wrow > 0 ? tid - 64 : tid, tdn = wrow + NR < kRH ? tid + 64 : tid;
+        // rows rb-1 .. rb+4 of every input channel
+        float v[NR + 2][CMID];
 #pragma unroll
-        for (int q = 0; q < NR / 2; ++q) {
-            // output rows rb + 2q, rb + 2q + 1 read window rows rb + 2q - 1 .. rb + 2q + 2
-            f2 P[3][CMID][3]; // P[dy] = {row rb+2q-1+dy, row rb+2q+dy}
+        for (int m = 0; m < CMID; ++m) {
+            v[0][m] = xin[(CMID + m) * kFThreads + tup];
+            v[NR + 1][m] = xin[m * kFThreads + tdn];
 #pragma unroll
-            for (int dy = 0; dy < 3; ++dy)
+            for (int p = 0; p < NR; ++p) v[p + 1][m] = (p & 1) ? img[p / 2][m].y : img[p / 2][m].x;
+        }
+        if (!rows_inner) {
+            const int gy0 = oy + wrow - 1; // image row of v[0]
 #pragma unroll
-                for (int k = 0; k < CMID; ++k)
+            for (int i = 1; i < NR + 2; ++i)
+                if (gy0 + i >= A.H)
 #pragma unroll
-                    for (int d = 0; d < 3; ++d) {
-                        const float *e = src + k * kPlane + (2 * q + dy) * kRW + (lx[d] - c);
-                        P[dy][k][d] = f2{e[0], e[kRW]};
+                    for (int m = 0; m < CMID; ++m) v[i][m] = v[i - 1][m];
+#pragma unroll
+            for (int i = NR; i >= 0; --i)
+                if (gy0 + i < 0)
+#pragma unroll
+                    for (int m = 0; m < CMID; ++m) v[i][m] = v[i + 1][m];
+        }
+        // packed row pairs: P[r][k] = {row rb - 1 + r, row rb + r}, r = 0 .. NR
+        f2 P[NR + 1][CMID];
+#pragma unroll
+        for (int r = 0; r <= NR; ++r)
+#pragma unroll
+            for (int k = 0; k < CMID; ++k) P[r][k] = f2{v[r][k], v[r + 1][k]};
+        // the weights are wave-uniform scalar loads; the output channel loop is unrolled (the
+        // outputs stay in registers, which a runtime channel index would send to scratch)
+        f2 nxt[NR / 2][CMID];
+#pragma unroll
+        for (int m = 0; m < CMID; ++m) {
+            const cfloat_ptr wm = wt + m * CMID * 9;
+            f2 S[3][NR / 2];
+#pragma unroll
+            for (int q = 0; q < NR / 2; ++q) {
+                S[0][q] = f2(0.f);
+                S[1][q] = f2(bs[m]);
+                S[2][q] = f2(0.f);
+            }
+#pragma unroll
+            for (int k = 0; k < CMID; ++k)
+#pragma unroll
+                for (int dy = 0; dy < 3; ++dy)
+#pragma unroll
+                    for (int dx = 0; dx < 3; ++dx) {
+                        const f2 w = f2(wm[(k * 3 + dy) * 3 + dx]);
+#pragma unroll
+                        for (int q = 0; q < NR / 2; ++q) S[dx][q] = __builtin_elementwise_fma(w, P[2 * q + dy][k], S[dx][q]);
                     }
-            // one output channel per iteration (not unrolled): its CMID*9 weights + bias are
-            // wave-uniform scalar loads, so the 3x3 stage spends no LDS bandwidth on weights
-#pragma unroll 1
-            for (int m = 0; m < CMID; ++m) {
-                const cfloat_ptr wm = wt + m * CMID * 9;
-                f2 acc = f2(bs[m]);
 #pragma unroll
-                for (int k = 0; k < CMID; ++k)
-#pragma unroll
-                    for (int dy = 0; dy < 3; ++dy)
-#pragma unroll
-                        for (int dx = 0; dx < 3; ++dx)
-                            acc = __builtin_elementwise_fma(f2(wm[(k * 3 + dy) * 3 + dx]), P[dy][k][dx], acc);
-                // residual: the input at the centre, re-read from LDS (a runtime-indexed
-                // register select would cost a VALU chain per channel)
-                const float *e = src + m * kPlane + (2 * q + 1) * kRW + (lx[1] - c);
-                acc = __builtin_elementwise_max(__builtin_elementwise_fma(rsd, f2{e[0], e[kRW]}, acc), lo);
-                float *d = dst + m * kPlane + 2 * q * kRW;
-                if (last || inner) {
-                    d[0] = acc.x;
-                    d[kRW] = acc.y;
-                } else {
-#pragma unroll
-                    for (int h = 0; h < 2; ++h) {
-                        const int gy = oy + rb + 2 * q + h;
-                        const float v = h ? acc.y : acc.x;
-                        if (gy >= 0 && gy < A.H) {
-                            d[h * kRW] = v;
-                            if (gy == 0) d[(h - 1) * kRW] = v;     // replicate above the image
-                            if (gy == A.H - 1) d[(h + 1) * kRW] = v; // and below it
-                        }
-                    }
-                }
+            for (int q = 0; q < NR / 2; ++q) {
+                f2 acc;
+                acc.x = (S[1][q].x + shr1(S[0][q].x)) + shl1(S[2][q].x);
+                acc.y = (S[1][q].y + shr1(S[0][q].y)) + shl1(S[2][q].y);
+                // residual: the input at the centre (row pair 2q + 1 = rows rb + 2q, rb + 2q + 1)
+                nxt[q][m] = __builtin_elementwise_max(__builtin_elementwise_fma(rsd, P[2 * q + 1][m], acc), lo);
             }
         }
+#pragma unroll
+        for (int q = 0; q < NR / 2; ++q)
+#pragma unroll
+            for (int m = 0; m < CMID; ++m) img[q][m] = nxt[q][m];
+        if constexpr (!last) {
+            if (!cols_inner) {
+                // lanes left / right of the image take the edge column's value
+                const int c0 = -ox, c1 = A.W - 1 - ox; // lanes of image columns 0, W-1
+                const int lane = tid & 63;
+#pragma unroll
+                for (int q = 0; q < NR / 2; ++q)
+#pragma unroll
+                    for (int m = 0; m < CMID; ++m) {
+                        float e0 = img[q][m].x, e1 = img[q][m].y;
+                        if (c0 > 0) {
+                            const float l0 = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(e0), c0));
+                            const float l1 = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(e1), c0));
+                            e0 = lane < c0 ? l0 : e0;
+                            e1 = lane < c0 ? l1 : e1;
+                        }
+                        if (c1 < kRW - 1) {
+                            const float r0 = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(e0), c1));
+                            const float r1 = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(e1), c1));
+                            e0 = lane > c1 ? r0 : e0;
+                            e1 = lane > c1 ? r1 : e1;
+                        }
+                        img[q][m] = f2{e0, e1};
+                    }
+            }
+            publish(xout);
+        }
     };
-    int cur = 0;
-    for (int s = 0; s < A.n_sp - 1; ++s, cur ^= 1) layer(std::false_type{}, s, cur);
-    layer(std::true_type{}, A.n_sp - 1, cur);
-    cur ^= 1;
-    // stores: this thread's own pixels of the last layer, back from LDS (program order, no
-    // barrier), one branch-free loop per output format
+    publish(xb0);
+    for (int s = 0; s < A.n_sp - 1; ++s) {
+        layer(std::false_type{}, s, xb0, xb1);
+        float *const t = xb0;
+        xb0 = xb1;
+        xb1 = t;
+    }
+    layer(std::true_type{}, A.n_sp - 1, xb0, nullptr);
+    // stores: this thread's own pixels of the last layer, from registers, one branch-free loop
+    // per output format
     {
         reidx();
         const int t = A.n_sp;
-        const float *fin = &buf(cur)[0][0] + (rb + 1) * kRW + c;
         const bool col_ok = c >= t && c < kRW - t && gx < A.W;
         const uint32_t pl = (uint32_t)plane;
         const uint32_t cw = (uint32_t)(A.W >> 1), cp = (uint32_t)((A.H >> 1) * (A.W >> 1));
@@ -832,7 +907,7 @@ __global__ __launch_bounds__(kFThreads) __attribute__((amdgpu_waves_per_eu(fused
 #pragma unroll
                 for (int m = 0; m < CMID; ++m) {
                     if (fmt == 2 && m > 0 && (gy & 1)) break; // 420: odd rows carry no chroma (wave-uniform)
-                    float v = fin[m * kPlane + p * kRW];
+                    float v = (p & 1) ? img[p / 2][m].y : img[p / 2][m].x;
                     if constexpr (fmt > 0) {
                         v = tab ? lut8[(int)fminf(fmaxf(rintf(v * 255.f), 0.f), 255.f)]
                                 : fminf(fmaxf(rintf(v * A.qmax) / A.qmax, 0.f), 1.f);

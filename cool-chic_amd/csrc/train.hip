@@ -1581,23 +1581,29 @@ __global__ __launch_bounds__(kHeadT) void t_head_bwd(const float *__restrict__ d
 }
 
 // Tiled form (the one launched): the hidden layer stays in registers (pairs of units, packed
-// FMAs, as the PAIR form), and the LDS rows that feed the weight-gradient MFMAs hold ONE
-// 16-unit tile at a time (pitch 17) next to a per-pixel row gp | 0 | x | 1 | 0 shared by both
-// MFMA loops: 7.7 KB of LDS per wave instead of 14.8 KB (LDS had capped the full-width form at
-// 2.5 waves / SIMD with 55 % of its wave cycles in WAIT_ANY; profiles/r4w_train_pmc.txt).
-// Per tile q: h rows -> dW1 tile (M = k < 3, N = the tile's units) -> g_h rows (the ReLU mask
-// from the registers) -> dW0 tile (M = the tile's units, N = i <= CIN) and this pixel's g_x.
+// FMAs, as the PAIR form), and the LDS that feeds the weight-gradient MFMAs holds ONE 16-unit
+// tile at a time next to the pixel fields gp | 0 | x | 1 shared by both MFMA loops: 8.2 KB of
+// LDS per wave instead of 14.8 KB (LDS had capped the full-width form at 2.5 waves / SIMD with
+// 55 % of its wave cycles in WAIT_ANY; profiles/r4w_train_pmc.txt).  Both are stored
+// pixel-minor -- one row of the wave's 64 pixels per unit / field, pitch 68 -- so a lane's
+// writes are consecutive across the wave and an MFMA loop reads its operands for four K-steps
+// (4 pixels) with one 128-bit read each (the 16 lanes of a read start 4 banks apart).
+// Per tile q: h -> dW1 tile (M = k < 3, N = the tile's units) -> g_h (the ReLU mask from the
+// registers) -> dW0 tile (M = the tile's units, N = i <= CIN) and this pixel's g_x.
 // The output layer must be linear (g.r1 == 0, every reference architecture's "X-1-linear-none"):
 // then g_out needs no pass over all units first, and a tile's units are computed just in time.
+constexpr int kHbXP = 68;
+constexpr int head_bwd_t_wave_floats(int cin) { return (16 + 4 + cin + 1) * kHbXP; }
+
 template <int CIN, int NT>
 __global__ __launch_bounds__(kHeadT, 4) void t_head_bwd_t(const float *__restrict__ dense, const float *__restrict__ gz0,
                                                        Geo g, const float *__restrict__ th, int64_t ps,
                                                        float *__restrict__ gdense, float *__restrict__ gth, int64_t gstride)
 {
     extern __shared__ float s_dyn[];
-    constexpr int kTP = 17;            // tile row pitch: 16 units + 1 (odd: conflict-free row writes)
-    constexpr int kSW = (CIN + 6) | 1; // pixel row: gp[0..3) | 0 | x[0..CIN) | 1 | 0, odd pitch
-    constexpr int kGX = 4;             // first x column
+    constexpr int kXP = kHbXP;         // row pitch (64 pixels + 4)
+    constexpr int kGX = 4;             // first x row
+    constexpr int kWF = head_bwd_t_wave_floats(CIN);
     __shared__ __attribute__((aligned(16))) float s_rec[16 * NT][12];
     static_assert(CIN + 4 <= 12, "hidden-unit record");
     constexpr int kPR = 2 * (CIN + 4) <= 24 ? 24 : 32;
@@ -1619,10 +1625,15 @@ __global__ __launch_bounds__(kHeadT, 4) void t_head_bwd_t(const float *__restric
         }
         s_rec2[jp][r] = v;
     }
-    const float bo0 = P[g.b1], bo1 = P[g.b1 + 1], bo2 = P[g.b1 + 2];
-    float *sv = s_dyn + w * 64 * (kTP + kSW), *sw = sv + 64 * kTP;
+    // sv: [16 units][64 px] (the tile's h, then its g_h); sw: [field][64 px]
+    float *sv = s_dyn + w * kWF, *sw = sv + 16 * kXP;
     const int ln = lane & 15, lk = lane >> 4;
-    const int ia = ln < 3 ? ln : 3, ib = kGX + (ln <= CIN ? ln : CIN + 1); // operand columns (pads read 0)
+    // operand rows: gp k (ln >= 3: the zero row 3), x i | 1 (ln > CIN: the zero row 3)
+    const int ia = ln < 3 ? ln : 3, ib = ln <= CIN ? kGX + ln : 3;
+    // constant rows: 0 (row 3), 1 (row kGX + CIN), written once
+    sw[3 * kXP + lane] = 0.f;
+    sw[(kGX + CIN) * kXP + lane] = 1.f;
+    typedef float v4 __attribute__((ext_vector_type(4)));
     v4f a1[NT], a0[NT];
 #pragma unroll
     for (int q = 0; q < NT; ++q) a1[q] = a0[q] = v4f{0.f, 0.f, 0.f, 0.f};
@@ -1654,14 +1665,11 @@ __global__ __launch_bounds__(kHeadT, 4) void t_head_bwd_t(const float *__restric
         if (ch + gridDim.x < nchunk) load_chunk(ch + gridDim.x);
 #pragma unroll
         for (int k = 0; k < 3; ++k) db1[k] += gp1[k];
-        // ---- this pixel's row: gp | 0 | x | 1 | 0 (invalid pixels: gp = 0, x = 0)
+        // ---- this pixel's column: gp, x (invalid pixels: gp = 0, x = 0)
 #pragma unroll
-        for (int k = 0; k < 3; ++k) sw[lane * kSW + k] = gp1[k];
-        sw[lane * kSW + 3] = 0.f;
+        for (int k = 0; k < 3; ++k) sw[k * kXP + lane] = gp1[k];
 #pragma unroll
-        for (int i = 0; i < CIN; ++i) sw[lane * kSW + kGX + i] = xv[i];
-        sw[lane * kSW + kGX + CIN] = 1.f;
-        sw[lane * kSW + kGX + CIN + 1] = 0.f;
+        for (int i = 0; i < CIN; ++i) sw[(kGX + i) * kXP + lane] = xv[i];
         f2 gxp[CIN];
 #pragma unroll
         for (int i = 0; i < CIN; ++i) gxp[i] = f2(0.f);
@@ -1672,7 +1680,7 @@ __global__ __launch_bounds__(kHeadT, 4) void t_head_bwd_t(const float *__restric
             int roff = 0;
             asm volatile("" : "+s"(roff));
             const float(*rec)[kPR] = s_rec2 + 8 * q + roff;
-            float *row = sv + lane * kTP;
+            float *col = sv + lane; // unit u of this pixel at col[u * kXP]
             // ---- the tile's hidden units h (pairs, packed FMAs) -> this lane's row; only the
             // ReLU mask stays in a register (bit 2u + parity)
             uint32_t hmask = 0;
@@ -1683,17 +1691,19 @@ __global__ __launch_bounds__(kHeadT, 4) void t_head_bwd_t(const float *__restric
 #pragma unroll
                 for (int i = 0; i < CIN; ++i) a = __builtin_elementwise_fma(r[i], f2(xv[i]), a);
                 a = __builtin_elementwise_max(a, lo0);
-                row[2 * u] = a.x;
-                row[2 * u + 1] = a.y;
+                col[(2 * u) * kXP] = a.x;
+                col[(2 * u + 1) * kXP] = a.y;
                 hmask |= ((a.x > 0.f ? 1u : 0u) | (a.y > 0.f ? 2u : 0u)) << (2 * u);
             }
             wave_lds_sync();
-            // ---- dW1 tile q += gp^T h; K = pixels px = s + 16 (lane >> 4): the two 16-lane groups
-            // of each 32-lane half read rows 16 apart, 16 banks apart (odd pitches)
+            // ---- dW1 tile q += gp^T h; K = pixels px = s + 16 (lane >> 4), four MFMAs per pair of
+            // 128-bit reads
 #pragma unroll
-            for (int s = 0; s < 16; ++s) {
-                const int px = s + 16 * lk;
-                a1[q] = mfma4(sw[px * kSW + ia], sv[px * kTP + ln], a1[q]);
+            for (int s = 0; s < 16; s += 4) {
+                const v4 av = *reinterpret_cast<const v4 *>(sw + ia * kXP + 16 * lk + s);
+                const v4 bv = *reinterpret_cast<const v4 *>(sv + ln * kXP + 16 * lk + s);
+#pragma unroll
+                for (int e = 0; e < 4; ++e) a1[q] = mfma4(av[e], bv[e], a1[q]);
             }
             wave_lds_sync(); // every lane has read the h rows before g_h replaces them
             // ---- g_h of the tile (replaces h in this lane's row) and g_x
@@ -1706,17 +1716,19 @@ __global__ __launch_bounds__(kHeadT, 4) void t_head_bwd_t(const float *__restric
                 gh = __builtin_elementwise_fma(r[CIN + 3], f2(gp1[2]), gh);
                 gh.x = (keep >> (2 * u)) & 1u ? gh.x : 0.f; // selects, not exec-mask branches
                 gh.y = (keep >> (2 * u + 1)) & 1u ? gh.y : 0.f;
-                row[2 * u] = gh.x;
-                row[2 * u + 1] = gh.y;
+                col[(2 * u) * kXP] = gh.x;
+                col[(2 * u + 1) * kXP] = gh.y;
 #pragma unroll
                 for (int i = 0; i < CIN; ++i) gxp[i] = __builtin_elementwise_fma(r[i], gh, gxp[i]);
             }
             wave_lds_sync();
             // ---- dW0 | db0 tile q += g_h^T [x | 1]
 #pragma unroll
-            for (int s = 0; s < 16; ++s) {
-                const int px = s + 16 * lk;
-                a0[q] = mfma4(sv[px * kTP + ln], sw[px * kSW + ib], a0[q]);
+            for (int s = 0; s < 16; s += 4) {
+                const v4 av = *reinterpret_cast<const v4 *>(sv + ln * kXP + 16 * lk + s);
+                const v4 bv = *reinterpret_cast<const v4 *>(sw + ib * kXP + 16 * lk + s);
+#pragma unroll
+                for (int e = 0; e < 4; ++e) a0[q] = mfma4(av[e], bv[e], a0[q]);
             }
             wave_lds_sync(); // before the next tile's h (or the next chunk's rows) overwrite these
         }
@@ -1728,8 +1740,8 @@ __global__ __launch_bounds__(kHeadT, 4) void t_head_bwd_t(const float *__restric
     }
     // ---- flush (t_head_bwd's): the waves' partial rows meet in LDS, one atomic per value
     const int nred = hid * (CIN + 4) + 3;
-    float *red = s_dyn + w * 64 * (kTP + kSW);
-    static_assert(64 * (kTP + kSW) >= 16 * NT * (CIN + 4) + 3, "a wave's partial row fits its LDS rows");
+    float *red = s_dyn + w * kWF;
+    static_assert(kWF >= 16 * NT * (CIN + 4) + 3, "a wave's partial row fits its LDS rows");
     __syncthreads();
 #pragma unroll
     for (int q = 0; q < NT; ++q) {
@@ -1758,7 +1770,7 @@ __global__ __launch_bounds__(kHeadT, 4) void t_head_bwd_t(const float *__restric
     for (int e = t; e < nred; e += kHeadT) {
         float v = 0.f;
 #pragma unroll
-        for (int ww = 0; ww < kW; ++ww) v += s_dyn[ww * 64 * (kTP + kSW) + e];
+        for (int ww = 0; ww < kW; ++ww) v += s_dyn[ww * kWF + e];
         const int dst = e < hid * CIN ? g.w0 + e
                         : e < hid * (CIN + 1) ? g.b0 + (e - hid * CIN)
                         : e < hid * (CIN + 4) ? g.w1 + (e - hid * (CIN + 1))
@@ -2612,7 +2624,7 @@ void launch_head(bool bwd, dim3 grid, hipStream_t s, const float *dense, const f
         const bool tiled = !g.r1;
 #endif
         constexpr int kXP = (CIN + 2 > 5 ? CIN + 2 : 5) | 1; // t_head_bwd's per-wave LDS rows
-        const size_t lds = tiled ? sizeof(float) * (kHeadT / 64) * 64 * (17 + ((CIN + 6) | 1))
+        const size_t lds = tiled ? sizeof(float) * (kHeadT / 64) * head_bwd_t_wave_floats(CIN)
                                  : sizeof(float) * (kHeadT / 64) * 64 * (16 * ((g.hid + 15) / 16) + 1 + kXP);
         // one resident round over the pixel chunks (full-width form LDS-bound: 5 workgroups per CU
         // at 32,000 B each, 276 us; at exactly 32 KB the query also allowed 5, but they did not all
