@@ -985,11 +985,13 @@ __global__ void t_colsum(const float *__restrict__ part, int nrows, int ncols, f
 }
 
 // ------------------------------------------------------------------ synthesis
-// Two pixels per thread (p and p + kT of the workgroup's 2 kT) on packed FMAs: each broadcast
-// weight record serves both, halving the LDS record traffic per pixel (the one-pixel form
-// sat 56 % of its wave cycles in SQ_WAIT_INST_LDS).  Record slots 3, 7, 11 stay empty when
-// the fields fit without them (the compiler copies a broadcast operand out of the last dword
-// of a ds_read_b128 first), as in the path-A fused kernel.
+// Four pixels per thread (p + u kT of the workgroup's 4 kT, u = 0..3, as two packed pairs):
+// each broadcast weight record serves four pixels, a quarter of the one-pixel form's LDS record
+// traffic per pixel (that form sat 56 % of its wave cycles in SQ_WAIT_INST_LDS, the two-pixel
+// form still 55 %, profiles/r5d_train_pmc.txt).  Record slots 3, 7, 11 stay empty when the
+// fields fit without them (the compiler copies a broadcast operand out of the last dword of a
+// ds_read_b128 first), as in the path-A fused kernel.
+constexpr int kHeadFwdPx = 4 * kT; // pixels per workgroup
 template <int CIN>
 __global__ __launch_bounds__(kT) void t_head_fwd(const float *__restrict__ dense, Geo g, const float *__restrict__ th,
                                                  int64_t ps, float *__restrict__ z0)
@@ -1011,41 +1013,47 @@ __global__ __launch_bounds__(kT) void t_head_fwd(const float *__restrict__ dense
         }
         if (f <= CIN + 3) s_rec[j][hr(f)] = v;
     }
-    __syncthreads();
-    const int64_t npx = (int64_t)g.H * g.W, p0 = (int64_t)blockIdx.x * 2 * kT + threadIdx.x, p1 = p0 + kT;
-    if (p0 >= npx) return;
-    const bool v1 = p1 < npx;
+    const int64_t npx = (int64_t)g.H * g.W, p0 = (int64_t)blockIdx.x * kHeadFwdPx + threadIdx.x;
     const float *x = dense + (int64_t)b * CIN * npx;
-    f2 xv[CIN];
+    // pair q = pixels p0 + 2q kT, p0 + (2q + 1) kT (zeros past the frame)
+    f2 xv[2][CIN];
 #pragma unroll
-    for (int i = 0; i < CIN; ++i) xv[i] = f2{x[i * npx + p0], v1 ? x[i * npx + p1] : 0.f};
+    for (int q = 0; q < 2; ++q) {
+        const int64_t pa = p0 + 2 * q * kT, pb = pa + kT;
+#pragma unroll
+        for (int i = 0; i < CIN; ++i) xv[q][i] = f2{pa < npx ? x[i * npx + pa] : 0.f, pb < npx ? x[i * npx + pb] : 0.f};
+    }
+    __syncthreads();
     const f2 lo0 = f2(g.r0 ? 0.f : -INFINITY);
-    f2 o0 = f2(P[g.b1]), o1 = f2(P[g.b1 + 1]), o2 = f2(P[g.b1 + 2]);
+    f2 o[2][3];
+#pragma unroll
+    for (int q = 0; q < 2; ++q)
+#pragma unroll
+        for (int m = 0; m < 3; ++m) o[q][m] = f2(P[g.b1 + m]);
 #pragma unroll 4
     for (int j = 0; j < hid; ++j) {
         const float *r = s_rec[j];
-        f2 h = f2(r[hr(CIN)]);
 #pragma unroll
-        for (int i = 0; i < CIN; ++i) h = __builtin_elementwise_fma(f2(r[hr(i)]), xv[i], h);
-        h = __builtin_elementwise_max(h, lo0);
-        o0 = __builtin_elementwise_fma(f2(r[hr(CIN + 1)]), h, o0);
-        o1 = __builtin_elementwise_fma(f2(r[hr(CIN + 2)]), h, o1);
-        o2 = __builtin_elementwise_fma(f2(r[hr(CIN + 3)]), h, o2);
-    }
-    if (g.r1) {
-        o0 = __builtin_elementwise_max(o0, f2(0.f));
-        o1 = __builtin_elementwise_max(o1, f2(0.f));
-        o2 = __builtin_elementwise_max(o2, f2(0.f));
+        for (int q = 0; q < 2; ++q) {
+            f2 h = f2(r[hr(CIN)]);
+#pragma unroll
+            for (int i = 0; i < CIN; ++i) h = __builtin_elementwise_fma(f2(r[hr(i)]), xv[q][i], h);
+            h = __builtin_elementwise_max(h, lo0);
+#pragma unroll
+            for (int m = 0; m < 3; ++m) o[q][m] = __builtin_elementwise_fma(f2(r[hr(CIN + 1 + m)]), h, o[q][m]);
+        }
     }
     float *z = z0 + (int64_t)b * 3 * npx;
-    z[p0] = o0.x;
-    z[npx + p0] = o1.x;
-    z[2 * npx + p0] = o2.x;
-    if (v1) {
-        z[p1] = o0.y;
-        z[npx + p1] = o1.y;
-        z[2 * npx + p1] = o2.y;
-    }
+#pragma unroll
+    for (int q = 0; q < 2; ++q)
+#pragma unroll
+        for (int m = 0; m < 3; ++m) {
+            f2 v = o[q][m];
+            if (g.r1) v = __builtin_elementwise_max(v, f2(0.f));
+            const int64_t pa = p0 + 2 * q * kT, pb = pa + kT;
+            if (pa < npx) z[m * npx + pa] = v.x;
+            if (pb < npx) z[m * npx + pb] = v.y;
+        }
 }
 
 // 3x3, 3 -> 3, replicate padding (synthesis.py:69-84), optional residual / ReLU.
@@ -2614,7 +2622,10 @@ template <int CIN>
 void launch_head(bool bwd, dim3 grid, hipStream_t s, const float *dense, const float *gz0, const Geo &g, const float *th,
                  int64_t ps, float *z0_or_gdense, float *gth, int64_t gstride)
 {
-    if (!bwd) hipLaunchKernelGGL((t_head_fwd<CIN>), grid, dim3(kT), 0, s, dense, g, th, ps, z0_or_gdense);
+    if (!bwd) {
+        const unsigned nwg = (unsigned)(((int64_t)g.H * g.W + kHeadFwdPx - 1) / kHeadFwdPx);
+        hipLaunchKernelGGL((t_head_fwd<CIN>), dim3(nwg, grid.y), dim3(kT), 0, s, dense, g, th, ps, z0_or_gdense);
+    }
     else {
         // the tiled form for a linear output layer (every reference architecture); the full-width
         // form otherwise (and in -DCCMI_HEAD_BWD_FULL A/B builds)
