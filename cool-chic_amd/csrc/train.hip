@@ -13,7 +13,7 @@
 //   loss.backward(); clip_grad_norm_(params, 0.1); torch.optim.Adam.step()
 //
 // Kernels, in launch order (all frames of the batch in every launch, grid.y = frame):
-//   t_expand      trainable half kernels -> full symmetric kernels (upsampling.py:46-68)
+//   t_prologue    per-step zeroing + trainable half kernels -> full symmetric kernels (upsampling.py:46-68)
 //   t_quant       y_hat = Q(gain * y) and dQ/dy; noise from a counter-based RNG (or given)
 //   t_arm<D,NH>   ARM forward + rate + full backward in one pass: 4 x 64 latent tile + causal
 //                 halo in LDS; context gradients accumulate in an LDS tile (ds_add) and are
@@ -92,20 +92,34 @@ __device__ __forceinline__ float block_sum(float v, float *red)
 }
 
 // ------------------------------------------------------------------ parameters
-__global__ void t_expand(const float *__restrict__ th, int64_t ps, Geo g, float *__restrict__ kf)
+// Per-step prologue in one launch (three launches before: a memset, t_zero_rows, t_expand --
+// each a dependent dispatch of ~6 us on the step's critical path, profiles/r5l_train_timeline.txt):
+// zero nz floats from z (acc4 .. the kernel-gradient slots .. the ARM's side gradient), zero the
+// parameter part of every frame's gradient row, expand the symmetric upsampling kernels.
+__global__ void t_prologue(float *__restrict__ z, int64_t nz, float *__restrict__ Gp, int64_t np, int64_t gstride,
+                           const float *__restrict__ th, int64_t ps, Geo g, float *__restrict__ kf, int B)
 {
-    const int b = blockIdx.y, i = blockIdx.x * kT + threadIdx.x;
-    if (i >= g.kfull) return;
-    const float *p = th + (int64_t)b * ps;
-    float v;
-    if (i < g.n_ups * g.K) {
-        const int u = i / g.K, t = i - u * g.K;
-        v = p[g.up_off + u * g.hu + min(t, g.K - 1 - t)];
-    } else {
-        const int r = i - g.n_ups * g.K, u = r / g.Kp, t = r - u * g.Kp;
-        v = p[g.pre_off + u * g.hp + min(t, g.Kp - 1 - t)];
+    const int64_t n2 = nz + (int64_t)B * np, n3 = n2 + (int64_t)B * g.kfull;
+    for (int64_t i = (int64_t)blockIdx.x * kT + threadIdx.x; i < n3; i += (int64_t)gridDim.x * kT) {
+        if (i < nz) {
+            z[i] = 0.f;
+        } else if (i < n2) {
+            const int64_t j = i - nz, b = j / np;
+            Gp[b * gstride + (j - b * np)] = 0.f;
+        } else {
+            const int j = (int)(i - n2), b = j / g.kfull, e = j - b * g.kfull;
+            const float *p = th + (int64_t)b * ps;
+            float v;
+            if (e < g.n_ups * g.K) {
+                const int u = e / g.K, t = e - u * g.K;
+                v = p[g.up_off + u * g.hu + min(t, g.K - 1 - t)];
+            } else {
+                const int r = e - g.n_ups * g.K, u = r / g.Kp, t = r - u * g.Kp;
+                v = p[g.pre_off + u * g.hp + min(t, g.Kp - 1 - t)];
+            }
+            kf[(int64_t)b * g.kfull + e] = v;
+        }
     }
-    kf[(int64_t)b * g.kfull + i] = v;
 }
 
 // ------------------------------------------------------------------ quantizer
@@ -921,6 +935,9 @@ __global__ __launch_bounds__(kT) __attribute__((amdgpu_waves_per_eu(t_arm16_wpe(
             atomicAdd(&gdst[min(max(y, 0), H - 1) * W + min(max(x, 0), W - 1)], in ? v : 0.f);
         }
     }
+#if defined(CCMI_DIAG_NOFLUSH) // diagnostic build only (make diag): wrong results
+    return;
+#endif
     // ---- flush: the four waves' partial sums meet in LDS (s_ga is free after the tile loop) and
     // each value goes out with ONE atomic per workgroup.  (One atomic per value per wave, every
     // workgroup of a frame on the same ~600 addresses, serialised in L2: the kernel's time grew
@@ -1056,40 +1073,57 @@ __global__ __launch_bounds__(kT) void t_head_fwd(const float *__restrict__ dense
         }
 }
 
-// 3x3, 3 -> 3, replicate padding (synthesis.py:69-84), optional residual / ReLU.
+// 3x3, 3 -> 3, replicate padding (synthesis.py:69-84), optional residual / ReLU.  A thread
+// computes kSpRows vertically consecutive pixels of one column: the rows it reads overlap, so
+// it loads (kSpRows + 2) x 3 neighbours per channel instead of 9 per pixel (one pixel per
+// thread issued 27 loads per pixel); same FMA order per pixel.
+constexpr int kSpRows = 4;
 __global__ __launch_bounds__(kT) void t_sp_fwd(const float *__restrict__ in, Geo g, const float *__restrict__ th, int64_t ps,
                                                int wo, int bo, int res, int relu, float *__restrict__ out)
 {
     const int b = blockIdx.y;
-    const int64_t npx = (int64_t)g.H * g.W, p = (int64_t)blockIdx.x * kT + threadIdx.x;
-    if (p >= npx) return;
-    const int py = (int)(p / g.W), px = (int)(p - (int64_t)py * g.W);
+    const int64_t npx = (int64_t)g.H * g.W;
+    const int q = blockIdx.x * kT + threadIdx.x; // (row group, column); a frame fits 31 bits
+    const int gy = q / g.W, px = q - gy * g.W, y0 = gy * kSpRows;
+    if (y0 >= g.H) return;
     const cfloat_ptr P = (cfloat_ptr)(size_t)(th + (int64_t)b * ps);
     const float *x = in + (int64_t)b * 3 * npx;
-    float v[3][9];
+    int xo[3];
+#pragma unroll
+    for (int d = 0; d < 3; ++d) xo[d] = clampi(px + d - 1, g.W - 1);
+    float v[3][kSpRows + 2][3];
 #pragma unroll
     for (int i = 0; i < 3; ++i)
 #pragma unroll
-        for (int k = 0; k < 9; ++k) {
-            const int yy = clampi(py + k / 3 - 1, g.H - 1), xx = clampi(px + k % 3 - 1, g.W - 1);
-            v[i][k] = x[i * npx + (int64_t)yy * g.W + xx];
+        for (int r = 0; r < kSpRows + 2; ++r) {
+            const float *row = x + i * npx + (int64_t)clampi(y0 + r - 1, g.H - 1) * g.W;
+#pragma unroll
+            for (int d = 0; d < 3; ++d) v[i][r][d] = row[xo[d]];
         }
-    float *o = out + (int64_t)b * 3 * npx + p;
+    float *o = out + (int64_t)b * 3 * npx + (int64_t)y0 * g.W + px;
 #pragma unroll
-    for (int c = 0; c < 3; ++c) {
-        float a = P[bo + c];
+    for (int t = 0; t < kSpRows; ++t) {
+        if (y0 + t >= g.H) break;
 #pragma unroll
-        for (int i = 0; i < 3; ++i)
+        for (int c = 0; c < 3; ++c) {
+            float a = P[bo + c];
 #pragma unroll
-            for (int k = 0; k < 9; ++k) a = fmaf(P[wo + (c * 3 + i) * 9 + k], v[i][k], a);
-        if (res) a += v[c][4];
-        if (relu) a = fmaxf(a, 0.f);
-        o[c * npx] = a;
+            for (int i = 0; i < 3; ++i)
+#pragma unroll
+                for (int k = 0; k < 9; ++k) a = fmaf(P[wo + (c * 3 + i) * 9 + k], v[i][t + k / 3][k % 3], a);
+            if (res) a += v[c][t + 1][1];
+            if (relu) a = fmaxf(a, 0.f);
+            o[c * npx + (int64_t)t * g.W] = a;
+        }
     }
 }
 
 // Train-mode frame output + MSE (frame.py:175-183, loss.py _compute_mse): gradient of the
 // MSE w.r.t. the raw synthesis output; sum of squared errors into acc4[b][0].
+// 444: kLossPx pixels per thread and iteration with every load issued first (one pixel per
+// iteration left the kernel waiting on memory latency: 82 % of its wave cycles in WAIT_ANY at
+// 2 waves / SIMD, profiles/r5l_train_pmc.txt); 420: the chroma planes at even rows / columns.
+constexpr int kLossPx = 4;
 __global__ __launch_bounds__(kT) void t_loss(const float *__restrict__ raw, Geo g, const float *__restrict__ tgt,
                                              int64_t tstride, int yuv420, float *__restrict__ graw, float *__restrict__ acc4)
 {
@@ -1100,33 +1134,69 @@ __global__ __launch_bounds__(kT) void t_loss(const float *__restrict__ raw, Geo 
     const float total = yuv420 ? (float)(npx + 2 * (int64_t)h2 * w2) : (float)(3 * npx);
     const float k2 = 2.f / total;
     float se = 0.f;
+    const float *o = raw + (int64_t)b * 3 * npx;
+    const float *T = tgt + (int64_t)b * tstride;
+    float *go = graw + (int64_t)b * 3 * npx;
     // grid-stride: a few hundred workgroups per frame, so the per-workgroup atomic on the
     // frame's one loss slot stays cheap (one workgroup per 256 pixels serialised ~1,500
     // same-address atomics per frame: 124 us per 8-frame 512x768 iteration)
-    for (int64_t p = (int64_t)blockIdx.x * kT + threadIdx.x; p < npx; p += (int64_t)gridDim.x * kT) {
-        const int py = (int)(p / g.W), px = (int)(p - (int64_t)py * g.W);
-        const float *o = raw + (int64_t)b * 3 * npx + p;
-        const float *T = tgt + (int64_t)b * tstride;
-        float *go = graw + (int64_t)b * 3 * npx + p;
+    if (!yuv420) {
+        for (int64_t p0 = (int64_t)blockIdx.x * kT * kLossPx + threadIdx.x; p0 < npx; p0 += (int64_t)gridDim.x * kT * kLossPx) {
+            float v[kLossPx][3], t[kLossPx][3];
 #pragma unroll
-        for (int c = 0; c < 3; ++c) {
-            bool used = true;
-            int64_t ti = c * npx + p;
-            if (yuv420 && c > 0) {
-                used = (py % 2 == 0) && (px % 2 == 0) && (py / 2) < h2 && (px / 2) < w2;
-                ti = npx + (int64_t)(c - 1) * h2 * w2 + (int64_t)(py / 2) * w2 + px / 2;
+            for (int u = 0; u < kLossPx; ++u) {
+                const int64_t p = p0 + u * kT;
+#pragma unroll
+                for (int c = 0; c < 3; ++c) {
+                    v[u][c] = p < npx ? o[c * npx + p] : 0.f;
+                    t[u][c] = p < npx ? T[c * npx + p] : 0.f;
+                }
             }
-            float gv = 0.f;
-            if (used) {
-                const float v = o[c * npx], vc = fminf(fmaxf(v, 0.f), 1.f), d = vc - T[ti];
-                se += d * d;
-                gv = (v >= 0.f && v <= 1.f) ? k2 * d : 0.f;
+#pragma unroll
+            for (int u = 0; u < kLossPx; ++u) {
+                const int64_t p = p0 + u * kT;
+#pragma unroll
+                for (int c = 0; c < 3; ++c) {
+                    const float vc = fminf(fmaxf(v[u][c], 0.f), 1.f), d = vc - t[u][c];
+                    se += d * d; // 0 past the frame
+                    if (p < npx) go[c * npx + p] = (v[u][c] >= 0.f && v[u][c] <= 1.f) ? k2 * d : 0.f;
+                }
             }
-            go[c * npx] = gv;
+        }
+    } else {
+        for (int64_t p = (int64_t)blockIdx.x * kT + threadIdx.x; p < npx; p += (int64_t)gridDim.x * kT) {
+            const int py = (int)p / g.W, px = (int)p - py * g.W; // a frame's pixels fit 31 bits
+#pragma unroll
+            for (int c = 0; c < 3; ++c) {
+                bool used = true;
+                int64_t ti = c * npx + p;
+                if (c > 0) {
+                    used = (py % 2 == 0) && (px % 2 == 0) && (py / 2) < h2 && (px / 2) < w2;
+                    ti = npx + (int64_t)(c - 1) * h2 * w2 + (int64_t)(py / 2) * w2 + px / 2;
+                }
+                float gv = 0.f;
+                if (used) {
+                    const float vv = o[c * npx + p], vc = fminf(fmaxf(vv, 0.f), 1.f), d = vc - T[ti];
+                    se += d * d;
+                    gv = (vv >= 0.f && vv <= 1.f) ? k2 * d : 0.f;
+                }
+                go[c * npx + p] = gv;
+            }
         }
     }
     const float s = block_sum(se, s_red);
     if (threadIdx.x == 0) atomicAdd(&acc4[b * 4 + 0], s);
+}
+
+// workgroups per frame of the per-frame sum reductions (t_loss, t_latgrad_sumsq): each
+// workgroup ends in ONE atomic on the frame's accumulator, and same-address atomics serialise
+// at ≈80 ns each (256 -> 384 workgroups per frame took t_loss from 29 to 35 us and 256 -> 512
+// t_latgrad_sumsq from 29 to 53 us, profiles/r5m_*), so a frame gets at most kSumWGs
+// workgroups, each with several batched iterations
+constexpr int kSumWGs = 128;
+static unsigned sum_blocks(int64_t n, int per_iter)
+{
+    return (unsigned)std::max<int64_t>(1, std::min<int64_t>(kSumWGs, (n + (int64_t)kT * per_iter - 1) / ((int64_t)kT * per_iter)));
 }
 
 // g_pre = g_out * relu'(out), in place.
@@ -1747,6 +1817,9 @@ __global__ __launch_bounds__(kHeadT, 4) void t_head_bwd_t(const float *__restric
         }
     }
     // ---- flush (t_head_bwd's): the waves' partial rows meet in LDS, one atomic per value
+#if defined(CCMI_DIAG_NOFLUSH) // diagnostic build only (make diag): wrong results
+    return;
+#endif
     const int nred = hid * (CIN + 4) + 3;
     float *red = s_dyn + w * kWF;
     static_assert(kWF >= 16 * NT * (CIN + 4) + 3, "a wave's partial row fits its LDS rows");
@@ -2305,11 +2378,6 @@ __global__ __launch_bounds__(kT) void t_lvl_bwd(RefBwd R, UpBwd Q, int nref)
 }
 
 // ------------------------------------------------------------------ latents, norm, Adam
-__global__ void t_zero_rows(float *__restrict__ p, int64_t n, int64_t stride)
-{
-    const int64_t i = (int64_t)blockIdx.x * kT + threadIdx.x;
-    if (i < n) p[(int64_t)blockIdx.y * stride + i] = 0.f;
-}
 
 // dL/dy of the latents (G[0, N) = dL/dyhat * dyhat/dy) and the squared norm of the whole
 // gradient row (latents + parameters, clip_grad_norm_) in one pass
@@ -2323,15 +2391,29 @@ __global__ __launch_bounds__(kT) void t_latgrad_sumsq(const float *__restrict__ 
     const float *gqb = gq + (int64_t)b * N, *dqb = dq + (int64_t)b * N;
     const float *gq2b = gq2 ? gq2 + (int64_t)b * N : nullptr; // the ARM's part (side-stream form)
     float s = 0.f;
-    for (int64_t i = (int64_t)blockIdx.x * kT + threadIdx.x; i < n; i += (int64_t)gridDim.x * kT) {
-        float v;
-        if (i < N) {
-            v = (gq2b ? gq2b[i] + gqb[i] : gqb[i]) * dqb[i];
-            g[i] = v;
-        } else {
-            v = g[i];
+    // four elements per thread and iteration, every load issued first (one per iteration waited
+    // on memory latency, as t_loss did)
+    constexpr int U = 4;
+    for (int64_t i0 = (int64_t)blockIdx.x * kT * U + threadIdx.x; i0 < n; i0 += (int64_t)gridDim.x * kT * U) {
+        float a[U], a2[U], d[U], r[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const int64_t i = i0 + u * kT, il = i < N ? i : 0;
+            a[u] = gqb[il];
+            a2[u] = gq2b ? gq2b[il] : 0.f;
+            d[u] = dqb[il];
+            r[u] = (i >= N && i < n) ? g[i] : 0.f;
         }
-        s = fmaf(v, v, s);
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const int64_t i = i0 + u * kT;
+            float v = r[u];
+            if (i < N) {
+                v = (gq2b ? a2[u] + a[u] : a[u]) * d[u];
+                g[i] = v;
+            }
+            s = fmaf(v, v, s); // 0 past the row
+        }
     }
     s = block_sum(s, s_red);
     if (threadIdx.x == 0) atomicAdd(&acc4[b * 4 + 2], s);
@@ -2342,6 +2424,8 @@ struct AdamArgs {
     int N, latents_only;
     int64_t n, gstride, ls, ps, ms;
     const float *bc; // optional [B][2] per-frame (lr / bc1, 1 / sqrt(bc2)) (per-frame Adam steps)
+    float *loss_out; // optional [B][4]: t_finish's row, written by workgroup (0, b)
+    float inv_total, lam_px;
 };
 
 // per-frame bias corrections when frames carry their own Adam step (a frame whose optimizer
@@ -2365,11 +2449,20 @@ __global__ void t_adam_bc(const int32_t *__restrict__ steps, double lr, double b
 }
 
 // torch.optim.Adam (_single_tensor_adam, no weight decay / amsgrad) after clip_grad_norm_
+__device__ __forceinline__ void finish_row(const float *__restrict__ acc4, float inv_total, float lam_px, float *__restrict__ out, int b)
+{
+    const float mse = acc4[b * 4 + 0] * inv_total, rate = acc4[b * 4 + 1];
+    out[b * 4 + 0] = mse + lam_px * rate;
+    out[b * 4 + 1] = mse;
+    out[b * 4 + 2] = rate;
+    out[b * 4 + 3] = sqrtf(acc4[b * 4 + 2]);
+}
 __global__ void t_adam(const float *__restrict__ G, float *__restrict__ lat, float *__restrict__ th, float *__restrict__ m,
                        float *__restrict__ v, const float *__restrict__ acc4, AdamArgs A)
 {
     const int b = blockIdx.y;
     const int64_t i = (int64_t)blockIdx.x * kT + threadIdx.x;
+    if (A.loss_out && i == 0) finish_row(acc4, A.inv_total, A.lam_px, A.loss_out, b); // (t_finish folded in)
     if (i >= A.n || (A.latents_only && i >= A.N)) return;
     if (A.bc && A.bc[2 * b + 1] < 0.f) return; // frozen frame (adam_steps <= 0)
     float coef = 1.f;
@@ -2389,12 +2482,7 @@ __global__ void t_adam(const float *__restrict__ G, float *__restrict__ lat, flo
 __global__ void t_finish(const float *__restrict__ acc4, float inv_total, float lam_px, float *__restrict__ out, int B)
 {
     const int b = threadIdx.x;
-    if (b >= B) return;
-    const float mse = acc4[b * 4 + 0] * inv_total, rate = acc4[b * 4 + 1];
-    out[b * 4 + 0] = mse + lam_px * rate;
-    out[b * 4 + 1] = mse;
-    out[b * 4 + 2] = rate;
-    out[b * 4 + 3] = sqrtf(acc4[b * 4 + 2]);
+    if (b < B) finish_row(acc4, inv_total, lam_px, out, b);
 }
 
 // ------------------------------------------------------------------ host planning
@@ -2784,16 +2872,20 @@ extern "C" int ccmi_train_step(const ccmi_train_args *a, void *stream)
     const int64_t npx = (int64_t)g.H * g.W;
     const float lam_px = a->lmbda / (float)npx;
 
-    // acc4 and the kernel-gradient slots are adjacent: one memset
-    CCMI_HIP_CHECK(hipMemsetAsync(acc4, 0, pl.total - pl.acc4, s));
     float *slots = F(pl.slots);
     const int nreg = g.syn_off - g.up_off; // upsampling kernels' parameters (half kernels)
-    // the parameter part of every gradient row (its latent part is written whole by
-    // t_latgrad_sumsq)
-    hipLaunchKernelGGL(t_zero_rows, grid1(g.P, B), dim3(kT), 0, s, G + g.N, (int64_t)g.P, GS);
+    {
+        // acc4 .. the end of the workspace plan (kernel-gradient slots, the ARM's side gradient)
+        // zeroed, the parameter part of every gradient row zeroed (its latent part is written
+        // whole by t_latgrad_sumsq), the symmetric kernels expanded: one launch
+        const int64_t nz = (int64_t)(pl.total - pl.acc4) / (int64_t)sizeof(float);
+        const int64_t n = nz + (int64_t)B * (g.P + g.kfull);
+        const unsigned nb = (unsigned)std::max<int64_t>(1, std::min<int64_t>(ccmi_div_up(n, 4 * kT), 2048));
+        hipLaunchKernelGGL(t_prologue, dim3(nb), dim3(kT), 0, s, acc4, nz, G + g.N, (int64_t)g.P, GS, a->params,
+                           a->param_stride, g, kf, B);
+    }
 
     // ---- forward
-    hipLaunchKernelGGL(t_expand, grid1(g.kfull, B), dim3(kT), 0, s, a->params, a->param_stride, g, kf);
     hipLaunchKernelGGL(t_quant, grid1(g.N, B), dim3(kT), 0, s, a->latent, a->latent_stride, g.N, a->gain, a->quantizer,
                        a->noise, quant_args(a->temperature, a->noise_param), (uint64_t)a->seed, a->step, a->noise_in, yq,
                        dq, gq);
@@ -2859,7 +2951,7 @@ extern "C" int ccmi_train_step(const ccmi_train_args *a, void *stream)
     head_dispatch(g.L, false, dim3((unsigned)((npx + 2 * kT - 1) / (2 * kT)), (unsigned)B), s, dense, nullptr, g, a->params,
                   a->param_stride, F(pl.z[0]), nullptr, 0); // two pixels per thread
     for (int i = 0; i < g.n_sp; ++i)
-        hipLaunchKernelGGL(t_sp_fwd, grid1(npx, B), dim3(kT), 0, s, F(pl.z[i]), g, a->params, a->param_stride, g.sp_w[i],
+        hipLaunchKernelGGL(t_sp_fwd, grid1((int64_t)ccmi_div_up(g.H, kSpRows) * g.W, B), dim3(kT), 0, s, F(pl.z[i]), g, a->params, a->param_stride, g.sp_w[i],
                            g.sp_b[i], g.sp_res[i], g.sp_relu[i], F(pl.z[i + 1]));
     if (a->raw_out)
         CCMI_HIP_CHECK(hipMemcpyAsync(a->raw_out, F(pl.z[g.n_sp]), sizeof(float) * 3 * npx * B, hipMemcpyDeviceToDevice, s));
@@ -2870,7 +2962,7 @@ extern "C" int ccmi_train_step(const ccmi_train_args *a, void *stream)
             // with a real target (target_stride > 0) the loss row holds the built-in MSE too;
             // otherwise (autograd: the loss lives in torch) MSE reads 0 and loss = lmbda-rate
             if (a->target && a->target_stride > 0)
-                hipLaunchKernelGGL(t_loss, dim3(std::min(grid1(npx, B).x, 256u), B), dim3(kT), 0, s, F(pl.z[g.n_sp]), g,
+                hipLaunchKernelGGL(t_loss, dim3(sum_blocks(npx, kLossPx), B), dim3(kT), 0, s, F(pl.z[g.n_sp]), g,
                                    a->target, a->target_stride, a->yuv420, graw, acc4);
             const float total = a->yuv420 ? (float)(npx + 2 * (int64_t)(g.H / 2) * (g.W / 2)) : (float)(3 * npx);
             hipLaunchKernelGGL(t_finish, dim3(1), dim3(std::max(64, B)), 0, s, acc4, 1.f / total, lam_px, a->loss_out, B);
@@ -2881,7 +2973,7 @@ extern "C" int ccmi_train_step(const ccmi_train_args *a, void *stream)
     if (a->grad_raw) // the caller's d loss / d raw output (autograd); no built-in MSE term
         CCMI_HIP_CHECK(hipMemcpyAsync(graw, a->grad_raw, sizeof(float) * 3 * npx * B, hipMemcpyDeviceToDevice, s));
     else
-        hipLaunchKernelGGL(t_loss, dim3(std::min(grid1(npx, B).x, 256u), B), dim3(kT), 0, s, F(pl.z[g.n_sp]), g, a->target, a->target_stride,
+        hipLaunchKernelGGL(t_loss, dim3(sum_blocks(npx, kLossPx), B), dim3(kT), 0, s, F(pl.z[g.n_sp]), g, a->target, a->target_stride,
                            a->yuv420, graw, acc4);
 
     // ---- synthesis backward
@@ -2977,18 +3069,19 @@ extern "C" int ccmi_train_step(const ccmi_train_args *a, void *stream)
     hipLaunchKernelGGL(t_dw_fold, dim3((unsigned)ccmi_div_up(nreg, 64), B), dim3(64), 0, s, slots, nreg, Gth, GS, g.up_off);
 
     // ---- latent gradients, norm, Adam
-    // about eight workgroups per CU over the batch, 4+ elements per thread
-    const unsigned nls = (unsigned)std::max<int64_t>(1, std::min<int64_t>(ccmi_div_up(GS, 4 * kT), std::max(1, 2048 / B)));
+    const unsigned nls = sum_blocks(GS, 4);
     CCMI_HIP_CHECK(join.wait());
     hipLaunchKernelGGL(t_latgrad_sumsq, dim3(nls, B), dim3(kT), 0, s, gq, side ? F(pl.gq_arm) : nullptr, dq, g.N, G, GS,
                        GS, acc4);
     const float total = a->yuv420 ? (float)(npx + 2 * (int64_t)(g.H / 2) * (g.W / 2)) : (float)(3 * npx);
-    if (a->loss_out) hipLaunchKernelGGL(t_finish, dim3(1), dim3(std::max(64, B)), 0, s, acc4, 1.f / total, lam_px, a->loss_out, B);
+    if (a->loss_out && !a->update)
+        hipLaunchKernelGGL(t_finish, dim3(1), dim3(std::max(64, B)), 0, s, acc4, 1.f / total, lam_px, a->loss_out, B);
     if (a->update) {
         const double bc1 = 1.0 - std::pow((double)a->beta1, a->step), bc2 = 1.0 - std::pow((double)a->beta2, a->step);
         AdamArgs A{(float)(a->lr / bc1), (float)(1.0 / std::sqrt(bc2)), a->beta1, a->beta2, a->eps, a->clip, g.N,
                    a->update == 2 ? 1 : 0, GS, GS,
-                   a->latent_stride, a->param_stride, (int64_t)a->latent_stride + a->param_stride, nullptr};
+                   a->latent_stride, a->param_stride, (int64_t)a->latent_stride + a->param_stride, nullptr,
+                   a->loss_out, 1.f / total, lam_px};
         if (a->adam_steps) {
             A.bc = F(pl.bc);
             hipLaunchKernelGGL(t_adam_bc, dim3((unsigned)ccmi_div_up(B, 64)), dim3(64), 0, s, a->adam_steps, (double)a->lr,
