@@ -43,6 +43,13 @@ namespace {
 constexpr int kT = 256;
 constexpr int kMaxSp = 3;
 constexpr int kHeadT = 128;
+// Parameter gradients: every workgroup that reduces weight / bias gradients (the ARM, the head,
+// the 3x3 layers, the upsampling kernels) adds its partial sums into one of kDwSlots copies of
+// the frame's parameter-gradient row (slot = workgroup % kDwSlots), and t_dw_fold sums the
+// slots into the gradient row once per step: same-address atomics serialise (≈80 ns each), and
+// the persistent kernels' workgroups all flush at once at their end.  The ARM's rate sums take
+// the same form (kDwSlots per frame).
+constexpr int kDwSlots = 32;
 constexpr float kLn2 = 0.6931471805599453f;
 
 // Per-frame geometry and parameter offsets (same for every frame of a batch).
@@ -94,20 +101,17 @@ __device__ __forceinline__ float block_sum(float v, float *red)
 // ------------------------------------------------------------------ parameters
 // Per-step prologue in one launch (three launches before: a memset, t_zero_rows, t_expand --
 // each a dependent dispatch of ~6 us on the step's critical path, profiles/r5l_train_timeline.txt):
-// zero nz floats from z (acc4 .. the kernel-gradient slots .. the ARM's side gradient), zero the
-// parameter part of every frame's gradient row, expand the symmetric upsampling kernels.
-__global__ void t_prologue(float *__restrict__ z, int64_t nz, float *__restrict__ Gp, int64_t np, int64_t gstride,
-                           const float *__restrict__ th, int64_t ps, Geo g, float *__restrict__ kf, int B)
+// zero nz floats from z (acc4, the rate and parameter-gradient slots, the ARM's side gradient)
+// and expand the symmetric upsampling kernels.
+__global__ void t_prologue(float *__restrict__ z, int64_t nz, const float *__restrict__ th, int64_t ps, Geo g,
+                           float *__restrict__ kf, int B)
 {
-    const int64_t n2 = nz + (int64_t)B * np, n3 = n2 + (int64_t)B * g.kfull;
-    for (int64_t i = (int64_t)blockIdx.x * kT + threadIdx.x; i < n3; i += (int64_t)gridDim.x * kT) {
+    const int64_t n = nz + (int64_t)B * g.kfull;
+    for (int64_t i = (int64_t)blockIdx.x * kT + threadIdx.x; i < n; i += (int64_t)gridDim.x * kT) {
         if (i < nz) {
             z[i] = 0.f;
-        } else if (i < n2) {
-            const int64_t j = i - nz, b = j / np;
-            Gp[b * gstride + (j - b * np)] = 0.f;
         } else {
-            const int j = (int)(i - n2), b = j / g.kfull, e = j - b * g.kfull;
+            const int j = (int)(i - nz), b = j / g.kfull, e = j - b * g.kfull;
             const float *p = th + (int64_t)b * ps;
             float v;
             if (e < g.n_ups * g.K) {
@@ -648,10 +652,10 @@ __global__ __launch_bounds__(kT) __attribute__((amdgpu_waves_per_eu(t_arm_wpe(D,
 #pragma unroll
     for (int L = 0; L < NH; ++L) stage_outer<D, D>(acc_h[L], accb_h[L], red + L * LS, red + L * LS + D * D);
     __syncthreads();
-    float *G = gth + (int64_t)b * gstride;
+    float *G = gth + ((int64_t)b * kDwSlots + blockIdx.x % kDwSlots) * gstride; // this workgroup's slot row
     for (int e = threadIdx.x; e < kRed; e += kT)
         atomicAdd(&G[e], (s_ga[e] + s_ga[kRed + e]) + (s_ga[2 * kRed + e] + s_ga[3 * kRed + e]));
-    wave_add(rsum, &acc4[b * 4 + 1]);
+    wave_add(rsum, &acc4[b * kDwSlots + blockIdx.x % kDwSlots]); // the frame's rate slots
 }
 
 // ARM forward + rate + backward for dim_arm = 16 with the MLP on the matrix cores.
@@ -935,8 +939,8 @@ __global__ __launch_bounds__(kT) __attribute__((amdgpu_waves_per_eu(t_arm16_wpe(
             atomicAdd(&gdst[min(max(y, 0), H - 1) * W + min(max(x, 0), W - 1)], in ? v : 0.f);
         }
     }
-#if defined(CCMI_DIAG_NOFLUSH) // diagnostic build only (make diag): wrong results
-    return;
+#if defined(CCMI_DIAG_NOFLUSH) // diagnostic build only (make diag): wrong results -- and with the
+    return;                       // accumulators dead, the compiler drops the weight-gradient work too
 #endif
     // ---- flush: the four waves' partial sums meet in LDS (s_ga is free after the tile loop) and
     // each value goes out with ONE atomic per workgroup.  (One atomic per value per wave, every
@@ -978,10 +982,10 @@ __global__ __launch_bounds__(kT) __attribute__((amdgpu_waves_per_eu(t_arm16_wpe(
         red[NH * LS + 2 * D + 1] = accbo1;
     }
     __syncthreads();
-    float *Gp = gth + (int64_t)b * gstride;
+    float *Gp = gth + ((int64_t)b * kDwSlots + blockIdx.x % kDwSlots) * gstride; // this workgroup's slot row
     for (int e = threadIdx.x; e < kRed; e += kT)
         atomicAdd(&Gp[e], (s_ga[e] + s_ga[kRed + e]) + (s_ga[2 * kRed + e] + s_ga[3 * kRed + e]));
-    wave_add(rsum, &acc4[b * 4 + 1]);
+    wave_add(rsum, &acc4[b * kDwSlots + blockIdx.x % kDwSlots]); // the frame's rate slots
 }
 
 // Column sums of per-workgroup partial rows: dst[b][col] += sum_r part[b][r][col].
@@ -1379,7 +1383,7 @@ __global__ __launch_bounds__(kT) __attribute__((amdgpu_waves_per_eu(MODE == 2 ? 
     if (threadIdx.x < 84) {
         const int e = threadIdx.x;
         const float v = s_red[0][e] + s_red[1][e] + s_red[2][e] + s_red[3][e];
-        float *dst = gth + (int64_t)b * gstride;
+        float *dst = gth + ((int64_t)b * kDwSlots + blockIdx.x % kDwSlots) * gstride; // this workgroup's slot row
         atomicAdd(&dst[e < 81 ? wo + e : bo + (e - 81)], v);
     }
 }
@@ -1644,7 +1648,7 @@ __global__ __launch_bounds__(kHeadT) void t_head_bwd(const float *__restrict__ d
         if (lane == 0) red[hid * (CIN + 4) + k] = v;
     }
     __syncthreads();
-    float *Gp = gth + (int64_t)b * gstride;
+    float *Gp = gth + ((int64_t)b * kDwSlots + blockIdx.x % kDwSlots) * gstride; // this workgroup's slot row
     constexpr int kW = kHeadT / 64;
     for (int e = t; e < nred; e += kHeadT) {
         float v = 0.f;
@@ -1817,8 +1821,8 @@ __global__ __launch_bounds__(kHeadT, 4) void t_head_bwd_t(const float *__restric
         }
     }
     // ---- flush (t_head_bwd's): the waves' partial rows meet in LDS, one atomic per value
-#if defined(CCMI_DIAG_NOFLUSH) // diagnostic build only (make diag): wrong results
-    return;
+#if defined(CCMI_DIAG_NOFLUSH) // diagnostic build only (make diag): wrong results -- and with the
+    return;                       // accumulators dead, the compiler drops the weight-gradient work too
 #endif
     const int nred = hid * (CIN + 4) + 3;
     float *red = s_dyn + w * kWF;
@@ -1846,7 +1850,7 @@ __global__ __launch_bounds__(kHeadT, 4) void t_head_bwd_t(const float *__restric
         if (lane == 0) red[hid * (CIN + 4) + k] = v;
     }
     __syncthreads();
-    float *Gp = gth + (int64_t)b * gstride;
+    float *Gp = gth + ((int64_t)b * kDwSlots + blockIdx.x % kDwSlots) * gstride; // this workgroup's slot row
     constexpr int kW = kHeadT / 64;
     for (int e = t; e < nred; e += kHeadT) {
         float v = 0.f;
@@ -1869,11 +1873,7 @@ struct UpLevel {
 
 // Sum of per-thread tap gradients over the workgroup, folded onto the symmetric half
 // kernel (upsampling.py:46-68): one atomic per half tap per workgroup.
-// Upsampling kernel gradients: each workgroup of a t_*_dw reduction adds its taps into one
-// of kDwSlots copies of the frame's upsampling-parameter gradients (slot = workgroup %
-// kDwSlots), so the big levels can use many workgroups without serialising on one
-// address; t_dw_fold sums the slots into the gradient row once per step.
-constexpr int kDwSlots = 32;
+// (The slot rows: see kDwSlots.)
 
 __global__ void t_dw_fold(const float *__restrict__ slots, int nreg, float *__restrict__ gth, int64_t gstride, int off)
 {
@@ -1883,7 +1883,7 @@ __global__ void t_dw_fold(const float *__restrict__ slots, int nreg, float *__re
     float v = 0.f;
 #pragma unroll 8
     for (int k = 0; k < kDwSlots; ++k) v += sl[(int64_t)k * nreg];
-    gth[(int64_t)b * gstride + off + e] += v;
+    gth[(int64_t)b * gstride + off + e] = v; // the only writer of the parameter gradients
 }
 
 template <int K>
@@ -2425,6 +2425,7 @@ struct AdamArgs {
     int64_t n, gstride, ls, ps, ms;
     const float *bc; // optional [B][2] per-frame (lr / bc1, 1 / sqrt(bc2)) (per-frame Adam steps)
     float *loss_out; // optional [B][4]: t_finish's row, written by workgroup (0, b)
+    const float *rslots;
     float inv_total, lam_px;
 };
 
@@ -2449,9 +2450,13 @@ __global__ void t_adam_bc(const int32_t *__restrict__ steps, double lr, double b
 }
 
 // torch.optim.Adam (_single_tensor_adam, no weight decay / amsgrad) after clip_grad_norm_
-__device__ __forceinline__ void finish_row(const float *__restrict__ acc4, float inv_total, float lam_px, float *__restrict__ out, int b)
+__device__ __forceinline__ void finish_row(const float *__restrict__ acc4, const float *__restrict__ rslots, float inv_total,
+                                           float lam_px, float *__restrict__ out, int b)
 {
-    const float mse = acc4[b * 4 + 0] * inv_total, rate = acc4[b * 4 + 1];
+    float rate = 0.f;
+#pragma unroll 8
+    for (int k = 0; k < kDwSlots; ++k) rate += rslots[b * kDwSlots + k];
+    const float mse = acc4[b * 4 + 0] * inv_total;
     out[b * 4 + 0] = mse + lam_px * rate;
     out[b * 4 + 1] = mse;
     out[b * 4 + 2] = rate;
@@ -2462,7 +2467,7 @@ __global__ void t_adam(const float *__restrict__ G, float *__restrict__ lat, flo
 {
     const int b = blockIdx.y;
     const int64_t i = (int64_t)blockIdx.x * kT + threadIdx.x;
-    if (A.loss_out && i == 0) finish_row(acc4, A.inv_total, A.lam_px, A.loss_out, b); // (t_finish folded in)
+    if (A.loss_out && i == 0) finish_row(acc4, A.rslots, A.inv_total, A.lam_px, A.loss_out, b); // (t_finish folded in)
     if (i >= A.n || (A.latents_only && i >= A.N)) return;
     if (A.bc && A.bc[2 * b + 1] < 0.f) return; // frozen frame (adam_steps <= 0)
     float coef = 1.f;
@@ -2479,10 +2484,11 @@ __global__ void t_adam(const float *__restrict__ G, float *__restrict__ lat, flo
     *p -= lr_bc1 * mm / denom;
 }
 
-__global__ void t_finish(const float *__restrict__ acc4, float inv_total, float lam_px, float *__restrict__ out, int B)
+__global__ void t_finish(const float *__restrict__ acc4, const float *__restrict__ rslots, float inv_total, float lam_px,
+                         float *__restrict__ out, int B)
 {
     const int b = threadIdx.x;
-    if (b < B) finish_row(acc4, inv_total, lam_px, out, b);
+    if (b < B) finish_row(acc4, rslots, inv_total, lam_px, out, b);
 }
 
 // ------------------------------------------------------------------ host planning
@@ -2515,7 +2521,7 @@ struct Plan {
     // workspace offsets (bytes)
     size_t gq_arm = 0; // the ARM's latent gradients when it runs on the side stream (CCMI_ARM_OVERLAP)
     size_t yq, dq, gq, kf, stacks, stacks_bytes, dense, z[kMaxSp + 1], graw, gbuf[2], gdense, gstack, tmpU, tmpG, G,
-        acc4, bc, slots, total;
+        acc4, bc, rslots, slots, total;
     int64_t gstack_off[CCMI_MAX_GRIDS]; // per level k (1..L-2) inside gstack, elements per frame
     int64_t gstack_per, stack_per, tmp_per;
 };
@@ -2646,7 +2652,10 @@ int make_plan(const ccmi_train_args *a, Plan &pl)
     pl.G = take(4 * B * ((size_t)g.N + g.P));
     pl.acc4 = take(4 * B * 4);
     pl.bc = take(4 * B * 2);
-    pl.slots = take(4 * B * kDwSlots * (size_t)(g.syn_off - g.up_off));
+    pl.rslots = take(4 * B * kDwSlots);
+    // every parameter's gradient through kDwSlots slot rows per frame (one row per workgroup
+    // residue), folded into the gradient row by t_dw_fold (kDwSlots)
+    pl.slots = take(4 * B * kDwSlots * (size_t)g.P);
     if (arm_overlap()) pl.gq_arm = take(4 * B * g.N); // after acc4: zeroed with it
     pl.total = o;
     return CCMI_OK;
@@ -2872,17 +2881,17 @@ extern "C" int ccmi_train_step(const ccmi_train_args *a, void *stream)
     const int64_t npx = (int64_t)g.H * g.W;
     const float lam_px = a->lmbda / (float)npx;
 
-    float *slots = F(pl.slots);
-    const int nreg = g.syn_off - g.up_off; // upsampling kernels' parameters (half kernels)
+    // the parameter gradients' slot rows ([B][kDwSlots][P], see make_plan) and the rate slots
+    float *slots = F(pl.slots), *rslots = F(pl.rslots);
+    float *uslots = slots + g.up_off; // the upsampling kernels' columns (their offsets are relative to up_off)
     {
-        // acc4 .. the end of the workspace plan (kernel-gradient slots, the ARM's side gradient)
-        // zeroed, the parameter part of every gradient row zeroed (its latent part is written
-        // whole by t_latgrad_sumsq), the symmetric kernels expanded: one launch
+        // acc4 .. the end of the workspace plan (rate and parameter-gradient slots, the ARM's side
+        // gradient) zeroed and the symmetric kernels expanded, in one launch; the gradient rows
+        // need no zeroing: t_latgrad_sumsq writes their latent part and t_dw_fold their parameters
         const int64_t nz = (int64_t)(pl.total - pl.acc4) / (int64_t)sizeof(float);
-        const int64_t n = nz + (int64_t)B * (g.P + g.kfull);
+        const int64_t n = nz + (int64_t)B * g.kfull;
         const unsigned nb = (unsigned)std::max<int64_t>(1, std::min<int64_t>(ccmi_div_up(n, 4 * kT), 2048));
-        hipLaunchKernelGGL(t_prologue, dim3(nb), dim3(kT), 0, s, acc4, nz, G + g.N, (int64_t)g.P, GS, a->params,
-                           a->param_stride, g, kf, B);
+        hipLaunchKernelGGL(t_prologue, dim3(nb), dim3(kT), 0, s, acc4, nz, a->params, a->param_stride, g, kf, B);
     }
 
     // ---- forward
@@ -2916,10 +2925,10 @@ extern "C" int ccmi_train_step(const ccmi_train_args *a, void *stream)
 #endif
         }
         switch (g.d) {
-        case 8: launch_arm_d<8>(g.nh, pl.nblk_arm, B, cap, sa, yq, g, pl.at, a->params, a->param_stride, lam_px, gqa, Gth, GS, acc4, a->grad_rate, a->rate_out); break;
-        case 16: launch_arm_d<16>(g.nh, pl.nblk_arm, B, cap, sa, yq, g, pl.at, a->params, a->param_stride, lam_px, gqa, Gth, GS, acc4, a->grad_rate, a->rate_out); break;
-        case 24: launch_arm_d<24>(g.nh, pl.nblk_arm, B, cap, sa, yq, g, pl.at, a->params, a->param_stride, lam_px, gqa, Gth, GS, acc4, a->grad_rate, a->rate_out); break;
-        default: launch_arm_d<32>(g.nh, pl.nblk_arm, B, cap, sa, yq, g, pl.at, a->params, a->param_stride, lam_px, gqa, Gth, GS, acc4, a->grad_rate, a->rate_out); break;
+        case 8: launch_arm_d<8>(g.nh, pl.nblk_arm, B, cap, sa, yq, g, pl.at, a->params, a->param_stride, lam_px, gqa, slots, g.P, rslots, a->grad_rate, a->rate_out); break;
+        case 16: launch_arm_d<16>(g.nh, pl.nblk_arm, B, cap, sa, yq, g, pl.at, a->params, a->param_stride, lam_px, gqa, slots, g.P, rslots, a->grad_rate, a->rate_out); break;
+        case 24: launch_arm_d<24>(g.nh, pl.nblk_arm, B, cap, sa, yq, g, pl.at, a->params, a->param_stride, lam_px, gqa, slots, g.P, rslots, a->grad_rate, a->rate_out); break;
+        default: launch_arm_d<32>(g.nh, pl.nblk_arm, B, cap, sa, yq, g, pl.at, a->params, a->param_stride, lam_px, gqa, slots, g.P, rslots, a->grad_rate, a->rate_out); break;
         }
         CCMI_HIP_CHECK(hipGetLastError());
         join.record();
@@ -2965,7 +2974,7 @@ extern "C" int ccmi_train_step(const ccmi_train_args *a, void *stream)
                 hipLaunchKernelGGL(t_loss, dim3(sum_blocks(npx, kLossPx), B), dim3(kT), 0, s, F(pl.z[g.n_sp]), g,
                                    a->target, a->target_stride, a->yuv420, graw, acc4);
             const float total = a->yuv420 ? (float)(npx + 2 * (int64_t)(g.H / 2) * (g.W / 2)) : (float)(3 * npx);
-            hipLaunchKernelGGL(t_finish, dim3(1), dim3(std::max(64, B)), 0, s, acc4, 1.f / total, lam_px, a->loss_out, B);
+            hipLaunchKernelGGL(t_finish, dim3(1), dim3(std::max(64, B)), 0, s, acc4, F(pl.rslots), 1.f / total, lam_px, a->loss_out, B);
         }
         CCMI_HIP_CHECK(hipGetLastError());
         return CCMI_OK;
@@ -2988,15 +2997,15 @@ extern "C" int ccmi_train_step(const ccmi_train_args *a, void *stream)
         {
             // input gradient: one tile per workgroup; weight gradients: grid-stride as before
             hipLaunchKernelGGL(t_sp_bwd<1>, dim3((unsigned)ntile, B), dim3(kT), 0, s, gcur, outp, F(pl.z[i]), g, a->params,
-                               a->param_stride, g.sp_w[i], g.sp_b[i], g.sp_res[i], gin, Gth, GS);
+                               a->param_stride, g.sp_w[i], g.sp_b[i], g.sp_res[i], gin, slots, g.P);
             hipLaunchKernelGGL(t_sp_bwd<2>, dim3(nb, B), dim3(kT), 0, s, gcur, outp, F(pl.z[i]), g, a->params,
-                               a->param_stride, g.sp_w[i], g.sp_b[i], g.sp_res[i], gin, Gth, GS);
+                               a->param_stride, g.sp_w[i], g.sp_b[i], g.sp_res[i], gin, slots, g.P);
         }
         gcur = gin;
     }
     {
         // grid-stride over pixel chunks: one resident round of workgroups (set by launch_head)
-        head_dispatch(g.L, true, dim3(1, B), s, dense, gcur, g, a->params, a->param_stride, gd, Gth, GS);
+        head_dispatch(g.L, true, dim3(1, B), s, dense, gcur, g, a->params, a->param_stride, gd, slots, g.P);
     }
 
     // ---- upsampling backward, finest level first (step L-2 .. 0)
@@ -3010,7 +3019,7 @@ extern "C" int ccmi_train_step(const ccmi_train_args *a, void *stream)
         // refine of y_hat(k-1): channel 0 of the destination stack (tiles 16 x 64)
         const int rtx = ccmi_div_up(wd, 64), nref = rtx * ccmi_div_up(hd, 16);
         const RefBwd R{GY, gys, yq + g.off[k - 1], (int64_t)g.N, hd, wd, kf, g.kfull,
-                       g.n_ups * g.K + (step % g.n_pre) * g.Kp, gq + g.off[k - 1], (int64_t)g.N, slots, (int64_t)nreg,
+                       g.n_ups * g.K + (step % g.n_pre) * g.Kp, gq + g.off[k - 1], (int64_t)g.N, uslots, (int64_t)g.P,
                        g.pre_off + (step % g.n_pre) * g.hp - g.up_off, rtx};
         // transposed-conv upsampling of the source stack: channels 1..C
         {
@@ -3031,7 +3040,7 @@ extern "C" int ccmi_train_step(const ccmi_train_args *a, void *stream)
             if (g.K == 8 && A.d_lo == -2 && A.d_hi == 2) {
                 // the whole step, refine and transposed conv, in one launch (t_lvl_bwd)
                 const int tx = ccmi_div_up(wd, 64), ty = ccmi_div_up(A.hs, 16);
-                const UpBwd Q{GY, gys, S, ss, A, kf, g.kfull, koff, GSd, gss, k == g.L - 1 ? 1 : 0, slots, (int64_t)nreg,
+                const UpBwd Q{GY, gys, S, ss, A, kf, g.kfull, koff, GSd, gss, k == g.L - 1 ? 1 : 0, uslots, (int64_t)g.P,
                               hoff - g.up_off, tx, ty};
                 const dim3 grid((unsigned)(nref + tx * ty * C), B);
                 switch (g.Kp) {
@@ -3056,9 +3065,9 @@ extern "C" int ccmi_train_step(const ccmi_train_args *a, void *stream)
             hipLaunchKernelGGL(t_up_gu, grid1(nu, B), dim3(kT), 0, s, GY, gys, A, kf, g.kfull, koff, GU, pl.tmp_per);
             const dim3 gr(dw_blocks((int64_t)C * hd * wd, 8), B); // measured: 8 items per thread beat 1 here
             switch (g.K) {
-            case 4: hipLaunchKernelGGL(t_up_dw<4>, gr, dim3(kT), 0, s, GY, gys, U, GU, pl.tmp_per, S, ss, A, slots, (int64_t)nreg, hoff - g.up_off); break;
-            case 6: hipLaunchKernelGGL(t_up_dw<6>, gr, dim3(kT), 0, s, GY, gys, U, GU, pl.tmp_per, S, ss, A, slots, (int64_t)nreg, hoff - g.up_off); break;
-            default: hipLaunchKernelGGL(t_up_dw<8>, gr, dim3(kT), 0, s, GY, gys, U, GU, pl.tmp_per, S, ss, A, slots, (int64_t)nreg, hoff - g.up_off); break;
+            case 4: hipLaunchKernelGGL(t_up_dw<4>, gr, dim3(kT), 0, s, GY, gys, U, GU, pl.tmp_per, S, ss, A, uslots, (int64_t)g.P, hoff - g.up_off); break;
+            case 6: hipLaunchKernelGGL(t_up_dw<6>, gr, dim3(kT), 0, s, GY, gys, U, GU, pl.tmp_per, S, ss, A, uslots, (int64_t)g.P, hoff - g.up_off); break;
+            default: hipLaunchKernelGGL(t_up_dw<8>, gr, dim3(kT), 0, s, GY, gys, U, GU, pl.tmp_per, S, ss, A, uslots, (int64_t)g.P, hoff - g.up_off); break;
             }
             hipLaunchKernelGGL(t_up_gs, grid1((int64_t)C * A.hs * A.ws, B), dim3(kT), 0, s, GU, pl.tmp_per, A, kf, g.kfull,
                                koff, GSd, gss, k == g.L - 1 ? 1 : 0);
@@ -3066,22 +3075,23 @@ extern "C" int ccmi_train_step(const ccmi_train_args *a, void *stream)
     }
     CCMI_HIP_CHECK(hipGetLastError());
 
-    hipLaunchKernelGGL(t_dw_fold, dim3((unsigned)ccmi_div_up(nreg, 64), B), dim3(64), 0, s, slots, nreg, Gth, GS, g.up_off);
 
     // ---- latent gradients, norm, Adam
     const unsigned nls = sum_blocks(GS, 4);
     CCMI_HIP_CHECK(join.wait());
+    // every parameter gradient (the ARM's from the side stream too) from its slot rows
+    hipLaunchKernelGGL(t_dw_fold, dim3((unsigned)ccmi_div_up(g.P, 64), B), dim3(64), 0, s, slots, g.P, Gth, GS, 0);
     hipLaunchKernelGGL(t_latgrad_sumsq, dim3(nls, B), dim3(kT), 0, s, gq, side ? F(pl.gq_arm) : nullptr, dq, g.N, G, GS,
                        GS, acc4);
     const float total = a->yuv420 ? (float)(npx + 2 * (int64_t)(g.H / 2) * (g.W / 2)) : (float)(3 * npx);
     if (a->loss_out && !a->update)
-        hipLaunchKernelGGL(t_finish, dim3(1), dim3(std::max(64, B)), 0, s, acc4, 1.f / total, lam_px, a->loss_out, B);
+        hipLaunchKernelGGL(t_finish, dim3(1), dim3(std::max(64, B)), 0, s, acc4, F(pl.rslots), 1.f / total, lam_px, a->loss_out, B);
     if (a->update) {
         const double bc1 = 1.0 - std::pow((double)a->beta1, a->step), bc2 = 1.0 - std::pow((double)a->beta2, a->step);
         AdamArgs A{(float)(a->lr / bc1), (float)(1.0 / std::sqrt(bc2)), a->beta1, a->beta2, a->eps, a->clip, g.N,
                    a->update == 2 ? 1 : 0, GS, GS,
                    a->latent_stride, a->param_stride, (int64_t)a->latent_stride + a->param_stride, nullptr,
-                   a->loss_out, 1.f / total, lam_px};
+                   a->loss_out, F(pl.rslots), 1.f / total, lam_px};
         if (a->adam_steps) {
             A.bc = F(pl.bc);
             hipLaunchKernelGGL(t_adam_bc, dim3((unsigned)ccmi_div_up(B, 64)), dim3(64), 0, s, a->adam_steps, (double)a->lr,
