@@ -56,8 +56,12 @@ def _targets():
     k01, bd = io.parse_ppm(out)
     assert bd == 8
     k01 = k01[0].float()  # [3, 512, 768]
+    out, = decode.decode_batch([(GOLDEN / "cool" / "kodim04-lmbda-00001.cool").read_bytes()], as_yuv=False)
+    k04, bd = io.parse_ppm(out)
+    assert bd == 8
     return {"kodim15_192x128": img[0].float(), "kodim01_768x512": k01.contiguous(),
-            "kodim01_crop512": k01[:, :512, :512].contiguous()}
+            "kodim01_crop512": k01[:, :512, :512].contiguous(),
+            "kodim04_512x768": k04[0].float().contiguous()}  # [3, 768, 512]: config 4's portrait batch
 
 
 def _ref(preset_file):
@@ -258,20 +262,32 @@ FULL_PSNR_MARGIN_DB = 0.15
 FULL_RATE_MARGIN = 0.04
 
 
+FULL_CASES = [
+    ("kodim01_768x512", "hop", 0.001),   # round 3
+    ("kodim01_768x512", "hop", 0.0004),  # round 4
+    ("kodim01_768x512", "hop", 0.004),   # round 4
+    ("kodim04_512x768", "hop", 0.001),   # round 5: config 4's portrait geometry batch
+    ("kodim01_768x512", "default", 0.001),  # round 5: the reference's default decoder (ARM 24,2; 40-wide head)
+]
+
+
 @pytest.mark.skipif(not (GOLDEN / "rd_reference_c3x_full.json").exists(), reason="full-schedule reference fixture absent")
-@pytest.mark.parametrize("lm", [0.001, 0.0004, 0.004])
-def test_c3x_full_schedule_matches_reference(lm, gpu):
-    """lambda 1e-3 (round 3), 4e-4 and 4e-3 (round 4): two full-schedule reference seeds each."""
+@pytest.mark.parametrize("image,arch_name,lm", FULL_CASES, ids=[f"{i}-{a}-{lm}" for i, a, lm in FULL_CASES])
+def test_c3x_full_schedule_matches_reference(image, arch_name, lm, gpu):
+    """kodim01 768x512 with the hop decoder at lambda 1e-3 (round 3), 4e-4 and 4e-3 (round 4), two
+    full-schedule reference seeds each; the portrait kodim04 512x768 (hop) and kodim01 with the
+    reference's default decoder at lambda 1e-3 (round 5)."""
     from ccmi import io, rd, train
     ref = json.loads((GOLDEN / "rd_reference_c3x_full.json").read_text())["runs"]
-    image = "kodim01_768x512"
-    ref = [r for r in ref if r["image"] == image and r["lmbda"] == lm and r["preset"] == "c3x"]
-    if lm != 0.001 and len(ref) < 2:
-        pytest.skip(f"full-schedule reference at lambda {lm} not generated yet")
-    assert len(ref) >= 2, "two reference seeds"
+    ref = [r for r in ref if r["image"] == image and r["lmbda"] == lm and r["preset"] == "c3x"
+           and r.get("arch", "hop") == arch_name]
+    if (image, arch_name, lm) != ("kodim01_768x512", "hop", 0.001) and not ref:
+        pytest.skip(f"full-schedule reference for {image} / {arch_name} at lambda {lm} not generated yet")
+    original = image == "kodim01_768x512" and arch_name == "hop"
+    assert len(ref) >= (2 if original else 1), "reference seeds"
     x = _targets()[image]
     H, W = x.shape[-2:]
-    arch = train.Arch(H, W, dim_arm=16, n_hidden=2, layers=HOP)
+    arch = train.Arch(H, W, **(DEFAULT_ARCH if arch_name == "default" else dict(dim_arm=16, n_hidden=2, layers=HOP)))
     tgt = io.to_target(x, "rgb").to(gpu)
     recs = rd.encode_points(tgt, H, W, (lm,), arch, yuv420=False, seeds=GPU_SEEDS, preset="c3x", scale=1.0,
                             name=image)
@@ -279,7 +295,7 @@ def test_c3x_full_schedule_matches_reference(lm, gpu):
     out.mkdir(exist_ok=True)
     f = out / "rd_gpu_c3x_full.json"
     prev = json.loads(f.read_text()) if f.exists() else {}
-    prev[f"{image}@{lm}"] = [r.as_dict() for r in recs]
+    prev[f"{image}@{lm}" + ("" if arch_name == "hop" else f"@{arch_name}")] = [r.as_dict() for r in recs]
     f.write_text(json.dumps(prev, indent=1))
     rp, rr, ri = [r["psnr_db"] for r in ref], [r["rate_bpp"] for r in ref], [r["iterations"] for r in ref]
     op = float(np.median([r.psnr_db for r in recs]))
@@ -287,7 +303,7 @@ def test_c3x_full_schedule_matches_reference(lm, gpu):
     its = int(np.median([r.iterations for r in recs]))
     tol_p = FULL_PSNR_MARGIN_DB
     tol_r = FULL_RATE_MARGIN
-    line = (f"{image} c3x full lambda {lm}: PSNR ref {np.mean(rp):.3f} ({min(rp):.3f}..{max(rp):.3f}) gpu median "
+    line = (f"{image} {arch_name} c3x full lambda {lm}: PSNR ref {np.mean(rp):.3f} ({len(rp)} seeds, {min(rp):.3f}..{max(rp):.3f}) gpu median "
             f"{op:.3f} (tol {tol_p:.2f}); rate ref {np.mean(rr):.4f} gpu {orr:.4f} (tol {tol_r:.2f}); iterations "
             f"ref {ri} gpu median {its} (min {min(r.iterations for r in recs)}, max {max(r.iterations for r in recs)})")
     print("\n" + line)
