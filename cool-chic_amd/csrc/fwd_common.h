@@ -33,6 +33,7 @@ struct FusedArgs {
     int hid;             // hidden width of a 2-layer head
     int head_mfma;       // 2-layer head on the f32 MFMA form (fwd_syn.hip, CCMI_HEAD_MFMA)
     int head_generic;    // never the unrolled 48-wide head (CCMI_HEAD_GENERIC, a test form)
+    int ntiles;          // windows per frame (the fused kernel's 1-D grid is ntiles x batch)
     int w0_off, b0_off, relu0;
     int w1_off, b1_off, relu1;
     int n_sp;            // 3x3 layers after the head

@@ -202,11 +202,18 @@ __global__ __launch_bounds__(kFThreads) __attribute__((amdgpu_waves_per_eu(fused
     constexpr bool kPadRec = CIN + 1 + CMID <= 12;
     auto hr = [](int f) constexpr { return kPadRec ? f + f / 3 : f; };
 
-    const int b = blockIdx.y;
+    // XCD-aware window order: workgroups are dealt round-robin over the 8 XCDs (block i and
+    // i + 8 share one, MI355X_MICROARCH.md "Workgroup dispatch"), so each XCD is given a
+    // contiguous run of windows (raster order, frame after frame): vertically adjacent windows,
+    // which re-read each other's halo rows, then run on one L2.  A bijection of [0, n) for any n.
+    const int nblk = gridDim.x, bi = blockIdx.x;
+    const int per = (nblk + 7) >> 3, rem = nblk & 7, xcd = bi & 7;
+    const int wt = (rem == 0 ? xcd * per : xcd * per - max(0, xcd - rem)) + (bi >> 3);
+    const int b = wt / A.ntiles, tile = wt - b * A.ntiles;
     const int halo = A.n_sp;
     const int TX = kRW - 2 * halo, TY = kRH - 2 * halo;
-    const int y0 = (blockIdx.x / A.tiles_x) * TY;
-    const int x0 = (blockIdx.x % A.tiles_x) * TX;
+    const int y0 = (tile / A.tiles_x) * TY;
+    const int x0 = (tile % A.tiles_x) * TX;
     const int oy = y0 - halo, ox = x0 - halo; // global coords of window (0,0)
     const cfloat_ptr prm = (cfloat_ptr)(size_t)(A.params + (int64_t)b * A.pstride);
     const float *in = A.in + (int64_t)b * A.in_stride;
@@ -1116,7 +1123,8 @@ int ccmi_launch_syn_f32(const ccmi_syn_args *a, hipStream_t s)
         P.fa.out_stride = a->out_stride;
         const int halo = P.fa.n_sp;
         P.fa.tiles_x = ccmi_div_up(a->w, kRW - 2 * halo);
-        dim3 grid(P.fa.tiles_x * ccmi_div_up(a->h, kRH - 2 * halo), a->batch);
+        P.fa.ntiles = P.fa.tiles_x * ccmi_div_up(a->h, kRH - 2 * halo);
+        dim3 grid((unsigned)(P.fa.ntiles * a->batch));
         if (P.cmid == 3) launch_fused<3, false>(grid, s, P.fa, LevelArgs{});
         else launch_fused<4, false>(grid, s, P.fa, LevelArgs{});
         CCMI_HIP_CHECK(hipGetLastError());
@@ -1200,7 +1208,8 @@ extern "C" int ccmi_decode_forward_f32(const ccmi_decode_args *a, void *stream)
     P.fa.head_generic = a->head == CCMI_HEAD_GENERIC;
     const int halo = P.fa.n_sp;
     P.fa.tiles_x = ccmi_div_up(y.w, kRW - 2 * halo);
-    dim3 grid(P.fa.tiles_x * ccmi_div_up(y.h, kRH - 2 * halo), y.batch);
+    P.fa.ntiles = P.fa.tiles_x * ccmi_div_up(y.h, kRH - 2 * halo);
+    dim3 grid((unsigned)(P.fa.ntiles * y.batch));
     if (P.cmid == 3) {
         if (!launch_fused_mfma_head<3>(grid, s, P.fa, last)) launch_fused<3, true>(grid, s, P.fa, last);
     } else if (!launch_fused_mfma_head<4>(grid, s, P.fa, last)) {
