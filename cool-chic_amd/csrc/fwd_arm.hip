@@ -88,8 +88,15 @@ __global__ __launch_bounds__(kThreads) void arm_fwd_kernel(
 {
     __shared__ float tile[kLH][kLW];
 
-    const int b = blockIdx.y;
-    const int t = blockIdx.x;
+    // XCD-aware tile order (as the fused synthesis kernel): workgroup i runs on XCD i % 8, so
+    // each XCD takes a contiguous run of tiles (frame after frame) and vertically adjacent
+    // tiles, which share the 4 causal halo rows, meet in one L2.  A bijection of [0, n).
+    const int nblk = gridDim.x, bi = blockIdx.x;
+    const int per = (nblk + 7) >> 3, rem = nblk & 7, xcd = bi & 7;
+    const int wt = (rem == 0 ? xcd * per : xcd * per - max(0, xcd - rem)) + (bi >> 3);
+    const int ntl = g.tile_start[g.n];
+    const int b = wt / ntl;
+    const int t = wt - b * ntl;
     int l = 0;
 #pragma unroll
     for (int k = 1; k < CCMI_MAX_GRIDS; ++k)
@@ -315,7 +322,7 @@ int ccmi_launch_arm_f32(const ccmi_arm_args *a, hipStream_t s)
     g.tile_start[a->n_grids] = tiles;
     if ((a->latent_stride != 0 && a->latent_stride < off) || a->out_stride < off)
         return ccmi_set_error(CCMI_ERR_ARG, "arm: stride smaller than the %d latents of a frame", off);
-    dim3 grid(tiles, a->batch);
+    dim3 grid((unsigned)(tiles * a->batch));
 #define CCMI_ARM_LAUNCH(DD)                                                                                     \
     hipLaunchKernelGGL(arm_fwd_kernel<DD>, grid, dim3(kThreads), 0, s, a->latent, a->latent_stride, g, a->gain, \
                        a->quantize, a->n_hidden, a->params, a->param_stride, a->mu, a->scale, a->log_scale,     \
