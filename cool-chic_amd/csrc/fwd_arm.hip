@@ -88,12 +88,9 @@ __global__ __launch_bounds__(kThreads) void arm_fwd_kernel(
 {
     __shared__ float tile[kLH][kLW];
 
-    // XCD-aware tile order (as the fused synthesis kernel): workgroup i runs on XCD i % 8, so
-    // each XCD takes a contiguous run of tiles (frame after frame) and vertically adjacent
-    // tiles, which share the 4 causal halo rows, meet in one L2.  A bijection of [0, n).
-    const int nblk = gridDim.x, bi = blockIdx.x;
-    const int per = (nblk + 7) >> 3, rem = nblk & 7, xcd = bi & 7;
-    const int wt = (rem == 0 ? xcd * per : xcd * per - max(0, xcd - rem)) + (bi >> 3);
+    // XCD-aware tile order (ccmi_fwd::xcd_order): vertically adjacent tiles, which share the
+    // 4 causal halo rows, meet in one L2
+    const int wt = ccmi_fwd::xcd_order(blockIdx.x, gridDim.x);
     const int ntl = g.tile_start[g.n];
     const int b = wt / ntl;
     const int t = wt - b * ntl;

@@ -14,6 +14,17 @@ typedef const __attribute__((address_space(4))) float *cfloat_ptr;
 
 __device__ __forceinline__ int clampi(int v, int hi) { return v < 0 ? 0 : (v > hi ? hi : v); }
 
+// XCD-aware workgroup order for a 1-D grid of n workgroups: the dispatcher deals workgroups
+// round-robin over the 8 XCDs (block i and i + 8 share one, MI355X_MICROARCH.md "Workgroup
+// dispatch"), so block i is given work item xcd_order(i, n), which hands each XCD a contiguous
+// run of items: neighbouring tiles, which re-read each other's halos, then meet in one L2.
+// A bijection of [0, n) for any n.
+__device__ __forceinline__ int xcd_order(int i, int n)
+{
+    const int per = (n + 7) >> 3, rem = n & 7, xcd = i & 7;
+    return (rem == 0 ? xcd * per : xcd * per - max(0, xcd - rem)) + (i >> 3);
+}
+
 // ---------------------------------------------------------------- synthesis plan
 constexpr int kMaxIn = 8;    // fused path: max synthesis input channels
 constexpr int kMaxMid = 4;   // fused path: max channels through the 3x3 layers

@@ -202,13 +202,9 @@ __global__ __launch_bounds__(kFThreads) __attribute__((amdgpu_waves_per_eu(fused
     constexpr bool kPadRec = CIN + 1 + CMID <= 12;
     auto hr = [](int f) constexpr { return kPadRec ? f + f / 3 : f; };
 
-    // XCD-aware window order: workgroups are dealt round-robin over the 8 XCDs (block i and
-    // i + 8 share one, MI355X_MICROARCH.md "Workgroup dispatch"), so each XCD is given a
-    // contiguous run of windows (raster order, frame after frame): vertically adjacent windows,
-    // which re-read each other's halo rows, then run on one L2.  A bijection of [0, n) for any n.
-    const int nblk = gridDim.x, bi = blockIdx.x;
-    const int per = (nblk + 7) >> 3, rem = nblk & 7, xcd = bi & 7;
-    const int wt = (rem == 0 ? xcd * per : xcd * per - max(0, xcd - rem)) + (bi >> 3);
+    // XCD-aware window order (raster order, frame after frame, a contiguous run per XCD):
+    // vertically adjacent windows re-read each other's halo rows from one L2
+    const int wt = xcd_order(blockIdx.x, gridDim.x);
     const int b = wt / A.ntiles, tile = wt - b * A.ntiles;
     const int halo = A.n_sp;
     const int TX = kRW - 2 * halo, TY = kRH - 2 * halo;

@@ -1085,9 +1085,13 @@ constexpr int kSpRows = 4;
 __global__ __launch_bounds__(kT) void t_sp_fwd(const float *__restrict__ in, Geo g, const float *__restrict__ th, int64_t ps,
                                                int wo, int bo, int res, int relu, float *__restrict__ out)
 {
-    const int b = blockIdx.y;
+    // 1-D grid of (blocks per frame) x frames in XCD-aware order: the row groups above and below,
+    // which load 2 of the same rows, run on one L2
+    const int per = (((g.H + kSpRows - 1) / kSpRows) * g.W + kT - 1) / kT; // blocks per frame
+    const int wt = ccmi_fwd::xcd_order(blockIdx.x, gridDim.x);
+    const int b = wt / per;
     const int64_t npx = (int64_t)g.H * g.W;
-    const int q = blockIdx.x * kT + threadIdx.x; // (row group, column); a frame fits 31 bits
+    const int q = (wt - b * per) * kT + threadIdx.x; // (row group, column); a frame fits 31 bits
     const int gy = q / g.W, px = q - gy * g.W, y0 = gy * kSpRows;
     if (y0 >= g.H) return;
     const cfloat_ptr P = (cfloat_ptr)(size_t)(th + (int64_t)b * ps);
@@ -1933,7 +1937,7 @@ constexpr int ref_bwd_lds()
 }
 // tile bx of the level (blockIdx.x of its own launch, or of the combined t_lvl_bwd)
 template <int KP>
-__device__ __forceinline__ void ref_bwd_tile(float *pool, int bx, const RefBwd &R)
+__device__ __forceinline__ void ref_bwd_tile(float *pool, int bx, int b, const RefBwd &R)
 {
     constexpr int P = KP / 2, TY = 16, TX = 64, SY = TY + 2 * P, SX = TX + 2 * P;
     float(*sx)[SX] = reinterpret_cast<float(*)[SX]>(pool);
@@ -1944,7 +1948,7 @@ __device__ __forceinline__ void ref_bwd_tile(float *pool, int bx, const RefBwd &
     const int64_t gys = R.gys, xs = R.xs, gxs = R.gxs, gstride = R.gstride;
     const int h = R.h, w = R.w, kstride = R.kstride, koff = R.koff, hoff = R.hoff, tiles_x = R.tiles_x;
     float *GX = R.GX, *slots = R.slots;
-    const int b = blockIdx.y, tid = threadIdx.x;
+    const int tid = threadIdx.x;
     const int ty0 = (bx / tiles_x) * TY, tx0 = (bx % tiles_x) * TX;
     const float *wk = kf + (int64_t)b * kstride + koff;
     float wv[KP];
@@ -2012,7 +2016,7 @@ template <int KP>
 __global__ __launch_bounds__(kT) void t_ref_bwd(RefBwd R)
 {
     __shared__ __attribute__((aligned(16))) float pool[ref_bwd_lds<KP>()];
-    ref_bwd_tile<KP>(pool, blockIdx.x, R);
+    ref_bwd_tile<KP>(pool, blockIdx.x, blockIdx.y, R);
 }
 
 __device__ __forceinline__ int up_tap(int a, int d, int K) { return a + K / 2 - 1 - 2 * d; }
@@ -2166,6 +2170,7 @@ struct UpBwd {
     float *slots;
     int64_t gstride;
     int hoff, tiles_x, tiles_y;
+    int batch; // frames (t_lvl_bwd's 1-D grid)
 };
 template <int K>
 constexpr int up_bwd_lds()
@@ -2174,7 +2179,7 @@ constexpr int up_bwd_lds()
     return (TR + DW) * (TM + DW) + (TR + DW) * TX + 2 * (TR + DW) * (TX + 2 * DW) + TR * (TX + 2 * DW);
 }
 template <int K>
-__device__ __forceinline__ void up_bwd_tile(float *pool, int bx, const UpBwd &Q)
+__device__ __forceinline__ void up_bwd_tile(float *pool, int bx, int b, const UpBwd &Q)
 {
     constexpr int K2 = K / 2, DLO = -((K2 + 1) / 2), DHI = K2 / 2, DW = DHI - DLO;
     constexpr int TR = 16, TX = 64, TM = TX / 2;
@@ -2190,7 +2195,7 @@ __device__ __forceinline__ void up_bwd_tile(float *pool, int bx, const UpBwd &Q)
     const int kstride = Q.kstride, koff = Q.koff, accumulate = Q.accumulate, hoff = Q.hoff;
     const int tiles_x = Q.tiles_x, tiles_y = Q.tiles_y;
     float *GS = Q.GS, *slots = Q.slots;
-    const int b = blockIdx.y, tid = threadIdx.x;
+    const int tid = threadIdx.x;
     const int tile = bx % (tiles_x * tiles_y), c = bx / (tiles_x * tiles_y);
     const int r0 = (tile / tiles_x) * TR, x0 = (tile % tiles_x) * TX, m0 = x0 / 2;
     const int gy0 = 2 * (r0 - DHI), gx0 = x0 - 2 * DHI; // GY / GU tile origin
@@ -2367,14 +2372,18 @@ __global__ __launch_bounds__(kT) void t_lvl_bwd(RefBwd R, UpBwd Q, int nref)
 {
     constexpr int n = ref_bwd_lds<KP>() > up_bwd_lds<K>() ? ref_bwd_lds<KP>() : up_bwd_lds<K>();
     __shared__ __attribute__((aligned(16))) float pool[n];
+    // 1-D grid of (nref + up tiles) x frames in XCD-aware order (neighbouring tiles share their
+    // halos through one L2)
+    const int per = gridDim.x / Q.batch, wt = ccmi_fwd::xcd_order(blockIdx.x, gridDim.x);
+    const int b = wt / per, bx = wt - b * per;
 #if defined(CCMI_DIAG_LVL_NOREF) // diagnostic builds only (tools/arm_diag.sh): wrong results
-    if ((int)blockIdx.x < nref) return;
+    if (bx < nref) return;
 #endif
 #if defined(CCMI_DIAG_LVL_NOUP)
-    if ((int)blockIdx.x >= nref) return;
+    if (bx >= nref) return;
 #endif
-    if ((int)blockIdx.x < nref) ref_bwd_tile<KP>(pool, blockIdx.x, R);
-    else up_bwd_tile<K>(pool, blockIdx.x - nref, Q);
+    if (bx < nref) ref_bwd_tile<KP>(pool, bx, b, R);
+    else up_bwd_tile<K>(pool, bx - nref, b, Q);
 }
 
 // ------------------------------------------------------------------ latents, norm, Adam
@@ -2960,7 +2969,7 @@ extern "C" int ccmi_train_step(const ccmi_train_args *a, void *stream)
     head_dispatch(g.L, false, dim3((unsigned)((npx + 2 * kT - 1) / (2 * kT)), (unsigned)B), s, dense, nullptr, g, a->params,
                   a->param_stride, F(pl.z[0]), nullptr, 0); // two pixels per thread
     for (int i = 0; i < g.n_sp; ++i)
-        hipLaunchKernelGGL(t_sp_fwd, grid1((int64_t)ccmi_div_up(g.H, kSpRows) * g.W, B), dim3(kT), 0, s, F(pl.z[i]), g, a->params, a->param_stride, g.sp_w[i],
+        hipLaunchKernelGGL(t_sp_fwd, dim3(grid1((int64_t)ccmi_div_up(g.H, kSpRows) * g.W, 1).x * B), dim3(kT), 0, s, F(pl.z[i]), g, a->params, a->param_stride, g.sp_w[i],
                            g.sp_b[i], g.sp_res[i], g.sp_relu[i], F(pl.z[i + 1]));
     if (a->raw_out)
         CCMI_HIP_CHECK(hipMemcpyAsync(a->raw_out, F(pl.z[g.n_sp]), sizeof(float) * 3 * npx * B, hipMemcpyDeviceToDevice, s));
@@ -3041,8 +3050,8 @@ extern "C" int ccmi_train_step(const ccmi_train_args *a, void *stream)
                 // the whole step, refine and transposed conv, in one launch (t_lvl_bwd)
                 const int tx = ccmi_div_up(wd, 64), ty = ccmi_div_up(A.hs, 16);
                 const UpBwd Q{GY, gys, S, ss, A, kf, g.kfull, koff, GSd, gss, k == g.L - 1 ? 1 : 0, uslots, (int64_t)g.P,
-                              hoff - g.up_off, tx, ty};
-                const dim3 grid((unsigned)(nref + tx * ty * C), B);
+                              hoff - g.up_off, tx, ty, B};
+                const dim3 grid((unsigned)((nref + tx * ty * C) * B));
                 switch (g.Kp) {
                 case 1: hipLaunchKernelGGL((t_lvl_bwd<1, 8>), grid, dim3(kT), 0, s, R, Q, nref); break;
                 case 3: hipLaunchKernelGGL((t_lvl_bwd<3, 8>), grid, dim3(kT), 0, s, R, Q, nref); break;
