@@ -1081,9 +1081,16 @@ __global__ __launch_bounds__(kT) void t_head_fwd(const float *__restrict__ dense
 // computes kSpRows vertically consecutive pixels of one column: the rows it reads overlap, so
 // it loads (kSpRows + 2) x 3 neighbours per channel instead of 9 per pixel (one pixel per
 // thread issued 27 loads per pixel); same FMA order per pixel.
+// LOSS (the last layer of a training step): t_loss's MSE fused in -- the layer's output is
+// consumed where it is produced (its gradient graw, the squared errors into the frame's mse
+// slots) and stored only when store_out (a ReLU's mask for the backward, or the caller's raw
+// output).  1: 444 target; 2: 420 target (chroma at even rows / columns, frame.py:175-183).
 constexpr int kSpRows = 4;
+template <int LOSS>
 __global__ __launch_bounds__(kT) void t_sp_fwd(const float *__restrict__ in, Geo g, const float *__restrict__ th, int64_t ps,
-                                               int wo, int bo, int res, int relu, float *__restrict__ out)
+                                               int wo, int bo, int res, int relu, float *__restrict__ out,
+                                               const float *__restrict__ tgt, int64_t tstride, float k2,
+                                               float *__restrict__ graw, float *__restrict__ mslots, int store_out)
 {
     // 1-D grid of (blocks per frame) x frames in XCD-aware order: the row groups above and below,
     // which load 2 of the same rows, run on one L2
@@ -1093,36 +1100,62 @@ __global__ __launch_bounds__(kT) void t_sp_fwd(const float *__restrict__ in, Geo
     const int64_t npx = (int64_t)g.H * g.W;
     const int q = (wt - b * per) * kT + threadIdx.x; // (row group, column); a frame fits 31 bits
     const int gy = q / g.W, px = q - gy * g.W, y0 = gy * kSpRows;
-    if (y0 >= g.H) return;
-    const cfloat_ptr P = (cfloat_ptr)(size_t)(th + (int64_t)b * ps);
-    const float *x = in + (int64_t)b * 3 * npx;
-    int xo[3];
+    float se = 0.f;
+    if (y0 < g.H) { // (no early return: the fused loss's block reduction needs every thread)
+        const cfloat_ptr P = (cfloat_ptr)(size_t)(th + (int64_t)b * ps);
+        const float *x = in + (int64_t)b * 3 * npx;
+        int xo[3];
 #pragma unroll
-    for (int d = 0; d < 3; ++d) xo[d] = clampi(px + d - 1, g.W - 1);
-    float v[3][kSpRows + 2][3];
+        for (int d = 0; d < 3; ++d) xo[d] = clampi(px + d - 1, g.W - 1);
+        float v[3][kSpRows + 2][3];
 #pragma unroll
-    for (int i = 0; i < 3; ++i)
+        for (int i = 0; i < 3; ++i)
 #pragma unroll
-        for (int r = 0; r < kSpRows + 2; ++r) {
-            const float *row = x + i * npx + (int64_t)clampi(y0 + r - 1, g.H - 1) * g.W;
+            for (int r = 0; r < kSpRows + 2; ++r) {
+                const float *row = x + i * npx + (int64_t)clampi(y0 + r - 1, g.H - 1) * g.W;
 #pragma unroll
-            for (int d = 0; d < 3; ++d) v[i][r][d] = row[xo[d]];
+                for (int d = 0; d < 3; ++d) v[i][r][d] = row[xo[d]];
+            }
+        const int64_t pix = (int64_t)y0 * g.W + px;
+        float *o = out + (int64_t)b * 3 * npx + pix;
+        const int h2 = g.H / 2, w2 = g.W / 2;
+#pragma unroll
+        for (int t = 0; t < kSpRows; ++t) {
+            if (y0 + t >= g.H) break;
+#pragma unroll
+            for (int c = 0; c < 3; ++c) {
+                float a = P[bo + c];
+#pragma unroll
+                for (int i = 0; i < 3; ++i)
+#pragma unroll
+                    for (int k = 0; k < 9; ++k) a = fmaf(P[wo + (c * 3 + i) * 9 + k], v[i][t + k / 3][k % 3], a);
+                if (res) a += v[c][t + 1][1];
+                if (relu) a = fmaxf(a, 0.f);
+                const int64_t e = c * npx + (int64_t)t * g.W;
+                if (LOSS == 0 || store_out) o[e] = a;
+                if constexpr (LOSS > 0) { // t_loss on this pixel, same arithmetic
+                    const int y = y0 + t;
+                    bool used = true;
+                    int64_t ti = c * npx + (int64_t)y * g.W + px;
+                    if (LOSS == 2 && c > 0) {
+                        used = (y % 2 == 0) && (px % 2 == 0) && (y / 2) < h2 && (px / 2) < w2;
+                        ti = npx + (int64_t)(c - 1) * h2 * w2 + (int64_t)(y / 2) * w2 + px / 2;
+                    }
+                    float gv = 0.f;
+                    if (used) {
+                        const float vc = fminf(fmaxf(a, 0.f), 1.f), d = vc - tgt[(int64_t)b * tstride + ti];
+                        se += d * d;
+                        gv = (a >= 0.f && a <= 1.f) ? k2 * d : 0.f;
+                    }
+                    graw[(int64_t)b * 3 * npx + e + pix] = gv;
+                }
+            }
         }
-    float *o = out + (int64_t)b * 3 * npx + (int64_t)y0 * g.W + px;
-#pragma unroll
-    for (int t = 0; t < kSpRows; ++t) {
-        if (y0 + t >= g.H) break;
-#pragma unroll
-        for (int c = 0; c < 3; ++c) {
-            float a = P[bo + c];
-#pragma unroll
-            for (int i = 0; i < 3; ++i)
-#pragma unroll
-                for (int k = 0; k < 9; ++k) a = fmaf(P[wo + (c * 3 + i) * 9 + k], v[i][t + k / 3][k % 3], a);
-            if (res) a += v[c][t + 1][1];
-            if (relu) a = fmaxf(a, 0.f);
-            o[c * npx + (int64_t)t * g.W] = a;
-        }
+    }
+    if constexpr (LOSS > 0) {
+        __shared__ float s_red[8];
+        const float sum = block_sum(se, s_red);
+        if (threadIdx.x == 0) atomicAdd(&mslots[b * kDwSlots + blockIdx.x % kDwSlots], sum);
     }
 }
 
@@ -2434,7 +2467,7 @@ struct AdamArgs {
     int64_t n, gstride, ls, ps, ms;
     const float *bc; // optional [B][2] per-frame (lr / bc1, 1 / sqrt(bc2)) (per-frame Adam steps)
     float *loss_out; // optional [B][4]: t_finish's row, written by workgroup (0, b)
-    const float *rslots;
+    const float *rslots, *mslots;
     float inv_total, lam_px;
 };
 
@@ -2459,13 +2492,19 @@ __global__ void t_adam_bc(const int32_t *__restrict__ steps, double lr, double b
 }
 
 // torch.optim.Adam (_single_tensor_adam, no weight decay / amsgrad) after clip_grad_norm_
-__device__ __forceinline__ void finish_row(const float *__restrict__ acc4, const float *__restrict__ rslots, float inv_total,
-                                           float lam_px, float *__restrict__ out, int b)
+// rslots: [B][kDwSlots] rate sums; mslots: [B][kDwSlots] squared-error sums of the loss fused
+// into the last t_sp_fwd (zero when t_loss ran: it adds into acc4[b][0])
+__device__ __forceinline__ void finish_row(const float *__restrict__ acc4, const float *__restrict__ rslots,
+                                           const float *__restrict__ mslots, float inv_total, float lam_px,
+                                           float *__restrict__ out, int b)
 {
-    float rate = 0.f;
+    float rate = 0.f, sq = acc4[b * 4 + 0];
 #pragma unroll 8
-    for (int k = 0; k < kDwSlots; ++k) rate += rslots[b * kDwSlots + k];
-    const float mse = acc4[b * 4 + 0] * inv_total;
+    for (int k = 0; k < kDwSlots; ++k) {
+        rate += rslots[b * kDwSlots + k];
+        sq += mslots[b * kDwSlots + k];
+    }
+    const float mse = sq * inv_total;
     out[b * 4 + 0] = mse + lam_px * rate;
     out[b * 4 + 1] = mse;
     out[b * 4 + 2] = rate;
@@ -2476,7 +2515,7 @@ __global__ void t_adam(const float *__restrict__ G, float *__restrict__ lat, flo
 {
     const int b = blockIdx.y;
     const int64_t i = (int64_t)blockIdx.x * kT + threadIdx.x;
-    if (A.loss_out && i == 0) finish_row(acc4, A.rslots, A.inv_total, A.lam_px, A.loss_out, b); // (t_finish folded in)
+    if (A.loss_out && i == 0) finish_row(acc4, A.rslots, A.mslots, A.inv_total, A.lam_px, A.loss_out, b); // (t_finish folded in)
     if (i >= A.n || (A.latents_only && i >= A.N)) return;
     if (A.bc && A.bc[2 * b + 1] < 0.f) return; // frozen frame (adam_steps <= 0)
     float coef = 1.f;
@@ -2493,11 +2532,11 @@ __global__ void t_adam(const float *__restrict__ G, float *__restrict__ lat, flo
     *p -= lr_bc1 * mm / denom;
 }
 
-__global__ void t_finish(const float *__restrict__ acc4, const float *__restrict__ rslots, float inv_total, float lam_px,
-                         float *__restrict__ out, int B)
+__global__ void t_finish(const float *__restrict__ acc4, const float *__restrict__ rslots, const float *__restrict__ mslots,
+                         float inv_total, float lam_px, float *__restrict__ out, int B)
 {
     const int b = threadIdx.x;
-    if (b < B) finish_row(acc4, rslots, inv_total, lam_px, out, b);
+    if (b < B) finish_row(acc4, rslots, mslots, inv_total, lam_px, out, b);
 }
 
 // ------------------------------------------------------------------ host planning
@@ -2530,7 +2569,7 @@ struct Plan {
     // workspace offsets (bytes)
     size_t gq_arm = 0; // the ARM's latent gradients when it runs on the side stream (CCMI_ARM_OVERLAP)
     size_t yq, dq, gq, kf, stacks, stacks_bytes, dense, z[kMaxSp + 1], graw, gbuf[2], gdense, gstack, tmpU, tmpG, G,
-        acc4, bc, rslots, slots, total;
+        acc4, bc, rslots, mslots, slots, total;
     int64_t gstack_off[CCMI_MAX_GRIDS]; // per level k (1..L-2) inside gstack, elements per frame
     int64_t gstack_per, stack_per, tmp_per;
 };
@@ -2662,6 +2701,7 @@ int make_plan(const ccmi_train_args *a, Plan &pl)
     pl.acc4 = take(4 * B * 4);
     pl.bc = take(4 * B * 2);
     pl.rslots = take(4 * B * kDwSlots);
+    pl.mslots = take(4 * B * kDwSlots); // the fused loss's squared-error sums
     // every parameter's gradient through kDwSlots slot rows per frame (one row per workgroup
     // residue), folded into the gradient row by t_dw_fold (kDwSlots)
     pl.slots = take(4 * B * kDwSlots * (size_t)g.P);
@@ -2968,9 +3008,23 @@ extern "C" int ccmi_train_step(const ccmi_train_args *a, void *stream)
     }
     head_dispatch(g.L, false, dim3((unsigned)((npx + 2 * kT - 1) / (2 * kT)), (unsigned)B), s, dense, nullptr, g, a->params,
                   a->param_stride, F(pl.z[0]), nullptr, 0); // two pixels per thread
-    for (int i = 0; i < g.n_sp; ++i)
-        hipLaunchKernelGGL(t_sp_fwd, dim3(grid1((int64_t)ccmi_div_up(g.H, kSpRows) * g.W, 1).x * B), dim3(kT), 0, s, F(pl.z[i]), g, a->params, a->param_stride, g.sp_w[i],
-                           g.sp_b[i], g.sp_res[i], g.sp_relu[i], F(pl.z[i + 1]));
+    // the training step's MSE fused into the last 3x3 layer (no separate t_loss pass over the
+    // synthesis output); the output itself is stored only when something reads it
+    const bool fuse_loss = !a->forward_only && !a->grad_raw && g.n_sp > 0;
+    for (int i = 0; i < g.n_sp; ++i) {
+        const bool fl = fuse_loss && i == g.n_sp - 1;
+        const int store = !fl || a->raw_out || g.sp_relu[i];
+        const dim3 grid(grid1((int64_t)ccmi_div_up(g.H, kSpRows) * g.W, 1).x * B);
+        const float total = a->yuv420 ? (float)(npx + 2 * (int64_t)(g.H / 2) * (g.W / 2)) : (float)(3 * npx);
+        auto launch = [&](auto LOSS) {
+            hipLaunchKernelGGL((t_sp_fwd<decltype(LOSS)::value>), grid, dim3(kT), 0, s, F(pl.z[i]), g, a->params, a->param_stride,
+                               g.sp_w[i], g.sp_b[i], g.sp_res[i], g.sp_relu[i], F(pl.z[i + 1]), a->target, a->target_stride,
+                               2.f / total, graw, F(pl.mslots), store);
+        };
+        if (!fl) launch(std::integral_constant<int, 0>{});
+        else if (a->yuv420) launch(std::integral_constant<int, 2>{});
+        else launch(std::integral_constant<int, 1>{});
+    }
     if (a->raw_out)
         CCMI_HIP_CHECK(hipMemcpyAsync(a->raw_out, F(pl.z[g.n_sp]), sizeof(float) * 3 * npx * B, hipMemcpyDeviceToDevice, s));
     if (a->forward_only) {
@@ -2983,14 +3037,14 @@ extern "C" int ccmi_train_step(const ccmi_train_args *a, void *stream)
                 hipLaunchKernelGGL(t_loss, dim3(sum_blocks(npx, kLossPx), B), dim3(kT), 0, s, F(pl.z[g.n_sp]), g,
                                    a->target, a->target_stride, a->yuv420, graw, acc4);
             const float total = a->yuv420 ? (float)(npx + 2 * (int64_t)(g.H / 2) * (g.W / 2)) : (float)(3 * npx);
-            hipLaunchKernelGGL(t_finish, dim3(1), dim3(std::max(64, B)), 0, s, acc4, F(pl.rslots), 1.f / total, lam_px, a->loss_out, B);
+            hipLaunchKernelGGL(t_finish, dim3(1), dim3(std::max(64, B)), 0, s, acc4, F(pl.rslots), F(pl.mslots), 1.f / total, lam_px, a->loss_out, B);
         }
         CCMI_HIP_CHECK(hipGetLastError());
         return CCMI_OK;
     }
     if (a->grad_raw) // the caller's d loss / d raw output (autograd); no built-in MSE term
         CCMI_HIP_CHECK(hipMemcpyAsync(graw, a->grad_raw, sizeof(float) * 3 * npx * B, hipMemcpyDeviceToDevice, s));
-    else
+    else if (!fuse_loss)
         hipLaunchKernelGGL(t_loss, dim3(sum_blocks(npx, kLossPx), B), dim3(kT), 0, s, F(pl.z[g.n_sp]), g, a->target, a->target_stride,
                            a->yuv420, graw, acc4);
 
@@ -3094,13 +3148,13 @@ extern "C" int ccmi_train_step(const ccmi_train_args *a, void *stream)
                        GS, acc4);
     const float total = a->yuv420 ? (float)(npx + 2 * (int64_t)(g.H / 2) * (g.W / 2)) : (float)(3 * npx);
     if (a->loss_out && !a->update)
-        hipLaunchKernelGGL(t_finish, dim3(1), dim3(std::max(64, B)), 0, s, acc4, F(pl.rslots), 1.f / total, lam_px, a->loss_out, B);
+        hipLaunchKernelGGL(t_finish, dim3(1), dim3(std::max(64, B)), 0, s, acc4, F(pl.rslots), F(pl.mslots), 1.f / total, lam_px, a->loss_out, B);
     if (a->update) {
         const double bc1 = 1.0 - std::pow((double)a->beta1, a->step), bc2 = 1.0 - std::pow((double)a->beta2, a->step);
         AdamArgs A{(float)(a->lr / bc1), (float)(1.0 / std::sqrt(bc2)), a->beta1, a->beta2, a->eps, a->clip, g.N,
                    a->update == 2 ? 1 : 0, GS, GS,
                    a->latent_stride, a->param_stride, (int64_t)a->latent_stride + a->param_stride, nullptr,
-                   a->loss_out, F(pl.rslots), 1.f / total, lam_px};
+                   a->loss_out, F(pl.rslots), F(pl.mslots), 1.f / total, lam_px};
         if (a->adam_steps) {
             A.bc = F(pl.bc);
             hipLaunchKernelGGL(t_adam_bc, dim3((unsigned)ccmi_div_up(B, 64)), dim3(64), 0, s, a->adam_steps, (double)a->lr,
