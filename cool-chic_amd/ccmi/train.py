@@ -40,7 +40,7 @@ class TrainArgs(C.Structure):
         ("noise_in", C.c_void_p), ("grad_out", C.c_void_p), ("loss_out", C.c_void_p), ("update", C.c_int),
         ("workspace", C.c_void_p), ("workspace_bytes", C.c_size_t),
         ("forward_only", C.c_int), ("raw_out", C.c_void_p), ("rate_out", C.c_void_p), ("grad_raw", C.c_void_p),
-        ("grad_rate", C.c_void_p), ("adam_steps", C.c_void_p),
+        ("grad_rate", C.c_void_p), ("adam_steps", C.c_void_p), ("step_counters", C.c_void_p),
     ]
 
 
@@ -217,7 +217,7 @@ class Overfitter:
         a = self._args()
         if update:
             self.t += 1
-            self.steps += 1
+            a.step_counters = self.steps.data_ptr()  # self.steps += 1, inside the step's prologue
             if not self.steps_uniform:
                 a.adam_steps = self.steps.data_ptr()
         a.adam_m, a.adam_v = self.m.data_ptr(), self.v.data_ptr()

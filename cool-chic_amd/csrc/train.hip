@@ -101,11 +101,13 @@ __device__ __forceinline__ float block_sum(float v, float *red)
 // ------------------------------------------------------------------ parameters
 // Per-step prologue in one launch (three launches before: a memset, t_zero_rows, t_expand --
 // each a dependent dispatch of ~6 us on the step's critical path, profiles/r5l_train_timeline.txt):
-// zero nz floats from z (acc4, the rate and parameter-gradient slots, the ARM's side gradient)
-// and expand the symmetric upsampling kernels.
+// zero nz floats from z (acc4, the rate and parameter-gradient slots, the ARM's side gradient),
+// expand the symmetric upsampling kernels, and count the step in the caller's step counters.
 __global__ void t_prologue(float *__restrict__ z, int64_t nz, const float *__restrict__ th, int64_t ps, Geo g,
-                           float *__restrict__ kf, int B)
+                           float *__restrict__ kf, int B, int32_t *__restrict__ counters)
 {
+    if (counters && blockIdx.x == 0)
+        for (int i = threadIdx.x; i < B; i += kT) counters[i] += 1; // the caller's per-frame step counts
     const int64_t n = nz + (int64_t)B * g.kfull;
     for (int64_t i = (int64_t)blockIdx.x * kT + threadIdx.x; i < n; i += (int64_t)gridDim.x * kT) {
         if (i < nz) {
@@ -2940,7 +2942,8 @@ extern "C" int ccmi_train_step(const ccmi_train_args *a, void *stream)
         const int64_t nz = (int64_t)(pl.total - pl.acc4) / (int64_t)sizeof(float);
         const int64_t n = nz + (int64_t)B * g.kfull;
         const unsigned nb = (unsigned)std::max<int64_t>(1, std::min<int64_t>(ccmi_div_up(n, 4 * kT), 2048));
-        hipLaunchKernelGGL(t_prologue, dim3(nb), dim3(kT), 0, s, acc4, nz, a->params, a->param_stride, g, kf, B);
+        hipLaunchKernelGGL(t_prologue, dim3(nb), dim3(kT), 0, s, acc4, nz, a->params, a->param_stride, g, kf, B,
+                           a->update ? a->step_counters : nullptr);
     }
 
     // ---- forward

@@ -426,6 +426,10 @@ typedef struct ccmi_train_args {
                                `step`; a frame whose optimizer state was reloaded from its best
                                record, train.py:226-236); a step <= 0 leaves that frame unchanged:
                                neither its parameters nor its Adam moments are written */
+    int32_t *step_counters; /* optional device [batch]: +1 per frame at the start of an update
+                               step (the caller's per-frame step counts kept on the device without
+                               a launch of its own; may alias adam_steps, which then reads the
+                               incremented value) */
 } ccmi_train_args;
 size_t ccmi_train_param_count(const ccmi_train_args *args);
 size_t ccmi_train_workspace_bytes(const ccmi_train_args *args);
