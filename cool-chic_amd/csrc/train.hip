@@ -314,6 +314,11 @@ __device__ __forceinline__ void bcast_rows(float x, float (&bc)[4])
 // Lane l supplies A[m = l & 15][k = l >> 4] and B[k = l >> 4][n = l & 15]; accumulator
 // register r of lane l is D[m = 4 (l >> 4) + r][n = l & 15].
 __device__ __forceinline__ v4f mfma4(float a, float b, v4f c) { return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0); }
+// v_mfma_f32_4x4x1_16b_f32: sixteen independent 4x4 outer products, block bk = l >> 2.  Lane l
+// supplies A[bk][m = l & 3] and B[bk][n = l & 3]; accumulator register r of lane l is
+// D[bk][m = r][n = l & 3].  2 passes (8 cycles) against 16x16x4's 8 (32 cycles) at a quarter
+// of the MACs -- the same MAC rate, so a product whose M or N is 3-8 wide wastes less of it.
+__device__ __forceinline__ v4f mfma4x4(float a, float b, v4f c) { return __builtin_amdgcn_mfma_f32_4x4x1f32(a, b, c, 0, 0, 0); }
 
 // One layer's weight gradient over a wave's 64 rows, on the matrix cores:
 // acc[mt][nt] += G^T A, G = [64][R] (pitch R + 1, column R zero), A = [64][D] (pitch D + 1,
@@ -1711,6 +1716,9 @@ __global__ __launch_bounds__(kHeadT) void t_head_bwd(const float *__restrict__ d
 // (4 pixels) with one 128-bit read each (the 16 lanes of a read start 4 banks apart).
 // Per tile q: h -> dW1 tile (M = k < 3, N = the tile's units) -> g_h (the ReLU mask from the
 // registers) -> dW0 tile (M = the tile's units, N = i <= CIN) and this pixel's g_x.
+// Both products run on the 4x4x1 sixteen-block MFMA (blocks = pixel streams x unit / column
+// quads, the streams summed once at the flush): on 16x16x4 the dW1 tile used 3 of 16 rows and
+// the dW0 tile 8 of 16 columns, 1,024 MFMA cycles per tile and wave; now 128 + 256.
 // The output layer must be linear (g.r1 == 0, every reference architecture's "X-1-linear-none"):
 // then g_out needs no pass over all units first, and a tile's units are computed just in time.
 constexpr int kHbXP = 68;
@@ -1749,8 +1757,15 @@ __global__ __launch_bounds__(kHeadT, 4) void t_head_bwd_t(const float *__restric
     // sv: [16 units][64 px] (the tile's h, then its g_h); sw: [field][64 px]
     float *sv = s_dyn + w * kWF, *sw = sv + 16 * kXP;
     const int ln = lane & 15, lk = lane >> 4;
-    // operand rows: gp k (ln >= 3: the zero row 3), x i | 1 (ln > CIN: the zero row 3)
-    const int ia = ln < 3 ? ln : 3, ib = ln <= CIN ? kGX + ln : 3;
+    // weight gradients on v_mfma_f32_4x4x1_16b (mfma4x4), 4x4 blocks bk = lane >> 2:
+    //  dW1: block (pixel stream lk, unit quad), A = gp k = lane & 3 (3: the zero row 3),
+    //       B = h of unit ln; stream lk covers pixels 16 lk .. 16 lk + 15
+    //  dW0: block (pixel stream s0, column quad iq, unit quad), A = g_h of unit ln, B = x | 1
+    //       column 4 iq + (lane & 3) (> CIN: the zero row 3); kNQ column quads, 4 / kNQ
+    //       streams of kPS pixels each
+    constexpr int kNQ = CIN + 1 <= 4 ? 1 : CIN + 1 <= 8 ? 2 : 4, kPS = 16 * kNQ;
+    const int iq = lk % kNQ, s0 = lk / kNQ, ic = 4 * iq + (lane & 3);
+    const int ia = (lane & 3) < 3 ? (lane & 3) : 3, ib = ic <= CIN ? kGX + ic : 3;
     // constant rows: 0 (row 3), 1 (row kGX + CIN), written once
     sw[3 * kXP + lane] = 0.f;
     sw[(kGX + CIN) * kXP + lane] = 1.f;
@@ -1817,14 +1832,13 @@ __global__ __launch_bounds__(kHeadT, 4) void t_head_bwd_t(const float *__restric
                 hmask |= ((a.x > 0.f ? 1u : 0u) | (a.y > 0.f ? 2u : 0u)) << (2 * u);
             }
             wave_lds_sync();
-            // ---- dW1 tile q += gp^T h; K = pixels px = s + 16 (lane >> 4), four MFMAs per pair of
-            // 128-bit reads
+            // ---- dW1 tile q += gp^T h, per pixel stream; four MFMAs per pair of 128-bit reads
 #pragma unroll
             for (int s = 0; s < 16; s += 4) {
                 const v4 av = *reinterpret_cast<const v4 *>(sw + ia * kXP + 16 * lk + s);
                 const v4 bv = *reinterpret_cast<const v4 *>(sv + ln * kXP + 16 * lk + s);
 #pragma unroll
-                for (int e = 0; e < 4; ++e) a1[q] = mfma4(av[e], bv[e], a1[q]);
+                for (int e = 0; e < 4; ++e) a1[q] = mfma4x4(av[e], bv[e], a1[q]);
             }
             wave_lds_sync(); // every lane has read the h rows before g_h replaces them
             // ---- g_h of the tile (replaces h in this lane's row) and g_x
@@ -1845,11 +1859,11 @@ __global__ __launch_bounds__(kHeadT, 4) void t_head_bwd_t(const float *__restric
             wave_lds_sync();
             // ---- dW0 | db0 tile q += g_h^T [x | 1]
 #pragma unroll
-            for (int s = 0; s < 16; s += 4) {
-                const v4 av = *reinterpret_cast<const v4 *>(sv + ln * kXP + 16 * lk + s);
-                const v4 bv = *reinterpret_cast<const v4 *>(sw + ib * kXP + 16 * lk + s);
+            for (int s = 0; s < kPS; s += 4) {
+                const v4 av = *reinterpret_cast<const v4 *>(sv + ln * kXP + kPS * s0 + s);
+                const v4 bv = *reinterpret_cast<const v4 *>(sw + ib * kXP + kPS * s0 + s);
 #pragma unroll
-                for (int e = 0; e < 4; ++e) a0[q] = mfma4(av[e], bv[e], a0[q]);
+                for (int e = 0; e < 4; ++e) a0[q] = mfma4x4(av[e], bv[e], a0[q]);
             }
             wave_lds_sync(); // before the next tile's h (or the next chunk's rows) overwrite these
         }
@@ -1867,19 +1881,26 @@ __global__ __launch_bounds__(kHeadT, 4) void t_head_bwd_t(const float *__restric
     float *red = s_dyn + w * kWF;
     static_assert(kWF >= 16 * NT * (CIN + 4) + 3, "a wave's partial row fits its LDS rows");
     __syncthreads();
+    // the pixel streams' partial blocks summed across lanes (16 lanes apart), then register r of
+    // lane l holds dW1[k = r][unit 16 q + ln] (l < 16) and dW0[unit 16 q + 4 ((l >> 2) & 3) + r][ic]
+    // (l < 16 kNQ)
 #pragma unroll
     for (int q = 0; q < NT; ++q) {
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
-            const int m = 4 * lk + r;
-            if (m < 3) { // dW1[k = m][j]
+            float v1 = a1[q][r], v0 = a0[q][r];
+            v1 += __shfl_xor(v1, 16);
+            v1 += __shfl_xor(v1, 32);
+#pragma unroll
+            for (int o = 16 * kNQ; o < 64; o <<= 1) v0 += __shfl_xor(v0, o);
+            if (r < 3 && lane < 16) { // dW1[k = r][j]
                 const int j = 16 * q + ln;
-                if (j < hid) red[hid * (CIN + 1) + m * hid + j] = a1[q][r];
+                if (j < hid) red[hid * (CIN + 1) + r * hid + j] = v1;
             }
-            const int j = 16 * q + m; // dW0[j][i = ln]
-            if (j < hid) {
-                if (ln < CIN) red[j * CIN + ln] = a0[q][r];
-                else if (ln == CIN) red[hid * CIN + j] = a0[q][r];
+            const int j = 16 * q + 4 * ((lane >> 2) & 3) + r; // dW0[j][i = ic]
+            if (lane < 16 * kNQ && j < hid) {
+                if (ic < CIN) red[j * CIN + ic] = v0;
+                else if (ic == CIN) red[hid * CIN + j] = v0;
             }
         }
     }
