@@ -1285,15 +1285,16 @@ __device__ __forceinline__ void qrange(int p, int dd, int n, int &lo, int &hi)
 //    an interior pixel p is the plain correlation sum_{c,k} W[c][i][k] G[c][p - d_k]; a
 //    pixel on the image border also collects the taps that the replicate padding clamps
 //    onto it (qrange), all within the ring.
-// MODE: 1 = input gradient only, 2 = weight / bias gradients only, 3 = both.  The step runs
-// the two halves as separate launches: the input-gradient kernel holds no 84 accumulators, so
-// it keeps many more waves resident to hide its tile loads (the combined kernel sat 71 % of
-// its wave cycles in s_waitcnt / barrier waits, SQ_WAIT_ANY), and needs no reduction.
+// MODE: 1 = input gradient only, 2 = weight / bias gradients only (per-thread VALU sums, 84
+// accumulators), 3 = both, the weight gradients on the matrix cores.  Round 4 ran modes 1 and 2
+// as two launches: with 84 accumulators per thread the combined VALU kernel sat 71 % of its wave
+// cycles in s_waitcnt / barrier waits (SQ_WAIT_ANY).  Mode 3 keeps them in the 4 accumulator
+// registers of v_mfma_f32_4x4x1_16b_f32 (+ 3 bias sums), so one launch reads every tile once.
 // (Measured and dropped: the input gradient one channel per iteration with 27 scalar weights
 // each instead of all 81 at once -- 74 vs 40 us, the scalar-load waits per channel.)
 constexpr int kSY = 16, kSX = 64;
 template <int MODE>
-__global__ __launch_bounds__(kT) __attribute__((amdgpu_waves_per_eu(MODE == 2 ? 4 : 1))) void t_sp_bwd(const float *__restrict__ gout, const float *__restrict__ outp,
+__global__ __launch_bounds__(kT) __attribute__((amdgpu_waves_per_eu(MODE == 2 ? 4 : MODE == 3 ? 4 : 1))) void t_sp_bwd(const float *__restrict__ gout, const float *__restrict__ outp,
                                                const float *__restrict__ in, Geo g, const float *__restrict__ th,
                                                int64_t ps, int wo, int bo, int res, float *__restrict__ gin,
                                                float *__restrict__ gth, int64_t gstride)
@@ -1313,16 +1314,19 @@ __global__ __launch_bounds__(kT) __attribute__((amdgpu_waves_per_eu(MODE == 2 ? 
     float *Ib = gin + (int64_t)b * 3 * npx;
     const int tx = (W + kSX - 1) / kSX, ntile = tx * ((H + kSY - 1) / kSY);
     const int c = threadIdx.x & 63, rb = (threadIdx.x >> 6) * 4;
-    float acc[DW ? 84 : 1];
+    constexpr bool VW = MODE == 2; // the VALU weight-gradient form
+    float acc[VW ? 84 : 1];
 #pragma unroll
-    for (int e = 0; e < (DW ? 84 : 1); ++e) acc[e] = 0.f;
+    for (int e = 0; e < (VW ? 84 : 1); ++e) acc[e] = 0.f;
+    v4f dacc = {0.f, 0.f, 0.f, 0.f}; // MODE 3: the MFMA blocks
+    float bacc[3] = {0.f, 0.f, 0.f};  // MODE 3: bias sums
     for (int t = blockIdx.x; t < ntile; t += gridDim.x) {
         const int y0 = (t / tx) * kSY, x0 = (t % tx) * kSX;
         __syncthreads();
         // the ring in batches of UN elements per thread: a batch's loads are all in flight
         // before its LDS stores (the input-gradient kernel, with few registers, takes the
         // whole ring in one batch; the weight-gradient kernel two per batch)
-        constexpr int NU = (RH * RW + kT - 1) / kT, UN = DW ? 2 : NU;
+        constexpr int NU = (RH * RW + kT - 1) / kT, UN = VW ? 2 : NU;
 #pragma unroll
         for (int u0 = 0; u0 < NU; u0 += UN) {
             float xs[UN][3], gs[UN][3], os[UN][3];
@@ -1355,6 +1359,25 @@ __global__ __launch_bounds__(kT) __attribute__((amdgpu_waves_per_eu(MODE == 2 ? 
             }
         }
         __syncthreads();
+        if constexpr (MODE == 3) {
+            // dW[oc][n = (i, ky, kx)] += sum_q G[oc][q] X[i][q + (ky - 1, kx - 1)] over the wave's 4 x 64
+            // pixels: block bk = lane >> 2 < 14 is (column quad nq = bk % 7, pixel stream bk / 7;
+            // stream s takes rows rb + 2 s, rb + 2 s + 1), A = G[oc = lane & 3], B = X at tap column
+            // n = 4 nq + (lane & 3), one pixel per MFMA.  Row oc = 3, column n = 27 and blocks 14, 15
+            // read valid (clamped) LDS and are never flushed.  Every operand address is a lane base +
+            // a compile-time offset.
+            const int ln4 = threadIdx.x & 3, bk = (threadIdx.x & 63) >> 2;
+            const int st = bk >= 7 ? 1 : 0, n = min(4 * (bk - 7 * st) + ln4, 26);
+            const int i = n / 9, k = n - 9 * i, ky = k / 3, kx = k - 3 * ky;
+            const float *pa = &sG[ln4 < 3 ? ln4 : 0][rb + 2 * st + 1][1];
+            const float *pb = &sX[i][rb + 2 * st + ky][kx];
+#pragma unroll 1
+            for (int j = 0; j < 2 * kSX; j += 16) { // 16 pixels per iteration (operand reads in flight)
+                const int o = (j >= kSX ? RW - kSX : 0) + j;
+#pragma unroll
+                for (int cc = 0; cc < 16; ++cc) dacc = mfma4x4(pa[o + cc], pb[o + cc], dacc);
+            }
+        }
         const int px = x0 + c;
 #pragma unroll 1
         for (int pr = 0; pr < 4; ++pr) {
@@ -1364,7 +1387,11 @@ __global__ __launch_bounds__(kT) __attribute__((amdgpu_waves_per_eu(MODE == 2 ? 
             float gp[3];
 #pragma unroll
             for (int ch = 0; ch < 3; ++ch) gp[ch] = sG[ch][ry + 1][c + 1];
-            if constexpr (DW) {
+            if constexpr (MODE == 3) {
+#pragma unroll
+                for (int oc = 0; oc < 3; ++oc) bacc[oc] += gp[oc];
+            }
+            if constexpr (VW) {
 #pragma unroll
                 for (int i = 0; i < 3; ++i)
 #pragma unroll
@@ -1418,10 +1445,25 @@ __global__ __launch_bounds__(kT) __attribute__((amdgpu_waves_per_eu(MODE == 2 ? 
     if constexpr (!DW) return;
     // block reduction of the 84 weight / bias gradients
     const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+    if constexpr (VW) {
 #pragma unroll
-    for (int e = 0; e < 84; ++e) {
-        const float v = wave_sum(acc[e]);
-        if (lane == 0) s_red[wid][e] = v;
+        for (int e = 0; e < 84; ++e) {
+            const float v = wave_sum(acc[e]);
+            if (lane == 0) s_red[wid][e] = v;
+        }
+    } else {
+        // lane l < 27 and lane l + 28 (the same column quad, the other stream) hold column n = l;
+        // register r is row oc = r
+#pragma unroll
+        for (int r = 0; r < 3; ++r) {
+            const float v = dacc[r] + __shfl(dacc[r], (lane + 28) & 63);
+            if (lane < 27) s_red[wid][r * 27 + lane] = v;
+        }
+#pragma unroll
+        for (int oc = 0; oc < 3; ++oc) {
+            const float v = wave_sum(bacc[oc]);
+            if (lane == 0) s_red[wid][81 + oc] = v;
+        }
     }
     __syncthreads();
     if (threadIdx.x < 84) {
@@ -3081,6 +3123,7 @@ extern "C" int ccmi_train_step(const ccmi_train_args *a, void *stream)
         // against 32 .. 512 per frame)
         const unsigned nb = (unsigned)std::max(1, std::min(ntile, 1024 / B));
         const float *outp = g.sp_relu[i] ? F(pl.z[i + 1]) : nullptr;
+#if defined(CCMI_SP_BWD_SPLIT) // A/B builds: the round-4 pair of launches
         {
             // input gradient: one tile per workgroup; weight gradients: grid-stride as before
             hipLaunchKernelGGL(t_sp_bwd<1>, dim3((unsigned)ntile, B), dim3(kT), 0, s, gcur, outp, F(pl.z[i]), g, a->params,
@@ -3088,6 +3131,12 @@ extern "C" int ccmi_train_step(const ccmi_train_args *a, void *stream)
             hipLaunchKernelGGL(t_sp_bwd<2>, dim3(nb, B), dim3(kT), 0, s, gcur, outp, F(pl.z[i]), g, a->params,
                                a->param_stride, g.sp_w[i], g.sp_b[i], g.sp_res[i], gin, slots, g.P);
         }
+#else
+        (void)nb;
+        // both halves, one tile per workgroup: each tile's X / G / out read once
+        hipLaunchKernelGGL(t_sp_bwd<3>, dim3((unsigned)ntile, B), dim3(kT), 0, s, gcur, outp, F(pl.z[i]), g, a->params,
+                           a->param_stride, g.sp_w[i], g.sp_b[i], g.sp_res[i], gin, slots, g.P);
+#endif
         gcur = gin;
     }
     {
