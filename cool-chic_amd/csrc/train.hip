@@ -1254,28 +1254,6 @@ __global__ void t_sp_gpre(float *__restrict__ gout, const float *__restrict__ ou
     if (i < n && out[i] <= 0.f) gout[i] = 0.f;
 }
 
-// Replicate-padding adjoint along one axis: output positions q whose tap offset dd reads
-// input position p (clamp(q + dd) == p): at most two (borders), returned as [lo, hi].
-__device__ __forceinline__ void qrange(int p, int dd, int n, int &lo, int &hi)
-{
-    if (n == 1) {
-        lo = 0;
-        hi = 0;
-    } else if (p == 0) {
-        lo = 0;
-        hi = min(n - 1, -dd);
-    } else if (p == n - 1) {
-        lo = max(0, n - 1 - dd);
-        hi = n - 1;
-    } else {
-        lo = hi = p - dd;
-        if (lo < 0 || lo >= n) {
-            lo = 1;
-            hi = 0;
-        }
-    }
-}
-
 // 3x3 layer backward on 16 x 64 pixel tiles staged in LDS (grid-stride over the tiles).
 //  * X (the layer input) at replicate-clamped coordinates over the tile + 1-pixel ring:
 //    dW[c][i][ky][kx] += G[c][q] X[i][clamp(q + (ky-1, kx-1))], accumulated per thread in
@@ -1284,7 +1262,7 @@ __device__ __forceinline__ void qrange(int p, int dd, int n, int &lo, int &hi)
 //    t_sp_gpre fused in) over the same ring, zero outside the image: the input gradient of
 //    an interior pixel p is the plain correlation sum_{c,k} W[c][i][k] G[c][p - d_k]; a
 //    pixel on the image border also collects the taps that the replicate padding clamps
-//    onto it (qrange), all within the ring.
+//    onto it (one kernel row / column / corner tap per image side it lies on), all within the ring.
 // MODE: 1 = input gradient only, 2 = weight / bias gradients only (per-thread VALU sums, 84
 // accumulators), 3 = both, the weight gradients on the matrix cores.  Round 4 ran modes 1 and 2
 // as two launches: with 84 accumulators per thread the combined VALU kernel sat 71 % of its wave
@@ -1301,8 +1279,15 @@ __global__ __launch_bounds__(kT) __attribute__((amdgpu_waves_per_eu(MODE == 2 ? 
 {
     constexpr bool DX = (MODE & 1) != 0, DW = (MODE & 2) != 0;
     constexpr int RH = kSY + 2, RW = kSX + 2;
-    __shared__ float sX[3][RH][RW];
-    __shared__ float sG[3][RH][RW];
+    // ring images at row pitch kRP = 67 and plane pitch kPP = 1225 (== 3 and 9 mod 32 banks): the 27
+    // taps (i, ky, kx) of one pixel sit on 27 distinct banks (9 i + 3 ky + kx), so the weight-
+    // gradient MFMA loop's operand reads are conflict-free (pitches 66 / 1188: ~3-way)
+    constexpr int kRP = 67, kPP = 1225;
+    static_assert(kRP >= RW && kPP >= RH * kRP, "ring fits its pitches");
+    __shared__ float sXf[3 * kPP];
+    __shared__ float sGf[3 * kPP];
+#define SX(ch, r, q) sXf[(ch) * kPP + (r) * kRP + (q)]
+#define SG(ch, r, q) sGf[(ch) * kPP + (r) * kRP + (q)]
     __shared__ float s_red[4][84];
     const int b = blockIdx.y;
     const int H = g.H, W = g.W;
@@ -1341,9 +1326,15 @@ __global__ __launch_bounds__(kT) __attribute__((amdgpu_waves_per_eu(MODE == 2 ? 
                 const bool live = u0 + uu < NU && i < RH * RW;
 #pragma unroll
                 for (int ch = 0; ch < 3; ++ch) {
+#if defined(CCMI_DIAG_SPB_NOLOAD) // diagnostic builds only (tools/spb_diag.sh): wrong results
+                    xs[uu][ch] = 0.001f * (float)(cl + ch);
+                    gs[uu][ch] = inb[uu] ? 0.002f * (float)(cl - ch) : 0.f;
+                    os[uu][ch] = 1.f;
+#else
                     xs[uu][ch] = (DW && live) ? Xb[ch * npx + cl] : 0.f;
                     gs[uu][ch] = (live && inb[uu]) ? Gb[ch * npx + cl] : 0.f;
                     os[uu][ch] = (Ob && live && inb[uu]) ? Ob[ch * npx + cl] : 1.f;
+#endif
                 }
             }
 #pragma unroll
@@ -1353,12 +1344,13 @@ __global__ __launch_bounds__(kT) __attribute__((amdgpu_waves_per_eu(MODE == 2 ? 
                 const int r = i / RW, q = i - r * RW;
 #pragma unroll
                 for (int ch = 0; ch < 3; ++ch) {
-                    if (DW) sX[ch][r][q] = xs[uu][ch];
-                    sG[ch][r][q] = os[uu][ch] <= 0.f ? 0.f : gs[uu][ch];
+                    if (DW) SX(ch, r, q) = xs[uu][ch];
+                    SG(ch, r, q) = os[uu][ch] <= 0.f ? 0.f : gs[uu][ch];
                 }
             }
         }
         __syncthreads();
+#if !defined(CCMI_DIAG_SPB_NODW)
         if constexpr (MODE == 3) {
             // dW[oc][n = (i, ky, kx)] += sum_q G[oc][q] X[i][q + (ky - 1, kx - 1)] over the wave's 4 x 64
             // pixels: block bk = lane >> 2 < 14 is (column quad nq = bk % 7, pixel stream bk / 7;
@@ -1369,15 +1361,16 @@ __global__ __launch_bounds__(kT) __attribute__((amdgpu_waves_per_eu(MODE == 2 ? 
             const int ln4 = threadIdx.x & 3, bk = (threadIdx.x & 63) >> 2;
             const int st = bk >= 7 ? 1 : 0, n = min(4 * (bk - 7 * st) + ln4, 26);
             const int i = n / 9, k = n - 9 * i, ky = k / 3, kx = k - 3 * ky;
-            const float *pa = &sG[ln4 < 3 ? ln4 : 0][rb + 2 * st + 1][1];
-            const float *pb = &sX[i][rb + 2 * st + ky][kx];
+            const float *pa = &SG(ln4 < 3 ? ln4 : 0, rb + 2 * st + 1, 1);
+            const float *pb = &SX(i, rb + 2 * st + ky, kx);
 #pragma unroll 1
             for (int j = 0; j < 2 * kSX; j += 16) { // 16 pixels per iteration (operand reads in flight)
-                const int o = (j >= kSX ? RW - kSX : 0) + j;
+                const int o = (j >= kSX ? kRP - kSX : 0) + j;
 #pragma unroll
                 for (int cc = 0; cc < 16; ++cc) dacc = mfma4x4(pa[o + cc], pb[o + cc], dacc);
             }
         }
+#endif
         const int px = x0 + c;
 #pragma unroll 1
         for (int pr = 0; pr < 4; ++pr) {
@@ -1386,7 +1379,7 @@ __global__ __launch_bounds__(kT) __attribute__((amdgpu_waves_per_eu(MODE == 2 ? 
             // weight / bias gradients at output q = (py, px)
             float gp[3];
 #pragma unroll
-            for (int ch = 0; ch < 3; ++ch) gp[ch] = sG[ch][ry + 1][c + 1];
+            for (int ch = 0; ch < 3; ++ch) gp[ch] = SG(ch, ry + 1, c + 1);
             if constexpr (MODE == 3) {
 #pragma unroll
                 for (int oc = 0; oc < 3; ++oc) bacc[oc] += gp[oc];
@@ -1396,7 +1389,7 @@ __global__ __launch_bounds__(kT) __attribute__((amdgpu_waves_per_eu(MODE == 2 ? 
                 for (int i = 0; i < 3; ++i)
 #pragma unroll
                     for (int k = 0; k < 9; ++k) {
-                        const float xv = sX[i][ry + k / 3][c + k % 3];
+                        const float xv = SX(i, ry + k / 3, c + k % 3);
 #pragma unroll
                         for (int oc = 0; oc < 3; ++oc) acc[(oc * 3 + i) * 9 + k] = fmaf(gp[oc], xv, acc[(oc * 3 + i) * 9 + k]);
                     }
@@ -1404,39 +1397,48 @@ __global__ __launch_bounds__(kT) __attribute__((amdgpu_waves_per_eu(MODE == 2 ? 
                 for (int oc = 0; oc < 3; ++oc) acc[81 + oc] += gp[oc];
             }
             if constexpr (!DX) continue;
-            // input gradient at p = (py, px)
+            // input gradient at p = (py, px): the correlation sum_{oc,k} W[oc][i][k] G[oc][p - d_k]
+            // (G is zero outside the image), plus what the replicate padding clamps onto a border
+            // pixel -- the padded-domain adjoint at the ring positions r with clamp(r) = p: above the
+            // top row the kernel's row 0 against G's row py, below the bottom row its row 2, left /
+            // right of the image its column 0 / 2 against G's column px, and at a corner the one
+            // corner tap against G(p).  Every operand is inside the tile's ring; a 1-pixel image side
+            // takes both of its edges' terms.  (Same sums as the qrange enumeration, another order.)
             float gi[3] = {0.f, 0.f, 0.f};
-            if (py > 0 && py < H - 1 && px > 0 && px < W - 1) {
+#if !defined(CCMI_DIAG_SPB_NODX)
 #pragma unroll
-                for (int k = 0; k < 9; ++k) {
-                    const int ky = k / 3, kx = k % 3;
+            for (int k = 0; k < 9; ++k) {
+                const int ky = k / 3, kx = k % 3;
 #pragma unroll
-                    for (int oc = 0; oc < 3; ++oc) {
-                        const float gq = sG[oc][ry + 2 - ky][c + 2 - kx];
+                for (int oc = 0; oc < 3; ++oc) {
+                    const float gq = SG(oc, ry + 2 - ky, c + 2 - kx);
 #pragma unroll
-                        for (int i = 0; i < 3; ++i) gi[i] = fmaf(P[wo + (oc * 3 + i) * 9 + k], gq, gi[i]);
-                    }
-                }
-            } else {
-                for (int ky = 0; ky < 3; ++ky) {
-                    int qy0, qy1;
-                    qrange(py, ky - 1, H, qy0, qy1);
-                    for (int qy = qy0; qy <= qy1; ++qy)
-                        for (int kx = 0; kx < 3; ++kx) {
-                            int qx0, qx1;
-                            qrange(px, kx - 1, W, qx0, qx1);
-                            for (int qx = qx0; qx <= qx1; ++qx) {
-#pragma unroll
-                                for (int oc = 0; oc < 3; ++oc) {
-                                    const float gq = sG[oc][qy - y0 + 1][qx - x0 + 1];
-#pragma unroll
-                                    for (int i = 0; i < 3; ++i)
-                                        gi[i] = fmaf(P[wo + (oc * 3 + i) * 9 + ky * 3 + kx], gq, gi[i]);
-                                }
-                            }
-                        }
+                    for (int i = 0; i < 3; ++i) gi[i] = fmaf(P[wo + (oc * 3 + i) * 9 + k], gq, gi[i]);
                 }
             }
+            const bool top = py == 0, bot = py == H - 1, lft = px == 0, rgt = px == W - 1;
+            if (top || bot || lft || rgt) {
+#pragma unroll 1
+                for (int oc = 0; oc < 3; ++oc) {
+                    const cfloat_ptr Wk = P + wo + oc * 27;
+#pragma unroll
+                    for (int i = 0; i < 3; ++i) {
+                        const cfloat_ptr Wi = Wk + i * 9; // Wi[3 ky + kx]
+                        float e = 0.f;
+#pragma unroll
+                        for (int t = 0; t < 3; ++t) {
+                            const float wr = (top ? Wi[t] : 0.f) + (bot ? Wi[6 + t] : 0.f);
+                            const float wc = (lft ? Wi[3 * t] : 0.f) + (rgt ? Wi[3 * t + 2] : 0.f);
+                            e = fmaf(wr, SG(oc, ry + 1, c + 2 - t), e);
+                            e = fmaf(wc, SG(oc, ry + 2 - t, c + 1), e);
+                        }
+                        const float wy0 = top ? 1.f : 0.f, wy2 = bot ? 1.f : 0.f;
+                        const float wcn = (lft ? wy0 * Wi[0] + wy2 * Wi[6] : 0.f) + (rgt ? wy0 * Wi[2] + wy2 * Wi[8] : 0.f);
+                        gi[i] += fmaf(wcn, gp[oc], e);
+                    }
+                }
+            }
+#endif
             const int64_t pi = (int64_t)py * W + px;
 #pragma unroll
             for (int i = 0; i < 3; ++i) Ib[i * npx + pi] = gi[i] + (res ? gp[i] : 0.f);
@@ -1473,6 +1475,8 @@ __global__ __launch_bounds__(kT) __attribute__((amdgpu_waves_per_eu(MODE == 2 ? 
         atomicAdd(&dst[e < 81 ? wo + e : bo + (e - 81)], v);
     }
 }
+#undef SX
+#undef SG
 
 // 1x1 head backward.  Per pixel (lane = pixel, VALU): the hidden layer recomputed, g_h and
 // g_dense.  The weight gradients are sums over pixels -- GEMMs with K = pixels -- and run on
