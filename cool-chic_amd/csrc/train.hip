@@ -1272,7 +1272,7 @@ __global__ void t_sp_gpre(float *__restrict__ gout, const float *__restrict__ ou
 // each instead of all 81 at once -- 74 vs 40 us, the scalar-load waits per channel.)
 constexpr int kSY = 16, kSX = 64;
 template <int MODE>
-__global__ __launch_bounds__(kT) __attribute__((amdgpu_waves_per_eu(MODE == 2 ? 4 : MODE == 3 ? 4 : 1))) void t_sp_bwd(const float *__restrict__ gout, const float *__restrict__ outp,
+__global__ __launch_bounds__(kT) __attribute__((amdgpu_waves_per_eu(MODE == 2 ? 4 : MODE == 3 ? 5 : 1))) void t_sp_bwd(const float *__restrict__ gout, const float *__restrict__ outp,
                                                const float *__restrict__ in, Geo g, const float *__restrict__ th,
                                                int64_t ps, int wo, int bo, int res, float *__restrict__ gin,
                                                float *__restrict__ gth, int64_t gstride)
@@ -1289,6 +1289,7 @@ __global__ __launch_bounds__(kT) __attribute__((amdgpu_waves_per_eu(MODE == 2 ? 
 #define SX(ch, r, q) sXf[(ch) * kPP + (r) * kRP + (q)]
 #define SG(ch, r, q) sGf[(ch) * kPP + (r) * kRP + (q)]
     __shared__ float s_red[4][84];
+    __shared__ float s_wt[81]; // MODE 3: the layer's weights for the border-tap fold
     const int b = blockIdx.y;
     const int H = g.H, W = g.W;
     const int64_t npx = (int64_t)H * W;
@@ -1300,6 +1301,8 @@ __global__ __launch_bounds__(kT) __attribute__((amdgpu_waves_per_eu(MODE == 2 ? 
     const int tx = (W + kSX - 1) / kSX, ntile = tx * ((H + kSY - 1) / kSY);
     const int c = threadIdx.x & 63, rb = (threadIdx.x >> 6) * 4;
     constexpr bool VW = MODE == 2; // the VALU weight-gradient form
+    if constexpr (DX) // visible after the tile loop's first barrier
+        for (int e = threadIdx.x; e < 81; e += kT) s_wt[e] = P[wo + e];
     float acc[VW ? 84 : 1];
 #pragma unroll
     for (int e = 0; e < (VW ? 84 : 1); ++e) acc[e] = 0.f;
@@ -1398,12 +1401,7 @@ __global__ __launch_bounds__(kT) __attribute__((amdgpu_waves_per_eu(MODE == 2 ? 
             }
             if constexpr (!DX) continue;
             // input gradient at p = (py, px): the correlation sum_{oc,k} W[oc][i][k] G[oc][p - d_k]
-            // (G is zero outside the image), plus what the replicate padding clamps onto a border
-            // pixel -- the padded-domain adjoint at the ring positions r with clamp(r) = p: above the
-            // top row the kernel's row 0 against G's row py, below the bottom row its row 2, left /
-            // right of the image its column 0 / 2 against G's column px, and at a corner the one
-            // corner tap against G(p).  Every operand is inside the tile's ring; a 1-pixel image side
-            // takes both of its edges' terms.  (Same sums as the qrange enumeration, another order.)
+            // (G is zero outside the image); border pixels get the rest after the row loop
             float gi[3] = {0.f, 0.f, 0.f};
 #if !defined(CCMI_DIAG_SPB_NODX)
 #pragma unroll
@@ -1416,33 +1414,69 @@ __global__ __launch_bounds__(kT) __attribute__((amdgpu_waves_per_eu(MODE == 2 ? 
                     for (int i = 0; i < 3; ++i) gi[i] = fmaf(P[wo + (oc * 3 + i) * 9 + k], gq, gi[i]);
                 }
             }
-            const bool top = py == 0, bot = py == H - 1, lft = px == 0, rgt = px == W - 1;
-            if (top || bot || lft || rgt) {
-#pragma unroll 1
-                for (int oc = 0; oc < 3; ++oc) {
-                    const cfloat_ptr Wk = P + wo + oc * 27;
-#pragma unroll
-                    for (int i = 0; i < 3; ++i) {
-                        const cfloat_ptr Wi = Wk + i * 9; // Wi[3 ky + kx]
-                        float e = 0.f;
-#pragma unroll
-                        for (int t = 0; t < 3; ++t) {
-                            const float wr = (top ? Wi[t] : 0.f) + (bot ? Wi[6 + t] : 0.f);
-                            const float wc = (lft ? Wi[3 * t] : 0.f) + (rgt ? Wi[3 * t + 2] : 0.f);
-                            e = fmaf(wr, SG(oc, ry + 1, c + 2 - t), e);
-                            e = fmaf(wc, SG(oc, ry + 2 - t, c + 1), e);
-                        }
-                        const float wy0 = top ? 1.f : 0.f, wy2 = bot ? 1.f : 0.f;
-                        const float wcn = (lft ? wy0 * Wi[0] + wy2 * Wi[6] : 0.f) + (rgt ? wy0 * Wi[2] + wy2 * Wi[8] : 0.f);
-                        gi[i] += fmaf(wcn, gp[oc], e);
-                    }
-                }
-            }
 #endif
             const int64_t pi = (int64_t)py * W + px;
 #pragma unroll
             for (int i = 0; i < 3; ++i) Ib[i * npx + pi] = gi[i] + (res ? gp[i] : 0.f);
         }
+#if !defined(CCMI_DIAG_SPB_NODX) && !defined(CCMI_DIAG_SPB_NOBORDER)
+        // What the replicate padding clamps onto a border pixel -- the padded-domain adjoint at the
+        // ring positions r with clamp(r) = p: above the top row the kernel's row 0 against G's row
+        // py, below the bottom row its row 2, left / right of the image its column 0 / 2 against G's
+        // column px, at a corner the one corner tap against G(p); a 1-pixel image side takes both of
+        // its edges' terms.  (The qrange enumeration's sums in another order.)  Added after the
+        // barrier by one thread per border pixel of a tile that touches the image border -- inside
+        // the row loop, a border lane held up its whole wave (profiles/r5ze_*, r5zf_*).  Slots:
+        // threads [0, 64) the top row, [64, 128) the bottom row, [128, 144) / [144, 160) the left /
+        // right column without those rows; the barrier orders the rows' global writes before these.
+        if constexpr (DX) {
+            const int rbot = H - 1 - y0, crt = W - 1 - x0; // the image's last row / column in tile coordinates
+            const bool etop = y0 == 0, ebot = rbot < kSY, elft = x0 == 0, ergt = crt < kSX;
+            if (etop || ebot || elft || ergt) { // workgroup-uniform
+                __syncthreads();
+                const int t = threadIdx.x;
+                int ry = -1, cx = -1;
+                if (t < kSX) {
+                    if (etop) ry = 0, cx = t;
+                } else if (t < 2 * kSX) {
+                    if (ebot && !(etop && rbot == 0)) ry = rbot, cx = t - kSX;
+                } else if (t < 2 * kSX + kSY) {
+                    const int r = t - 2 * kSX;
+                    if (elft && y0 + r != 0 && r != rbot) ry = r, cx = 0;
+                } else if (t < 2 * kSX + 2 * kSY) {
+                    const int r = t - 2 * kSX - kSY;
+                    if (ergt && !(elft && crt == 0) && y0 + r != 0 && r != rbot) ry = r, cx = crt;
+                }
+                const int by = y0 + ry, bx = x0 + cx;
+                if (ry >= 0 && by < H && bx < W) {
+                    const bool top = by == 0, bot = by == H - 1, lft = bx == 0, rgt = bx == W - 1;
+                    float e[3] = {0.f, 0.f, 0.f};
+#pragma unroll
+                    for (int oc = 0; oc < 3; ++oc) {
+                        const float *Wk = s_wt + oc * 27;
+                        const float gq = SG(oc, ry + 1, cx + 1);
+#pragma unroll
+                        for (int i = 0; i < 3; ++i) {
+                            const float *Wi = Wk + i * 9; // Wi[3 ky + kx]
+#pragma unroll
+                            for (int u = 0; u < 3; ++u) {
+                                const float wr = (top ? Wi[u] : 0.f) + (bot ? Wi[6 + u] : 0.f);
+                                const float wc = (lft ? Wi[3 * u] : 0.f) + (rgt ? Wi[3 * u + 2] : 0.f);
+                                e[i] = fmaf(wr, SG(oc, ry + 1, cx + 2 - u), e[i]);
+                                e[i] = fmaf(wc, SG(oc, ry + 2 - u, cx + 1), e[i]);
+                            }
+                            const float wy0 = top ? 1.f : 0.f, wy2 = bot ? 1.f : 0.f;
+                            const float wcn = (lft ? wy0 * Wi[0] + wy2 * Wi[6] : 0.f) + (rgt ? wy0 * Wi[2] + wy2 * Wi[8] : 0.f);
+                            e[i] = fmaf(wcn, gq, e[i]);
+                        }
+                    }
+                    const int64_t pi = (int64_t)by * W + bx;
+#pragma unroll
+                    for (int i = 0; i < 3; ++i) Ib[i * npx + pi] += e[i];
+                }
+            }
+        }
+#endif
     }
     if constexpr (!DW) return;
     // block reduction of the 84 weight / bias gradients
