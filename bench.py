@@ -532,7 +532,7 @@ def encoder_shard(rank: int, lambdas=None):
 # Per-kernel rooflines of the encoder's training step, from a committed rocprofv3 kernel trace
 # of tools/bench_train.py 8 with CCMI_ARM_OVERLAP=0 (every kernel alone; 8 frames of 512 x 768,
 # hop, c3x; one launch per iteration each; tools/gpu_r5e.sh)
-TRAIN_PROFILE = "profiles/r5zg_train_iso_kernel_stats.csv"
+TRAIN_PROFILE = "profiles/r5zl_train_iso_kernel_stats.csv"
 TRAIN_FRAMES, TRAIN_H, TRAIN_W = 8, 512, 768
 
 

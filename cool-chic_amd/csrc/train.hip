@@ -1126,6 +1126,27 @@ __global__ __launch_bounds__(kT) void t_sp_fwd(const float *__restrict__ in, Geo
         const int64_t pix = (int64_t)y0 * g.W + px;
         float *o = out + (int64_t)b * 3 * npx + pix;
         const int h2 = g.H / 2, w2 = g.W / 2;
+        // the fused loss's target values, loaded with the inputs (loaded where used, each was a
+        // dependent memory latency per output: 62 % of the wave cycles in WAIT_ANY,
+        // profiles/r5zk_train_pmc.txt)
+        float tv[LOSS > 0 ? kSpRows : 1][3];
+        bool tu[LOSS > 0 ? kSpRows : 1][3];
+        if constexpr (LOSS > 0) {
+#pragma unroll
+            for (int t = 0; t < kSpRows; ++t)
+#pragma unroll
+                for (int c = 0; c < 3; ++c) {
+                    const int y = y0 + t;
+                    bool used = y < g.H;
+                    int64_t ti = c * npx + (int64_t)y * g.W + px;
+                    if (LOSS == 2 && c > 0) {
+                        used = used && (y % 2 == 0) && (px % 2 == 0) && (y / 2) < h2 && (px / 2) < w2;
+                        ti = npx + (int64_t)(c - 1) * h2 * w2 + (int64_t)(y / 2) * w2 + px / 2;
+                    }
+                    tu[t][c] = used;
+                    tv[t][c] = used ? tgt[(int64_t)b * tstride + ti] : 0.f;
+                }
+        }
 #pragma unroll
         for (int t = 0; t < kSpRows; ++t) {
             if (y0 + t >= g.H) break;
@@ -1141,16 +1162,9 @@ __global__ __launch_bounds__(kT) void t_sp_fwd(const float *__restrict__ in, Geo
                 const int64_t e = c * npx + (int64_t)t * g.W;
                 if (LOSS == 0 || store_out) o[e] = a;
                 if constexpr (LOSS > 0) { // t_loss on this pixel, same arithmetic
-                    const int y = y0 + t;
-                    bool used = true;
-                    int64_t ti = c * npx + (int64_t)y * g.W + px;
-                    if (LOSS == 2 && c > 0) {
-                        used = (y % 2 == 0) && (px % 2 == 0) && (y / 2) < h2 && (px / 2) < w2;
-                        ti = npx + (int64_t)(c - 1) * h2 * w2 + (int64_t)(y / 2) * w2 + px / 2;
-                    }
                     float gv = 0.f;
-                    if (used) {
-                        const float vc = fminf(fmaxf(a, 0.f), 1.f), d = vc - tgt[(int64_t)b * tstride + ti];
+                    if (tu[t][c]) {
+                        const float vc = fminf(fmaxf(a, 0.f), 1.f), d = vc - tv[t][c];
                         se += d * d;
                         gv = (a >= 0.f && a <= 1.f) ? k2 * d : 0.f;
                     }
