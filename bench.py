@@ -531,9 +531,29 @@ def encoder_shard(rank: int, lambdas=None):
 
 # Per-kernel rooflines of the encoder's training step, from a committed rocprofv3 kernel trace
 # of tools/bench_train.py 8 with CCMI_ARM_OVERLAP=0 (every kernel alone; 8 frames of 512 x 768,
-# hop, c3x; one launch per iteration each; tools/gpu_r5e.sh)
+# hop, c3x; one launch per iteration each).  A HISTORICAL profile, not this run: its sidecar
+# <csv>.sources.json records the sha256 of the kernel sources it was measured on, and the
+# bench line says whether today's sources still match (profile_provenance).
 TRAIN_PROFILE = "profiles/r5zl_train_iso_kernel_stats.csv"
 TRAIN_FRAMES, TRAIN_H, TRAIN_W = 8, 512, 768
+
+
+def profile_provenance(csv_path: str) -> dict:
+    """Which sources a committed profile was measured on, and whether they are still today's:
+    {"profile", "measured_at_commit", "sources_match_current": bool | None, "changed": [...]}."""
+    import hashlib
+    side = ROOT / (csv_path + ".sources.json")
+    out = {"profile": csv_path, "kind": "historical rocprofv3 trace (committed), not measured by this run"}
+    if not side.exists():
+        out["sources_match_current"] = None
+        return out
+    meta = json.loads(side.read_text())
+    changed = [f for f, h in meta.get("sha256", {}).items()
+               if not (ROOT / f).exists() or hashlib.sha256((ROOT / f).read_bytes()).hexdigest() != h]
+    out.update(measured_at_commit=meta.get("commit"), sources_match_current=not changed, changed=changed)
+    if changed:
+        print(f"warning: {csv_path} was measured on other sources than today's ({', '.join(changed)})", file=sys.stderr)
+    return out
 
 
 def train_kernel_rooflines(csv_path: str = TRAIN_PROFILE) -> list:
@@ -562,7 +582,7 @@ def train_kernel_rooflines(csv_path: str = TRAIN_PROFILE) -> list:
                     "flop_per_launch": fl, "avg_us": round(us, 2), "achieved": round(ach, 3),
                     "peak": PEAK_FP32_TFLOPS, "unit": "TFLOP/s", "frac": round(ach / PEAK_FP32_TFLOPS, 4),
                     "launch": f"{TRAIN_FRAMES} frames {TRAIN_H}x{TRAIN_W}, one per iteration",
-                    "source": csv_path})
+                    "source": profile_provenance(csv_path)})
     return out
 
 
@@ -659,7 +679,7 @@ def compare_with_reference(recs, lambdas):
     return out
 
 
-def cpu_encoder_baseline(iters: int = 2):
+def cpu_encoder_baseline(iters: int = 10, warm: int = 2):
     """The CPU oracle (torch fp32 autograd restatement of the training step, same math) at
     512x768: seconds per iteration on this host's cores, projected onto the c3x schedule.
     Also the reference-equivalent rate: the reference encoder's own s/iteration was measured
@@ -671,20 +691,23 @@ def cpu_encoder_baseline(iters: int = 2):
     st = to.TrainState(mp, [0.01 * torch.randn(h, w, generator=g) for h, w in mp.sizes])
     tgt = {"y": torch.rand(512, 768), "u": torch.rand(256, 384), "v": torch.rand(256, 384)}
     opt = to.Adam(st.params(), 1e-2)
-    to.grads(st, tgt, "softround", 0.3, 1e-3, True)
-    t0 = time.perf_counter()
-    for _ in range(iters):
+    ts = []
+    for it in range(warm + iters):
+        t0 = time.perf_counter()
         to.grads(st, tgt, "softround", 0.3, 1e-3, True)
         opt.step()
-    per = (time.perf_counter() - t0) / iters
+        ts.append(time.perf_counter() - t0)
+    ts = ts[warm:]
+    per = sum(ts) / iters
     # per image: 5 x 400 + 2 x 400 warm-up candidate iterations + 13,100 phase iterations
     per_image = per * (5 * 400 + 2 * 400 + 13100)
     cal = json.loads((ROOT / "tests/golden/cpu_calibration.json").read_text())["512x768"]
     ratio = cal["port_over_reference"]
     return {"value": round(3600.0 / per_image, 3), "unit": "images/hr", "cores": torch.get_num_threads(),
-            "kind": "port", "sample": f"{iters} training iterations at 512x768 (oracle/train_oracle.py, torch fp32 "
-                                      f"autograd on CPU, {torch.get_num_threads()} threads): {per * 1e3:.0f} ms/iteration, "
-                                      f"projected onto the 15,900 image-iterations of c3x",
+            "kind": "port", "sample": f"{iters} training iterations at 512x768 after {warm} untimed ones "
+                                      f"(oracle/train_oracle.py, torch fp32 autograd on CPU, {torch.get_num_threads()} "
+                                      f"threads): mean {per * 1e3:.0f} ms/iteration (min {min(ts) * 1e3:.0f}, max "
+                                      f"{max(ts) * 1e3:.0f}), projected onto the 15,900 image-iterations of c3x",
             "reference_equivalent_value": round(3600.0 / per_image * ratio, 3),
             "calibration": {"port_over_reference_s_per_iter": round(ratio, 4), "threads": 8,
                             "source": "tests/golden/cpu_calibration.json (reference train step vs oracle, same host)"}}

@@ -26,7 +26,7 @@ EXPORTED = [
     "ccmi_arm_forward_f32", "ccmi_arm_context_f32", "ccmi_arm_mlp_f32", "ccmi_ups_workspace_bytes", "ccmi_ups_forward_f32",
     "ccmi_syn_workspace_bytes", "ccmi_syn_forward_f32", "ccmi_post_f32", "ccmi_decode_forward_f32",
     "ccmi_decode_file", "ccmi_decode_batch", "ccmi_decode_output_size", "ccmi_decode_last_timing",
-    "ccmi_decode_latents", "ccmi_decode_batch_workspace_bytes", "ccmi_decode_batch_plan", "ccmi_decode_batch_ws", "ccmi_decode_weights_i32",
+    "ccmi_decode_last_arm_flags", "ccmi_decode_latents", "ccmi_decode_batch_workspace_bytes", "ccmi_decode_batch_plan", "ccmi_decode_batch_ws", "ccmi_decode_weights_i32",
     "ccmi_ups_workspace_bytes_i32", "ccmi_ups_forward_i32", "ccmi_syn_workspace_bytes_i32", "ccmi_syn_forward_i32",
     "ccmi_cool_parse", "ccmi_code_wb", "ccmi_decode_wb", "ccmi_code_latent_layer", "ccmi_arm_forward_i32",
     "ccmi_encode_frame", "ccmi_row_reduce_f32", "ccmi_train_param_count", "ccmi_train_workspace_bytes", "ccmi_train_step",
@@ -144,6 +144,9 @@ def lib() -> C.CDLL:
     L.ccmi_decode_output_size.restype = C.c_int
     L.ccmi_decode_last_timing.argtypes = [C.POINTER(C.c_float)]
     L.ccmi_decode_last_timing.restype = C.c_int
+    if hasattr(L, "ccmi_decode_last_arm_flags"):  # absent from older builds loaded for A/B runs
+        L.ccmi_decode_last_arm_flags.argtypes = [C.POINTER(C.c_uint32), C.c_int, C.POINTER(C.c_int)]
+        L.ccmi_decode_last_arm_flags.restype = C.c_int
     _lib = L
     return L
 

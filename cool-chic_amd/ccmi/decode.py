@@ -229,5 +229,20 @@ def last_timing() -> dict:
     return dict(zip(("upload", "arm_cabac", "ups_syn_out", "download"), list(ms)))
 
 
-__all__ = ["last_timing", "decode_latents", "decode_file", "decode_batch", "decode_batch_workspace_bytes", "output_size",
+# CCMI_ARM_FLAG_* (include/ccmi.h): what the latent decode of a stream did
+ARM_FLAG_TIMEOUT, ARM_FLAG_Q32, ARM_FLAG_W32, ARM_FLAG_PRE32, ARM_FLAG_BIG = 1, 2, 4, 8, 16
+
+
+def last_arm_flags() -> list[int]:
+    """Per stream of this thread's last decode call: the OR of its latent grids'
+    CCMI_ARM_FLAG_* bits (which multiply forms the ARM kernels ran; TIMEOUT = the call failed)."""
+    L = lib()
+    n = C.c_int(0)
+    check(L.ccmi_decode_last_arm_flags(None, 0, C.byref(n)))
+    out = (C.c_uint32 * max(n.value, 1))()
+    check(L.ccmi_decode_last_arm_flags(out, n.value, C.byref(n)))
+    return [int(v) for v in out[: n.value]]
+
+
+__all__ = ["last_timing", "last_arm_flags", "decode_latents", "decode_file", "decode_batch", "decode_batch_workspace_bytes", "output_size",
            "weights_i32", "ups_forward_i32", "syn_forward_i32", "CcmiError"]

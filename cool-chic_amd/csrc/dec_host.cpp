@@ -286,6 +286,16 @@ struct DevPlan {
 };
 
 thread_local float g_last_ms[4] = {0, 0, 0, 0};
+thread_local std::vector<uint32_t> g_last_flags; // per stream: OR of its grids' CCMI_ARM_FLAG_* bits
+
+// polls per two-wave wait of the chain kernel before it gives up (ArmStreamDesc::spin_cap)
+int arm_spin_cap()
+{
+    const char *e = getenv("CCMI_DEC_SPIN_CAP");
+    if (!e || !*e) return 1 << 24;
+    const long v = strtol(e, nullptr, 10);
+    return v < 0 ? 0 : v > (1L << 30) ? (1 << 30) : (int)v;
+}
 
 struct EventSet {
     hipEvent_t e[5] = {};
@@ -428,6 +438,10 @@ int decode_many(const uint8_t *const *streams, const size_t *lens, int n, uint8_
     for (int i = 0; i < n; ++i) tail_cap += dec_tail_table_bytes(fr[i].n_layers, 1);
     const size_t tail_off = tot;
     tot += align_up(tail_cap, 256);
+    // one status word per (frame, latent grid) for the ARM kernels' CCMI_ARM_FLAG_* bits
+    const size_t status_off = tot;
+    const size_t n_status = (size_t)n * CCMI_MAX_GRIDS;
+    tot += align_up(4 * n_status, 256);
 #if defined(CCMI_ARM_STAMPS)
     const size_t dbg_off = tot;
     tot += align_up(16 * 8 * (size_t)n * CCMI_MAX_GRIDS, 256);
@@ -465,6 +479,9 @@ int decode_many(const uint8_t *const *streams, const size_t *lens, int n, uint8_
     EventSet ev;
     ev.rec(0, s);
     CCMI_HIP_CHECK(hipMemcpyAsync(dev, host.data(), cst, hipMemcpyHostToDevice, s));
+    uint32_t *status = reinterpret_cast<uint32_t *>(dev + status_off);
+    CCMI_HIP_CHECK(hipMemsetAsync(status, 0, 4 * n_status, s));
+    const int spin_cap = arm_spin_cap();
 
     // ---- frames in K chunks by decode cost (coded bytes of their latent layers), cheapest
     // first.  Each chunk's ARM launch and decoder tail run on a stream of their own, so the
@@ -515,6 +532,8 @@ int decode_many(const uint8_t *const *streams, const size_t *lens, int n, uint8_
             a.weights = reinterpret_cast<const int32_t *>(dev + p.arm_off);
             a.flags = 1;
             a.dbg = nullptr;
+            a.status = status + (size_t)i * CCMI_MAX_GRIDS + l;
+            a.spin_cap = spin_cap;
 #if defined(CCMI_ARM_STAMPS)
             a.dbg = reinterpret_cast<uint64_t *>(dev + dbg_off) + 16 * (desc.size() + all_count++);
 #endif
@@ -724,7 +743,20 @@ int decode_many(const uint8_t *const *streams, const size_t *lens, int n, uint8_
     ev.rec(4, s);
     for (int i = 0; i < n && lat_out; ++i)
         CCMI_HIP_CHECK(hipMemcpyAsync(lat_out[i], dev + pl[i].lat_off, pl[i].lat_elems * 4, hipMemcpyDeviceToHost, s));
+    std::vector<uint32_t> st(n_status);
+    CCMI_HIP_CHECK(hipMemcpyAsync(st.data(), status, 4 * n_status, hipMemcpyDeviceToHost, s));
     CCMI_HIP_CHECK(hipStreamSynchronize(s));
+    g_last_flags.assign(n, 0u);
+    for (int i = 0; i < n; ++i)
+        for (int l = 0; l < CCMI_MAX_GRIDS; ++l) g_last_flags[i] |= st[(size_t)i * CCMI_MAX_GRIDS + l];
+    for (int i = 0; i < n; ++i)
+        for (int l = 0; l < CCMI_MAX_GRIDS; ++l)
+            if (st[(size_t)i * CCMI_MAX_GRIDS + l] & CCMI_ARM_FLAG_TIMEOUT)
+                // the two waves of a stream lost their hand-off: the latents cannot be trusted
+                return ccmi_set_error(CCMI_ERR_HIP,
+                                      "decode: stream %d, latent grid %d: the ARM decode's wave hand-off gave up "
+                                      "after %d polls; output discarded",
+                                      i, l, spin_cap);
     for (int i = 0; i < n && lat_out; ++i)
         for (size_t k = 0; k < pl[i].lat_elems; ++k) lat_out[i][k] >>= kArmPrec;
 #if defined(CCMI_ARM_STAMPS)
@@ -770,6 +802,15 @@ extern "C" int ccmi_decode_last_timing(float *ms4)
 {
     if (!ms4) return ccmi_set_error(CCMI_ERR_ARG, "decode_last_timing: null argument");
     for (int k = 0; k < 4; ++k) ms4[k] = g_last_ms[k];
+    return CCMI_OK;
+}
+
+extern "C" int ccmi_decode_last_arm_flags(uint32_t *flags, int cap, int *n)
+{
+    if (!n || (cap > 0 && !flags)) return ccmi_set_error(CCMI_ERR_ARG, "decode_last_arm_flags: null argument");
+    const int m = std::min(cap, (int)g_last_flags.size());
+    for (int i = 0; i < m; ++i) flags[i] = g_last_flags[i];
+    *n = (int)g_last_flags.size();
     return CCMI_OK;
 }
 

@@ -64,6 +64,8 @@ struct ArmStreamDesc {
     const int32_t *weights; // device copy of FrameHost::arm
     int32_t *out;           // device h*w plane, value << kArmPrec
     uint64_t *dbg;          // diagnostic builds only (CCMI_ARM_STAMPS): 8 counters per stream
+    uint32_t *status;       // device word, zeroed by the host: CCMI_ARM_FLAG_* bits OR-ed in by the kernel
+    int spin_cap;           // chain kernel: polls per wait before it gives up and flags CCMI_ARM_FLAG_TIMEOUT
 };
 
 // One launch for n_streams streams sharing (d, nh); max_w / max_blocks size the LDS

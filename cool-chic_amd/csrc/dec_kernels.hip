@@ -121,6 +121,12 @@ __device__ __forceinline__ int32_t imul(int32_t a, int32_t b)
     else return (int32_t)((uint32_t)a * (uint32_t)b);
 }
 
+// OR of CCMI_ARM_FLAG_* bits into the stream's status word (one lane; a vector global atomic)
+__device__ __forceinline__ void put_status(const ArmStreamDesc &S, uint32_t bits)
+{
+    if (bits && S.status) __hip_atomic_fetch_or(S.status, bits, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
 // One residual hidden layer, lane o = neuron o: (b + 256 a_o + sum_i W[o][i] a_i), ReLU, round >> 8.
 template <int D, bool F24>
 __device__ __forceinline__ int32_t arm_hidden(const int32_t (&W)[D], int32_t bias, int32_t a)
@@ -315,6 +321,7 @@ __global__ __launch_bounds__(64) void dec_arm_kernel(const ArmStreamDesc *__rest
         for (int x = lane; x < w; x += 64) dst[x] = row[x];
         __syncthreads();
     }
+    if (lane == 0) put_status(S, (big ? CCMI_ARM_FLAG_BIG : 0u) | (w24 ? 0u : CCMI_ARM_FLAG_W32));
 #if defined(CCMI_ARM_STAMPS)
     st_acc[6] = __builtin_amdgcn_s_memtime() - t_loop; // whole latent loop
     if (lane == 0 && S.dbg)
@@ -591,6 +598,7 @@ __global__ __launch_bounds__(64) void dec_arm_spec_kernel(const ArmStreamDesc *_
         for (int x = lane; x < w; x += 64) dst[x] = row[x];
         __syncthreads();
     }
+    if (lane == 0) put_status(S, (big ? CCMI_ARM_FLAG_BIG : 0u) | (w24 ? 0u : CCMI_ARM_FLAG_W32));
 #if defined(CCMI_ARM_STAMPS)
     st_acc[6] = __builtin_amdgcn_s_memtime() - t_loop;
     if (lane == 0 && S.dbg)
@@ -772,7 +780,7 @@ __global__ __launch_bounds__(128) void dec_arm_chain_kernel(const ArmStreamDesc 
 #define CSTAMP(var)
 #endif
     extern __shared__ int32_t smem[];
-    volatile int32_t *ctl = smem;                                       // [0] ready seq [1] chain seq [2] done
+    int32_t *ctl = smem;                                                // [0] ready seq [1] chain seq [2] done
     uint32_t *ctab = reinterpret_cast<uint32_t *>(smem + 4);            // 17 x 50 packed bin codes
     int32_t *w0s = smem + 4 + 17 * 50 + 2;                              // [16][16] layer-0 weights, [16] biases (16 B aligned)
     int32_t *pre = w0s + 16 * 16 + 16;                                  // [kPreRing + kPreMir][16] preG
@@ -852,6 +860,16 @@ __global__ __launch_bounds__(128) void dec_arm_chain_kernel(const ArmStreamDesc 
         __builtin_amdgcn_wave_barrier();
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
     };
+    // the two waves' hand-off words: a workgroup-scope release store publishes everything the
+    // wave wrote before it (every lane's stores: lds_order() first), an acquire load orders the
+    // reader's later LDS loads (the preG slots, the ring rows) behind the word it saw
+    auto ctl_get = [ctl](int k) __attribute__((always_inline)) {
+        return __builtin_amdgcn_readfirstlane(__hip_atomic_load(ctl + k, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP));
+    };
+    auto ctl_put = [ctl, tid](int k, int32_t v) __attribute__((always_inline)) {
+        if ((tid & 63) == 0) __hip_atomic_store(ctl + k, v, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+    };
+    const int spin_cap = S.spin_cap;
 
     if (wid == 1) {
         // ================= helper wave: preG of every chunk with a coded latent, in (row, chunk)
@@ -860,6 +878,7 @@ __global__ __launch_bounds__(128) void dec_arm_chain_kernel(const ArmStreamDesc 
         // and (b) the row above is final under the chunk's contexts (done >= its last column)
         const int dmax = blk > 0 ? 0 : 1; // no block map: every latent coded
         int seq = 0;
+        uint32_t hbits = 0;
         for (int y = 0; y < h; ++y) {
             const int brow = blk > 0 ? (y >> shift) * nbx : 0;
             for (int c = 0; c < nch; ++c, ++seq) {
@@ -874,13 +893,17 @@ __global__ __launch_bounds__(128) void dec_arm_chain_kernel(const ArmStreamDesc 
                     coded = __ballot(bb <= b1 && (f == 1 || (f == 3 && !(y & mask)))) != 0;
                 }
                 const int need = y == 0 ? 0 : (y - 1) * w + min(c * 64 + 66, w);
-                // bounded: a synchronisation bug ends in a wrong decode (caught by the md5 tests), not
-                // in a wave that never retires
-                for (int spin = 0; spin < (1 << 24); ++spin) {
-                    if (__builtin_amdgcn_readfirstlane(ctl[1]) >= seq - 3 && __builtin_amdgcn_readfirstlane(ctl[2]) >= need)
+                // bounded, so that a lost hand-off ends in a wave that retires and a status word
+                // the host turns into an error (CCMI_ARM_FLAG_TIMEOUT), never in a hang
+                bool ok = false;
+                for (int spin = 0; spin < spin_cap; ++spin) {
+                    if (ctl_get(1) >= seq - 3 && ctl_get(2) >= need) {
+                        ok = true;
                         break;
+                    }
                     __builtin_amdgcn_s_sleep(1);
                 }
+                if (!ok) hbits |= CCMI_ARM_FLAG_TIMEOUT;
                 CSTAMP(tw1);
                 LACC(15, tw1 - tw0);
                 if (coded) {
@@ -901,6 +924,7 @@ __global__ __launch_bounds__(128) void dec_arm_chain_kernel(const ArmStreamDesc 
 #pragma unroll
                     for (int i = 0; i < D; ++i) small = small && (uint32_t)(ctx[i] + (1 << 22)) < (1u << 23);
                     const bool f24 = __ballot(!small) == 0;
+                    if (!f24) hbits |= CCMI_ARM_FLAG_PRE32;
                     int32_t *dst = pre + (slot * 64 + lane) * 16;
                     int32_t *mir = pre + (kPreRing + lane) * 16;
                     auto sums = [&](auto F24) __attribute__((always_inline)) {
@@ -939,11 +963,12 @@ __global__ __launch_bounds__(128) void dec_arm_chain_kernel(const ArmStreamDesc 
                     LACC(14, 1);
                 }
                 lds_order();
-                if (lane == 0) ctl[0] = seq + 1;
+                ctl_put(0, seq + 1);
                 CSTAMP(tw2);
                 LACC(12, tw2 - tw1);
             }
         }
+        if (lane == 0) put_status(S, hbits);
 #if defined(CCMI_ARM_STAMPS)
         if (lane >= 12 && lane < 16 && S.dbg) S.dbg[lane] = st_v;
 #endif
@@ -983,6 +1008,7 @@ __global__ __launch_bounds__(128) void dec_arm_chain_kernel(const ArmStreamDesc 
     uint32_t qspan = 0;
     // 0: 24-bit layer 0 + 24-bit hidden / output layers; 1: 32-bit layer 0; 2: all 32-bit
     int mode = w24 ? 0 : 2;
+    uint32_t cbits = 0;
 #if defined(CCMI_ARM_STAMPS)
     LACC(5, __builtin_amdgcn_s_memtime() - t_begin);
     const uint64_t t_loop = __builtin_amdgcn_s_memtime();
@@ -1009,16 +1035,23 @@ __global__ __launch_bounds__(128) void dec_arm_chain_kernel(const ArmStreamDesc 
             if (lane < x - xb) row[xb + lane] = vrow;
             xb = x;
             lds_order();
-            if (lane == 0) ctl[2] = y * w + x;
+            ctl_put(2, y * w + x);
         };
         // preG for latents up to x + 7: publish the chain's chunk (frees the slots before it) and
         // wait for the helper
         auto wait_pre = [&]() __attribute__((always_inline)) {
             CSTAMP(tq0);
             const int need = (min(x + 8, w) - 1) >> 6;
-            if (lane == 0) ctl[1] = rseq + (x >> 6);
-            for (int spin = 0; spin < (1 << 24) && __builtin_amdgcn_readfirstlane(ctl[0]) <= rseq + need; ++spin)
-                __builtin_amdgcn_s_sleep(1); // bounded, as the helper's wait
+            ctl_put(1, rseq + (x >> 6));
+            bool ok = false;
+            for (int spin = 0; spin < spin_cap; ++spin) { // bounded, as the helper's wait
+                if (ctl_get(0) > rseq + need) {
+                    ok = true;
+                    break;
+                }
+                __builtin_amdgcn_s_sleep(1);
+            }
+            if (!ok) cbits |= CCMI_ARM_FLAG_TIMEOUT;
             pre_lim = (need + 1) * 64 >= w ? 0x7FFFFFFF : (need + 1) * 64;
             CSTAMP(tq1);
             LACC(7, tq1 - tq0);
@@ -1161,11 +1194,12 @@ __global__ __launch_bounds__(128) void dec_arm_chain_kernel(const ArmStreamDesc 
         flush(); // done = (y + 1) w: the whole row is final
         // the chain is past every chunk of this row: without this, rows with no coded run (no
         // wait_pre) left the helper waiting for slots forever (the decode's last rows, uncoded)
-        if (lane == 0) ctl[1] = (y + 1) * nch;
+        ctl_put(1, (y + 1) * nch);
         int32_t *dst = S.out + (int64_t)y * w;
         for (int i = lane; i < w; i += 64) dst[i] = row[i];
         LACC(9, __builtin_amdgcn_s_memtime() - tw0);
     }
+    if (lane == 0) put_status(S, cbits | (mode == 1 ? CCMI_ARM_FLAG_Q32 : 0u) | (w24 ? 0u : CCMI_ARM_FLAG_W32));
 #if defined(CCMI_ARM_STAMPS)
     LACC(6, __builtin_amdgcn_s_memtime() - t_loop);
     if (lane < 12 && S.dbg) S.dbg[lane] = st_v;

@@ -212,6 +212,20 @@ int ccmi_decode_batch(const uint8_t *const *streams, const size_t *lens, int n,
  * [3] download of the decoded bytes. */
 int ccmi_decode_last_timing(float *ms4);
 
+/* What the latent decode of this thread's last ccmi_decode_* call did, per stream: flags[i]
+ * ORs the CCMI_ARM_FLAG_* bits of stream i's latent grids (*n = streams reported, at most
+ * cap).  TIMEOUT is an error (the call itself returned CCMI_ERR_HIP and discarded the
+ * output); the other bits say which integer multiply forms ran, i.e. which paths a stream
+ * exercised (the reference's int32 ARM, arm_cpu.cpp:65-95, has one form).  The chain kernel's
+ * wait limit is 2^24 polls, or the environment's CCMI_DEC_SPIN_CAP (a test hook: 0 makes
+ * every wait give up at once). */
+#define CCMI_ARM_FLAG_TIMEOUT 1u  /* a two-wave synchronisation wait gave up: decode invalid */
+#define CCMI_ARM_FLAG_Q32 2u      /* chain kernel: a |q| > 16383 switched layer 0 to 32-bit products */
+#define CCMI_ARM_FLAG_W32 4u      /* an ARM weight >= 2^23: every layer in 32-bit products */
+#define CCMI_ARM_FLAG_PRE32 8u    /* chain helper wave: a chunk's contexts left 22 bits (32-bit sums) */
+#define CCMI_ARM_FLAG_BIG 16u     /* spec / one-latent kernels: a |q| >= 2^15, layer 0 in 32-bit */
+int ccmi_decode_last_arm_flags(uint32_t *flags, int cap, int *n);
+
 /* The integer latents of one intra stream (ARM + CABAC decode on the GPU; values, not
  * shifted), grids flattened in order: out needs sum_l h_l * w_l int32 (host buffer). */
 int ccmi_decode_latents(const uint8_t *stream, size_t len, int32_t *out, size_t cap, void *stream_handle);

@@ -304,6 +304,16 @@ def test_gpu_gradients_synthesis_and_grid_variants(n_grids, layers, yuv420, gpu)
     _random_arch_vs_oracle(gpu, 42, 66, n_grids, n_grids=n_grids, layers=fo.parse_layers(layers), yuv420=yuv420)
 
 
+@pytest.mark.parametrize("H,W", [(33, 65), (17, 1), (1, 70), (2, 1), (81, 129)])
+def test_gpu_gradients_border_tile_shapes(H, W, gpu):
+    """Sizes whose last image row / column is the first of a 16 x 64 backward tile (H = 1 mod
+    16, W = 1 mod 64) and 1-pixel image sides: the 3x3 backward's replicate-padding adjoint
+    post-pass (t_sp_bwd<3>) then excludes ring slots and adds both edge terms of one pixel, and
+    every pyramid level is 1 wide or 1 high.  The reference pads by replication
+    (synthesis.py:264-277); the oracle's autograd differentiates exactly that."""
+    _random_arch_vs_oracle(gpu, H, W, 7 * H + W)
+
+
 def test_gpu_batch_of_frames_each_with_own_network(gpu):
     """Frames in a batch are independent: frame b's gradient equals a batch-of-1 run."""
     z = np.load(FILES[1])

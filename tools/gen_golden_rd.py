@@ -394,6 +394,13 @@ if __name__ == "__main__":
         gen_bd(GOLD / "bd_reference.json")
     if what in ("debug", "all"):
         run_rd("debug", GOLD / "rd_reference_debug.json")
+    if what == "debug_seeds":
+        # more reference seeds for the debug preset into their own file (merged by hand):
+        # python tools/gen_golden_rd.py debug_seeds IMAGE SEEDS THREADS OUT ARCH
+        img, sd, th, out, arch = sys.argv[2:7]
+        torch.set_num_threads(int(th))
+        run_rd("debug", Path(out), images=[img], seeds=[int(x) for x in sd.split(",")], arch=arch)
+        sys.exit(0)
     if what == "debug_default":  # the reference's default decoder (arm 24,2; 40-wide head)
         if len(sys.argv) > 2:
             torch.set_num_threads(int(sys.argv[2]))
