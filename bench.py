@@ -43,6 +43,11 @@ HOP = [(48, 1, False, True), (3, 1, False, False), (3, 3, True, True), (3, 3, Tr
 DIM_ARM, N_HIDDEN, N_GRIDS, GAIN = 16, 2, 7, 16.0
 PEAK_FP32_TFLOPS = 157.3  # MI355X FP32 (vector == f32-MFMA rate), MI355X_MICROARCH.md
 PEAK_HBM_GBS = 8000.0
+# int32 multiply-add on the VALU: v_mad_i32_i24 / v_mad_u32_u24 issue one per lane per clock,
+# unpacked -- half the packed-f32 FMA rate of PEAK_FP32_TFLOPS (MI355X_MICROARCH.md lists no
+# integer VALU peak; this is the f32 vector peak without v_pk_fma_f32's second lane), counted
+# as 2 ops per multiply-add like the FLOPs.  v_mul_lo_u32 (the 32-bit form) is quarter rate.
+PEAK_INT32_TOPS = PEAK_FP32_TFLOPS / 2
 
 
 def sizes(h=H, w=W, n=N_GRIDS):
@@ -417,6 +422,75 @@ def bench_single_stream_decode(cls: str = "E", reps: int = 3, ref_reps: int = 2)
     return out
 
 
+# committed rocprofv3 kernel traces of the path-B batch decode (tools/bench_decode.py under
+# rocprofv3 --kernel-trace --stats), per class; historical, with a sources sidecar
+DECODE_PROFILE = {"E": "profiles/r6d_decode_E_kernel_stats.csv", "B": "profiles/r6d_decode_B_kernel_stats.csv"}
+
+
+def path_b_tail_work(streams) -> dict:
+    """Algorithmic work of the integer decoder tail per batch (from the streams' headers):
+    syn_ops -- 2 x the synthesis multiply-adds (every layer n_in x n_out x ks^2 per pixel,
+    synfused_cpu.hpp / syn_cpu.hpp); ups_bytes -- HBM bytes of the pyramid steps (each
+    dec_ups_level reads the level-k stack and the level-(k-1) latent and writes the C+1
+    channels of level k-1, int32; ups_refine_cpu.hpp / ups_upsample_cpu.hpp)."""
+    from ccmi import encode
+    syn_ops = ups_bytes = 0
+    for data in streams:
+        fr = encode.parse(data)
+        d = fr.desc
+        sz = fr.grid_sizes
+        npx = d.h * d.w
+        c = d.n_grids
+        for i in range(d.n_syn_layers):
+            syn_ops += 2 * npx * c * d.syn_out[i] * d.syn_ks[i] * d.syn_ks[i]
+            c = d.syn_out[i]
+        L = d.n_grids
+        for j in range(L - 2, -1, -1):  # destination level j from the (L-1-j)-channel stack of level j+1
+            C = L - 1 - j
+            ups_bytes += 4 * (C * sz[j + 1][0] * sz[j + 1][1] + sz[j][0] * sz[j][1] + (C + 1) * sz[j][0] * sz[j][1])
+    return {"syn_ops": syn_ops, "ups_bytes": ups_bytes}
+
+
+def path_b_tail_roofline(streams, cls: str, tail_ms: float) -> dict:
+    """Roofline of the data-parallel int32 tail of path B: the dominant tail kernel
+    (dec_syn_fused_batch, int32 VALU-bound) and the pyramid (dec_ups_level_batch, HBM), each as
+    algorithmic work / its total time in the committed trace of the same batch (every launch of
+    that kernel summed: one per geometry group and pyramid step), plus the live tail stage of
+    this run (ccmi_decode_last_timing: upsampling + synthesis + output together)."""
+    import csv
+    wk = path_b_tail_work(streams)
+    out = {"syn_ops_per_batch": wk["syn_ops"], "ups_hbm_bytes_per_batch": wk["ups_bytes"],
+           "live_tail_stage": {"ms": round(tail_ms, 3),
+                               "int32_tops_syn_only": round(wk["syn_ops"] / (tail_ms * 1e-3) / 1e12, 3)}}
+    path = DECODE_PROFILE.get(cls)
+    if path and (ROOT / path).exists():
+        rows = list(csv.DictReader((ROOT / path).open()))
+        meta = json.loads((ROOT / (path + ".sources.json")).read_text()) if (ROOT / (path + ".sources.json")).exists() else {}
+        frames_prof = int(meta.get("frames", 0)) or None
+        scale = len(streams) / frames_prof if frames_prof else None
+        def tot(key):
+            r = next((r for r in rows if key in r["Name"]), None)
+            return (float(r["TotalDurationNs"]) * 1e-9, int(r["Calls"])) if r else (None, 0)
+        ts, ns = tot("dec_syn_fused_batch")
+        tu, nu = tot("dec_ups_level_batch")
+        if ts and scale:
+            ach = wk["syn_ops"] / scale / ts / 1e12
+            out.update(bound="int32-valu", kernel="dec_syn_fused_batch", achieved=round(ach, 3), peak=PEAK_INT32_TOPS,
+                       unit="TOPS (int32, 2 per multiply-add)", frac=round(ach / PEAK_INT32_TOPS, 4),
+                       kernel_ms_per_batch=round(ts * 1e3, 3), launches=ns)
+        if tu and scale:
+            gbs = wk["ups_bytes"] / scale / tu / 1e9
+            out["pyramid"] = {"kernel": "dec_ups_level_batch", "bound": "hbm", "achieved": round(gbs, 1),
+                              "peak": PEAK_HBM_GBS, "unit": "GB/s", "frac": round(gbs / PEAK_HBM_GBS, 4),
+                              "ms_per_batch": round(tu * 1e3, 3), "launches": nu}
+        out["source"] = profile_provenance(path)
+        out["profiled_frames"] = frames_prof
+        out["note"] = ("batches of >= 64 streams run in two cost-ordered chunks: the cheap chunk's tail kernels "
+                       "share the CUs with the other chunk's ARM chains (dec_host.cpp), so these kernel times "
+                       "include that sharing")
+    return out
+
+
 def bench_bitexact_decode(reps: int, cls: str = "E", H=H, W=W, rank=0, world=1, dist=None, dev=None):
     """Path B: the bit-exact HIP decoder on the shipped JVET class-`cls` .cool streams
     (class E: 15 files at 1280x720; class B: 5 committed files at 1920x1080).  Weak scaling:
@@ -450,6 +524,7 @@ def bench_bitexact_decode(reps: int, cls: str = "E", H=H, W=W, rank=0, world=1, 
             "per_gpu_kernels": round(len(job) * H * W / t["kern_s"] / 1e6, 2),
             "per_gpu_wall": round(len(job) * H * W / t["wall"] / 1e6, 2),
             "stage_ms": {k: round(v, 3) for k, v in tm.items()},
+            "roofline": path_b_tail_roofline(streams, cls, tm["ups_syn_out"]),
             "bit_exact_vs_reference_md5": int(c["exact"]) == world,
             "scaling": "weak",
             "data": f"{len(files)} shipped JVET class-{cls} .cool bitstreams (results/image/jvet), x{reps} per GPU"}

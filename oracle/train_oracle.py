@@ -75,9 +75,11 @@ class TrainState:
         return out
 
 
-def loss(st: TrainState, target, qtype, t, lmbda, yuv420, noise=None):
+def loss(st: TrainState, target, qtype, t, lmbda, yuv420, noise=None, keep=None):
     """Training forward + loss.  target: [3,H,W] (444) or dict(y, u, v).  Returns
-    (loss, mse, rate_bit_sum)."""
+    (loss, mse, rate_bit_sum).  keep (a dict, tests only): receives the ARM outputs mu and
+    log_scale with their gradients retained, so a test can see the per-latent terms a
+    bias gradient sums."""
     mp = st.mp
     flat = torch.cat([x.reshape(-1) for x in st.lat]) * mp.gain
     q = quantize(flat, qtype, t, noise)
@@ -86,7 +88,11 @@ def loss(st: TrainState, target, qtype, t, lmbda, yuv420, noise=None):
         grids.append(q[o:o + h * w].view(h, w))
         o += h * w
     ctx = torch.cat([fo.context(x, mp.dim_arm) for x in grids], dim=0)
-    mu, scale, _ = fo.arm_mlp(ctx, st.arm)
+    mu, scale, log_scale = fo.arm_mlp(ctx, st.arm)
+    if keep is not None:
+        mu.retain_grad()
+        log_scale.retain_grad()
+        keep.update(mu=mu, log_scale=log_scale)
     r = fo.rate(q, mu, scale)
     ups = fo.upsampling(grids, [fo.sym_kernel(h, mp.ups_k) for h in st.ups],
                         [fo.sym_kernel(h, mp.pre_k) for h in st.pre])

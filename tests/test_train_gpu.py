@@ -47,8 +47,10 @@ def _flat_grads(st):
     return torch.cat([p.grad.reshape(-1) for p in st.params()]).numpy()
 
 
-def _grad_close(got, ref, name):
+def _grad_close(got, ref, name, floor=None):
     tol = 2e-3 * np.abs(ref) + 1e-7 + 2e-4 * np.abs(ref).max()
+    if floor is not None:
+        tol = np.maximum(tol, floor)
     if "latent_grids" in name:
         # the rate term's 1 / P with P cancelling in fp32 deep in the Laplace tails (header):
         # at most 0.1 % of a latent grid's entries may reach 4x the tolerance
@@ -56,7 +58,7 @@ def _grad_close(got, ref, name):
         assert np.mean(err > tol) <= 1e-3 and np.all(err <= 4 * tol), \
             (name, int((err > tol).sum()), float((err / tol).max()))
     else:
-        np.testing.assert_allclose(got, ref, rtol=2e-3, atol=1e-7 + 2e-4 * np.abs(ref).max(), err_msg=name)
+        assert np.all(np.abs(got - ref) <= tol), (name, got, ref, tol)
 
 
 def _adam_close(got, ref, lr, name, g0=None):
@@ -258,7 +260,14 @@ def _random_arch_vs_oracle(gpu, H, W, seed, K=8, Kp=7, yuv420=False, **kw):
         target, tflat = img, img.reshape(-1)
     st = to.TrainState(mp, lat)
     noise = to.kumaraswamy(torch.rand(arch.n_latents, generator=g), 2.0)
-    to.grads(st, target, "softround", 0.3, 1e-3, yuv420, noise=noise)
+    keep = {}
+    to.grads(st, target, "softround", 0.3, 1e-3, yuv420, noise=noise, keep=keep)
+    # the ARM output biases' gradients are plain sums over the latents of dL/dmu and
+    # dL/dlog_scale; on tiny frames those few terms can cancel (17 x 1: four terms of +-5e-3 sum
+    # to 5e-5), so their absolute floor is 2e-4 x the sum of the terms' magnitudes rather than
+    # of the (cancelled) result -- the same 2e-4-relative bar per term as every other tensor
+    bias_floor = np.array([float(keep["mu"].grad.abs().sum()), float(keep["log_scale"].grad.abs().sum())])
+    out_bias = 2 * (mp.n_hidden + 1) + mp.n_grids - 1  # index of the ARM output-layer bias in st.params()
     of = T.Overfitter(arch, torch.cat([x.reshape(-1) for x in lat])[None].to(gpu),
                       T.pack_params(mp.arm, mp.ups_half, mp.pre_half, mp.syn)[None].to(gpu),
                       tflat[None].to(gpu), yuv420=yuv420)
@@ -270,7 +279,7 @@ def _random_arch_vs_oracle(gpu, H, W, seed, K=8, Kp=7, yuv420=False, **kw):
     for i, p in enumerate(st.params()):
         n = p.numel()
         _grad_close(got[o:o + n], p.grad.reshape(-1).numpy(), f"{kw} K={K} Kp={Kp} tensor {i}" +
-                    (" latent_grids" if i < mp.n_grids else ""))
+                    (" latent_grids" if i < mp.n_grids else ""), floor=2e-4 * bias_floor if i == out_bias else None)
         o += n
 
 

@@ -1,5 +1,5 @@
 """Per-phase cycles of the fused decode kernel (diagnostic stamps build):
-CCMI_LIB=cool-chic_amd/lib/libccmi_stamps.so python tools/prof_fused.py"""
+CCMI_LIB=cool-chic_amd/lib/diag/libccmi_stamps.so python tools/prof_fused.py"""
 import ctypes
 import sys
 from pathlib import Path

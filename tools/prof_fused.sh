@@ -18,7 +18,7 @@ run() { # name seconds command...
     if [ $rc -ne 0 ]; then tail -30 "$OUT/$name.log"; exit $rc; fi
 }
 BENCH="$ROOT/bench.py --steps 5 --warmup 2 --no-cpu-baseline --decode-reps 0 --encode-images 0 --hd-steps 0 --hd-decode-reps 0 --serial"
-run stamps 120 env CCMI_LIB=$ROOT/cool-chic_amd/lib/libccmi_stamps.so python3 $ROOT/tools/prof_fused.py
+run stamps 120 env CCMI_LIB=$ROOT/cool-chic_amd/lib/diag/libccmi_stamps.so python3 $ROOT/tools/prof_fused.py
 run syn_micro 120 python3 $ROOT/tools/syn_micro.py
 run trace 180 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/trace -- python3 $BENCH
 run pmc1 120 rocprofv3 --pmc SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_INSTS_VALU SQ_ACTIVE_INST_VALU SQ_INSTS_LDS SQ_WAIT_ANY SQ_WAIT_INST_ANY GRBM_GUI_ACTIVE GRBM_COUNT --output-format csv -d $OUT/pmc1 -- python3 $BENCH
