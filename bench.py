@@ -76,11 +76,16 @@ def flops_per_frame(H=H, W=W):
     return {"arm": 2 * arm_mac, "ups": 2 * ups_mac, "syn": 2 * syn_mac, "n_lat": n_lat}
 
 
-def flops_fused_per_frame(H=H, W=W):
-    """The fused kernel: last upsampling step (level 1 -> 0) + synthesis (+ post, no flops)."""
+def flops_fused_per_frame(H=H, W=W, fold=None):
+    """The fused kernel: last upsampling step (level 1 -> 0) + synthesis (+ post, no flops);
+    with the fold also the level-2 -> 1 step (each counted once, halo recompute not)."""
+    fold = Pipeline.fold if fold is None else fold
     fl = flops_per_frame(H, W)
-    h0, w0 = sizes(H, W)[0]
+    s = sizes(H, W)
+    h0, w0 = s[0]
     last_ups = 2 * h0 * w0 * (14 + 8 * (N_GRIDS - 1))
+    if fold:
+        last_ups += 2 * s[1][0] * s[1][1] * (14 + 8 * (N_GRIDS - 2))
     return last_ups + fl["syn"]
 
 
@@ -93,8 +98,10 @@ def bytes_per_frame(H=H, W=W):
             "ups": 4 * (n_lat + N_GRIDS * npx),          # read latents, write dense synthesis input
             "syn": 4 * (N_GRIDS * npx + 3 * npx),        # read dense input, write 3 planes
             "post": 4 * (3 * npx + npx * 3 // 2),
-            # fused: read the level-1 stack + full-res latent, write the 420 frame
-            "decode_fused": 4 * ((N_GRIDS - 1) * h1 * w1 + npx + npx * 3 // 2)}
+            # fused: read the level-1 stack + full-res latent, write the 420 frame; folded: the
+            # level-2 stack + the level-1 and full-res latents instead of the level-1 stack
+            "decode_fused": 4 * ((N_GRIDS - 2) * s[2][0] * s[2][1] + h1 * w1 + npx + npx * 3 // 2) if Pipeline.fold
+            else 4 * ((N_GRIDS - 1) * h1 * w1 + npx + npx * 3 // 2)}
 
 
 def _oracle():
@@ -122,6 +129,7 @@ class Pipeline:
     """Preallocated buffers + direct C-ABI launches (no per-step allocation)."""
 
     head = 0  # ccmi_decode_args.head (CCMI_HEAD_*), set from --head
+    fold = False  # --fold: the pyramid's level-2 -> 1 step inside the fused kernel (stages bit 3, opt-in)
 
     def __init__(self, inp, B, dev):
         import ctypes
@@ -154,7 +162,8 @@ class Pipeline:
         # fused decode tail: pyramid (levels 6 -> 1) then ONE kernel for the last
         # upsampling step + synthesis + 420 post (no dense stack, no raw synthesis output)
         self.dec = [ccmi.DecodeArgs(ups=self.ups, syn=self.synargs, bitdepth=8, yuv420=1, out=p(self.yuv),
-                                    out_stride=self.yuv.shape[1], stages=st, head=Pipeline.head) for st in (1, 2)]
+                                    out_stride=self.yuv.shape[1], stages=st | (8 if Pipeline.fold else 0),
+                                    head=Pipeline.head) for st in (1, 2)]
         self.byref = ctypes.byref
         self.stream = torch.cuda.current_stream(dev)
         # the ARM (rate) and the decode tail (pixels) only share the latents: with overlap
@@ -866,6 +875,8 @@ def main():
     ap.add_argument("--no-graph", action="store_true",
                     help="time the eager launches instead of HIP-graph replays of the fused pipeline")
     ap.add_argument("--hd-steps", type=int, default=20, help="steps of the 1920x1080 float-forward leg (0: skip)")
+    ap.add_argument("--fold", action="store_true",
+                    help="evaluate the level-2 -> 1 upsampling step inside the fused kernel (opt-in; measured slower)")
     ap.add_argument("--head", choices=("default", "valu", "mfma"), default="default",
                     help="the fused kernel's 1x1 synthesis head: fp32 VALU or f32 MFMA (CCMI_HEAD_*)")
     ap.add_argument("--hd-decode-reps", type=int, default=64,
@@ -906,6 +917,7 @@ def main():
 
     B = args.batch
     Pipeline.head = {"default": 0, "valu": 1, "mfma": 2}[args.head]
+    Pipeline.fold = args.fold and args.head != "mfma"
     inp = make_inputs(B, dev, seed=1000 * rank + 1)
     mode = "staged" if args.staged else "fused"
     ovp = args.overlap_pyramid and not args.serial and mode == "fused"
@@ -955,7 +967,9 @@ def main():
         "config": {"workload": "1280x720 YUV420 8-bit frames, hop/c3x decoder (arm 16x2, syn 48-1/3-1/3-3r/3-3r, "
                                "7 latent grids), float forward ARM+rate -> upsampling -> synthesis -> 420 post",
                    "frames_per_step_per_gpu": B, "parallelism": f"image-parallel x{world}",
-                   "kernels": ("ARM | upsampling pyramid | fused last-upsampling+synthesis+post" if mode == "fused"
+                   "kernels": (("ARM | upsampling pyramid (to level 2) | fused level-2->1 + last upsampling + synthesis + post"
+                                if Pipeline.fold else "ARM | upsampling pyramid | fused last-upsampling+synthesis+post")
+                               if mode == "fused"
                                else "ARM | upsampling | synthesis | post")
                    + (" (ARM on a second stream, concurrent with the pyramid)" if ovp else
                       " (ARM on a second stream, concurrent)" if overlap else " (one stream)")},

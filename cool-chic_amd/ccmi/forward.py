@@ -173,10 +173,12 @@ def post_forward(x: torch.Tensor, bitdepth: int = 8, yuv420: bool = False) -> to
 
 def decode_forward(latent: torch.Tensor, sizes, ups_params: torch.Tensor, ups_k: int, n_ups: int, pre_k: int,
                    n_pre: int, layers, syn_params: torch.Tensor, gain: float = 16.0, quantize: bool = True,
-                   bitdepth: int = 8, yuv420: bool = False, head: int = 0) -> torch.Tensor:
+                   bitdepth: int = 8, yuv420: bool = False, head: int = 0, fold: bool = False) -> torch.Tensor:
     """Fused upsampling -> synthesis -> post (ccmi_decode_forward_f32): latent [B, N] ->
     post-processed frames (layout of post_forward), or with bitdepth=0 the raw synthesis
     output [B, C_out, H, W].  head: ccmi.HEAD_* (the 1x1 head on the VALU or on f32 MFMA).
+    fold=True also evaluates the level-2 -> 1 upsampling step inside the fused kernel (stages
+    bit 3, opt-in: the same values bit for bit, measured slower).
     Raises CcmiError(ERR_UNSUPPORTED) for architectures without a fused kernel (use
     ups_forward / syn_forward / post_forward)."""
     squeeze = latent.dim() == 1
@@ -213,7 +215,7 @@ def decode_forward(latent: torch.Tensor, sizes, ups_params: torch.Tensor, ups_k:
                   B, L, H, W, syn_stride)
     y.in_ = None
     a = DecodeArgs(ups=u, syn=y, bitdepth=int(bitdepth), yuv420=int(bool(yuv420)), out=ptr(out), out_stride=n,
-                   head=int(head))
+                   head=int(head), stages=8 if fold else 0)
     check(lib().ccmi_decode_forward_f32(a, stream_handle(latent.device)))
     if bitdepth == 0 or not yuv420:
         out = out.view(B, n_out, H, W)

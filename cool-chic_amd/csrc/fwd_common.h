@@ -111,7 +111,9 @@ struct UpsTile {
 
 // Validates the ups arguments and (launch = true) runs pyramid steps 0 .. L-3 (every step
 // but the last, which produces the full-resolution stack); fills *last with the arguments
-// of the final step (source level 1 -> level 0).  Returns CCMI_OK or an error code.
-int ups_pyramid(const ccmi_ups_args *a, hipStream_t s, LevelArgs *last, bool launch = true);
+// of the final step (source level 1 -> level 0).  prev (fold): step L-3 (level 2 -> 1) is not
+// launched either, its arguments go to *prev for a kernel that evaluates it in place.
+// Returns CCMI_OK or an error code.
+int ups_pyramid(const ccmi_ups_args *a, hipStream_t s, LevelArgs *last, bool launch = true, LevelArgs *prev = nullptr);
 
 } // namespace ccmi_fwd

@@ -170,9 +170,13 @@ constexpr int fused_wpe(int cin, int cmid, bool ups, bool mh = false)
 // i.e. from 4 to 3 waves per SIMD, and decode_fused from 0.97 to 1.40 ms per 32 frames)
 // HID > 0: the 2-layer head's hidden width fixed at compile time (fully unrolled unit loop:
 // weight records at immediate LDS offsets, no loop counter or record rotation)
-template <int CIN, int CMID, bool UPS, bool MH = false, int HID = 0>
-__global__ __launch_bounds__(kFThreads) __attribute__((amdgpu_waves_per_eu(fused_wpe(CIN, CMID, UPS, MH)))) void syn_fused_kernel(FusedArgs A, LevelArgs U)
+// FOLD (UPS only): the pyramid's level-2 -> 1 step is evaluated in the kernel too (U2 holds its
+// arguments): the level-1 values phase A needs are computed from the level-2 stack and the
+// level-1 latent instead of read from a level-1 stack in HBM (see "fold" below)
+template <int CIN, int CMID, bool UPS, bool MH = false, int HID = 0, bool FOLD = false>
+__global__ __launch_bounds__(kFThreads) __attribute__((amdgpu_waves_per_eu(fused_wpe(CIN, CMID, UPS, MH)))) void syn_fused_kernel(FusedArgs A, LevelArgs U, LevelArgs U2)
 {
+    static_assert(!FOLD || (UPS && CIN >= 3), "the fold needs the fused level-1 -> 0 step and a level-2 stack");
     constexpr int NR = kRowsPerThread;
     constexpr int C = UPS ? CIN - 1 : 0, NG = fused_groups(CIN, UPS), GC = (C + NG - 1) / NG;
     // region 0: raw input tiles of a channel group (UPS, phases A-B), then the 3x3 layers'
@@ -326,6 +330,7 @@ __global__ __launch_bounds__(kFThreads) __attribute__((amdgpu_waves_per_eu(fused
             for (int G = 0; G < NG; ++G)
 #pragma unroll
                 for (int u = 0; u < kSU; ++u) {
+                    if constexpr (FOLD) break; // computed below from the level-2 stack
                     const int r = wv + kNW * u;
                     // ch = r / kHsRows without a division: wv < kNW moves r past at most one boundary
                     const int c0 = (kNW * u) / kHsRows, tb = kHsRows * (c0 + 1) - kNW * u; // folded (u unrolled)
@@ -362,6 +367,147 @@ __global__ __launch_bounds__(kFThreads) __attribute__((amdgpu_waves_per_eu(fused
 #endif
                 }
             }
+        }
+        if constexpr (FOLD) {
+            // ---- fold: the level-1 stack values of this window's phase A, computed here from
+            // the level-2 stack (C2 channels) and the level-1 latent with ups_level_fixed<8, 7>'s
+            // operation order (bitwise the values the pyramid's level-2 -> 1 launch writes):
+            // F1 the raw tiles into LDS, F2 the horizontal passes, F3 each wave's rows of the
+            // [channel][kHsRows] tile (lane = column) by the vertical passes, into sv.  The
+            // window reads level-1 rows clamp(jbase + jj) and columns clamp(ibase + lane): the
+            // rectangle [R0, R1] x [C0, C1] (<= 21 x 37) of the level-1 image.
+            constexpr int C2 = CIN - 2;
+            constexpr int kFLR = kHsRows + 6, kFLW = kSW + 6, kFLP = kFLW + 1; // latent-1 tile (refine halo 3)
+            constexpr int kFP = 40;                                          // pitch of the horizontal passes
+            constexpr int kF2R = (kHsRows - 1) / 2 + 1 + FT::NS - 1;         // level-2 rows under <= 21 level-1 rows
+            constexpr int kF2W = (kSW - 1) / 2 + 1 + FT::NS - 1, kF2P = kF2W + 1;
+            static_assert(kFP >= kSW, "pass pitch");
+            float *f_lat = s_pool;                       // [kFLR][kFLP]
+            float *f_ref = f_lat + kFLR * kFLP;          // [kFLR][kFP]   refine, horizontal
+            float *f_src = f_ref + kFLR * kFP;           // [C2][kF2R][kF2P]
+            float *f_h2 = f_src + C2 * kF2R * kF2P;      // [C2][kF2R][kFP] transposed conv, horizontal
+            static_assert(kFLR * kFLP + kFLR * kFP + C2 * kF2R * (kF2P + kFP) <= kTot - 256, "fold tiles fit before the LUT");
+            const int hs1 = U.hs, ws1 = U.ws, hs2 = U2.hs, ws2 = U2.ws;
+            const int R0 = clampi(jbase, hs1 - 1), R1 = clampi(jbase + kHsRows - 1, hs1 - 1);
+            const int C0 = clampi(ibase, ws1 - 1);
+            const int r2 = (R0 >> 1) + FT::D0, c2 = (C0 >> 1) + FT::D0; // level-2 origin of the tile
+            const float *uprm2 = U2.params + (int64_t)b * U2.pstride;
+            float wu2[8], wr2[7];
+#pragma unroll
+            for (int k = 0; k < 8; ++k) wu2[k] = uprm2[U2.up_off + k];
+#pragma unroll
+            for (int k = 0; k < 7; ++k) wr2[k] = uprm2[U2.pre_off + k];
+            const int tid = threadIdx.x;
+            // F1: every load in flight before the first LDS store
+            {
+                const float *l1 = U2.ref_src + (int64_t)b * U2.ref_stride;
+                const float *s2 = U2.src + (int64_t)b * U2.src_stride;
+                constexpr int NL = (kFLR * kFLW + kFThreads - 1) / kFThreads;
+                constexpr int NS2 = (C2 * kF2R * kF2W + kFThreads - 1) / kFThreads;
+                float lv[NL], sv2[NS2];
+#pragma unroll
+                for (int u = 0; u < NL; ++u) {
+                    const int i = tid + u * kFThreads, r = i / kFLW, c = i - r * kFLW;
+                    const int Y = R0 - 3 + r, X = C0 - 3 + c;
+                    lv[u] = (i < kFLR * kFLW && Y >= 0 && Y < hs1 && X >= 0 && X < ws1) ? l1[Y * ws1 + X] : 0.f;
+                }
+#pragma unroll
+                for (int u = 0; u < NS2; ++u) {
+                    const int i = tid + u * kFThreads, ch = i / (kF2R * kF2W), rem = i - ch * (kF2R * kF2W);
+                    const int r = rem / kF2W, c = rem - r * kF2W;
+                    sv2[u] = i < C2 * kF2R * kF2W
+                                 ? s2[(ch * hs2 + clampi(r2 + r, hs2 - 1)) * ws2 + clampi(c2 + c, ws2 - 1)]
+                                 : 0.f;
+                }
+#pragma unroll
+                for (int u = 0; u < NL; ++u) {
+                    const int i = tid + u * kFThreads, r = i / kFLW, c = i - r * kFLW;
+                    if (i < kFLR * kFLW) f_lat[r * kFLP + c] = U2.ref_quant ? rintf(U2.gain * lv[u]) : lv[u];
+                }
+#pragma unroll
+                for (int u = 0; u < NS2; ++u) {
+                    const int i = tid + u * kFThreads, ch = i / (kF2R * kF2W), rem = i - ch * (kF2R * kF2W);
+                    const int r = rem / kF2W, c = rem - r * kF2W;
+                    if (i < C2 * kF2R * kF2W) f_src[(ch * kF2R + r) * kF2P + c] = U2.src_quant ? rintf(U2.gain * sv2[u]) : sv2[u];
+                }
+            }
+            __syncthreads();
+            // F2: horizontal passes.  Refine: 7 taps over the zero-padded latent row.  Transposed
+            // conv: level-1 columns (2 q, 2 q + 1) from level-2 columns q + D0 .. q + D0 + NS - 1,
+            // for the pairs q covering columns C0 .. C0 + kSW - 1.
+            for (int i = tid; i < kFLR * kSW; i += kFThreads) {
+                const int r = i / kSW, c = i - r * kSW;
+                const float *p = f_lat + r * kFLP + c;
+                float acc = 0.f;
+#pragma unroll
+                for (int k = 0; k < 7; ++k) acc = fmaf(wr2[k], p[k], acc);
+                f_ref[r * kFP + c] = acc;
+            }
+            {
+                constexpr int NQ = kSW / 2 + 1; // pairs touching C0 .. C0 + kSW - 1
+                const int q0 = C0 >> 1;
+                for (int i = tid; i < C2 * kF2R * NQ; i += kFThreads) {
+                    const int ch = i / (kF2R * NQ), rem = i - ch * (kF2R * NQ), r = rem / NQ, q = rem - r * NQ;
+                    const float *p = f_src + (ch * kF2R + r) * kF2P + q; // level-2 column q0 + q + D0
+                    float e = 0.f, o = 0.f;
+#pragma unroll
+                    for (int m = 0; m < FT::NS; ++m) {
+                        const float v = p[m];
+                        const int te = FT::tap(0, FT::D0 + m), to = FT::tap(1, FT::D0 + m);
+                        if (te >= 0) e = fmaf(wu2[te], v, e);
+                        if (to >= 0) o = fmaf(wu2[to], v, o);
+                    }
+                    const int ce = 2 * (q0 + q) - C0; // tile column of the even output
+                    float *h = f_h2 + (ch * kF2R + r) * kFP;
+                    if (ce >= 0 && ce < kSW) h[ce] = e;
+                    if (ce + 1 < kSW) h[ce + 1] = o;
+                }
+            }
+            __syncthreads();
+            // F3: this wave's rows r = wv + kNW u of each group's [GC][kHsRows] tile, lane = column
+            {
+                const int cx = clampi(ibase + (lane < kSW ? lane : kSW - 1), ws1 - 1) - C0;
+#pragma unroll
+                for (int G = 0; G < NG; ++G)
+#pragma unroll
+                    for (int u = 0; u < kSU; ++u) {
+                        const int r = wv + kNW * u;
+                        const int c0 = (kNW * u) / kHsRows, tb = kHsRows * (c0 + 1) - kNW * u;
+                        const int lc = c0 + (wv >= tb ? 1 : 0), jj = r - lc * kHsRows;
+                        const int ch = G * GC + lc; // level-1 channel: 0 the refined latent, 1.. upsampled
+                        float v = 0.f;
+                        if ((u < kSU - 1 || r < kSR) && ch < C) {
+                            const int Y1 = clampi(jbase + jj, hs1 - 1), ry = Y1 - R0; // wave-uniform
+                            if (ch == 0) {
+                                const float *p = f_ref + ry * kFP + cx;
+                                float acc = 0.f;
+#pragma unroll
+                                for (int k = 0; k < 7; ++k) acc = fmaf(wr2[k], p[k * kFP], acc);
+                                v = acc + f_lat[(ry + 3) * kFLP + cx + 3];
+                            } else {
+                                const float *p = f_h2 + ((ch - 1) * kF2R + (Y1 >> 1) - (R0 >> 1)) * kFP + cx;
+                                float acc = 0.f;
+                                if (Y1 & 1) {
+#pragma unroll
+                                    for (int m = 0; m < FT::NS; ++m) {
+                                        const int t = FT::tap(1, FT::D0 + m);
+                                        if (t >= 0) acc = fmaf(wu2[t], p[m * kFP], acc);
+                                    }
+                                } else {
+#pragma unroll
+                                    for (int m = 0; m < FT::NS; ++m) {
+                                        const int t = FT::tap(0, FT::D0 + m);
+                                        if (t >= 0) acc = fmaf(wu2[t], p[m * kFP], acc);
+                                    }
+                                }
+                                v = acc;
+                            }
+                        }
+                        sv[G][u] = v;
+                    }
+            }
+            (void)R1;
+            __syncthreads(); // the fold's tiles are overwritten by phase A's stores below
         }
         f2 wp[FT::NS];
 #pragma unroll
@@ -988,18 +1134,21 @@ __global__ __launch_bounds__(kThreads) void post_kernel(const float *__restrict_
     }
 }
 
+// the presets' 7-grid decoders with a 48-wide head (hop and its relatives): unrolled head
+bool unrolled_head(const FusedArgs &fa) { return fa.cin == 7 && fa.n_head == 2 && fa.hid == 48 && fa.relu0 && !fa.head_generic; }
+
 template <int CMID, bool UPS>
 void launch_fused(dim3 grid, hipStream_t s, const FusedArgs &fa, const LevelArgs &u)
 {
-    // the presets' 7-grid decoders with a 48-wide head (hop and its relatives): unrolled head
-    if (fa.cin == 7 && fa.n_head == 2 && fa.hid == 48 && fa.relu0 && !fa.head_generic) { // (its scaled ReLU assumes one)
-        hipLaunchKernelGGL((syn_fused_kernel<7, CMID, UPS, false, 48>), grid, dim3(kFThreads), 0, s, fa, u);
+    const LevelArgs none{};
+    if (unrolled_head(fa)) { // (its scaled ReLU assumes a first-layer ReLU)
+        hipLaunchKernelGGL((syn_fused_kernel<7, CMID, UPS, false, 48>), grid, dim3(kFThreads), 0, s, fa, u, none);
         return;
     }
     switch (fa.cin) {
-    case 1: hipLaunchKernelGGL((syn_fused_kernel<1, CMID, false>), grid, dim3(kFThreads), 0, s, fa, u); break;
+    case 1: hipLaunchKernelGGL((syn_fused_kernel<1, CMID, false>), grid, dim3(kFThreads), 0, s, fa, u, none); break;
 #define CCMI_FUSED_CASE(N) \
-    case N: hipLaunchKernelGGL((syn_fused_kernel<N, CMID, UPS>), grid, dim3(kFThreads), 0, s, fa, u); break;
+    case N: hipLaunchKernelGGL((syn_fused_kernel<N, CMID, UPS>), grid, dim3(kFThreads), 0, s, fa, u, none); break;
     CCMI_FUSED_CASE(2) CCMI_FUSED_CASE(3) CCMI_FUSED_CASE(4) CCMI_FUSED_CASE(5) CCMI_FUSED_CASE(6)
     CCMI_FUSED_CASE(7) CCMI_FUSED_CASE(8)
 #undef CCMI_FUSED_CASE
@@ -1012,9 +1161,13 @@ template <int CMID>
 bool launch_fused_mfma_head(dim3 grid, hipStream_t s, const FusedArgs &fa, const LevelArgs &u)
 {
     if (!fa.head_mfma || fa.cin != 7 || fa.n_head != 2 || fa.hid != 48 || fa.n_sp < 1) return false;
-    hipLaunchKernelGGL((syn_fused_kernel<7, CMID, true, true, 48>), grid, dim3(kFThreads), 0, s, fa, u);
+    hipLaunchKernelGGL((syn_fused_kernel<7, CMID, true, true, 48>), grid, dim3(kFThreads), 0, s, fa, u, LevelArgs{});
     return true;
 }
+
+// the folded form (level 2 -> 1 in the kernel): the headline decoder only (7 grids, 48-wide
+// VALU head, 3-channel tail)
+bool fold_eligible(const FusedArgs &fa, int cmid) { return cmid == 3 && unrolled_head(fa) && !fa.head_mfma; }
 
 } // namespace
 
@@ -1184,10 +1337,17 @@ extern "C" int ccmi_decode_forward_f32(const ccmi_decode_args *a, void *stream)
     if (u.ups_k != 8 || u.pre_k != 7 || !make_plan(&y, &P))
         return ccmi_set_error(CCMI_ERR_UNSUPPORTED, "decode: no fused kernel for this architecture");
     if (a->bitdepth > 0 && P.cmid != 3) return ccmi_set_error(CCMI_ERR_ARG, "decode: post-processing needs 3 output planes");
+    if (a->head < CCMI_HEAD_DEFAULT || a->head > CCMI_HEAD_GENERIC) return ccmi_set_error(CCMI_ERR_ARG, "decode: head %d", a->head);
     hipStream_t s = static_cast<hipStream_t>(stream);
-    const int stages = a->stages ? a->stages : 3;
-    LevelArgs last{};
-    if (int rc = ups_pyramid(&u, s, &last, (stages & 1) != 0)) return rc;
+    const int stages = (a->stages & 3) ? a->stages : a->stages | 3;
+    // opt-in (stages bit 3): the pyramid's level-2 -> 1 step folded into the fused kernel.  Same
+    // values bit for bit, but slower: the folded step's halo and passes cost the VALU-bound kernel
+    // more than the HBM-bound pyramid launch it removes (profiles/r6e_*)
+    P.fa.head_mfma = a->head == CCMI_HEAD_MFMA;
+    P.fa.head_generic = a->head == CCMI_HEAD_GENERIC;
+    const bool fold = (stages & 8) && u.n_grids >= 3 && fold_eligible(P.fa, P.cmid);
+    LevelArgs last{}, prev{};
+    if (int rc = ups_pyramid(&u, s, &last, (stages & 1) != 0, fold ? &prev : nullptr)) return rc;
     if (!(stages & 2)) return CCMI_OK;
     if ((int64_t)4 * last.C * last.hs * last.ws >= ((int64_t)1 << 31) || (int64_t)4 * last.hd * last.wd >= ((int64_t)1 << 31))
         return ccmi_set_error(CCMI_ERR_UNSUPPORTED, "decode: level-1 stack of %d x %d x %d exceeds 2 GB buffer addressing", last.C,
@@ -1199,14 +1359,13 @@ extern "C" int ccmi_decode_forward_f32(const ccmi_decode_args *a, void *stream)
     P.fa.out_stride = a->out_stride;
     P.fa.qmax = a->bitdepth > 0 ? (float)((1 << a->bitdepth) - 1) : 0.f;
     P.fa.yuv420 = a->yuv420;
-    if (a->head < CCMI_HEAD_DEFAULT || a->head > CCMI_HEAD_GENERIC) return ccmi_set_error(CCMI_ERR_ARG, "decode: head %d", a->head);
-    P.fa.head_mfma = a->head == CCMI_HEAD_MFMA;
-    P.fa.head_generic = a->head == CCMI_HEAD_GENERIC;
     const int halo = P.fa.n_sp;
     P.fa.tiles_x = ccmi_div_up(y.w, kRW - 2 * halo);
     P.fa.ntiles = P.fa.tiles_x * ccmi_div_up(y.h, kRH - 2 * halo);
     dim3 grid((unsigned)(P.fa.ntiles * y.batch));
-    if (P.cmid == 3) {
+    if (fold) {
+        hipLaunchKernelGGL((syn_fused_kernel<7, 3, true, false, 48, true>), grid, dim3(kFThreads), 0, s, P.fa, last, prev);
+    } else if (P.cmid == 3) {
         if (!launch_fused_mfma_head<3>(grid, s, P.fa, last)) launch_fused<3, true>(grid, s, P.fa, last);
     } else if (!launch_fused_mfma_head<4>(grid, s, P.fa, last)) {
         launch_fused<4, true>(grid, s, P.fa, last);

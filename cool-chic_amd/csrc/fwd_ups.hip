@@ -293,7 +293,7 @@ int launch_level(const LevelArgs &A, int batch, hipStream_t s)
 }
 } // namespace
 
-int ccmi_fwd::ups_pyramid(const ccmi_ups_args *a, hipStream_t s, LevelArgs *last, bool launch)
+int ccmi_fwd::ups_pyramid(const ccmi_ups_args *a, hipStream_t s, LevelArgs *last, bool launch, LevelArgs *prev)
 {
     const int L = a->n_grids;
     if (L < 2) return ccmi_set_error(CCMI_ERR_UNSUPPORTED, "ups: needs at least 2 latent grids (got %d)", L);
@@ -362,6 +362,10 @@ int ccmi_fwd::ups_pyramid(const ccmi_ups_args *a, hipStream_t s, LevelArgs *last
         if (step == L - 2) {
             *last = A;
             break;
+        }
+        if (prev && step == L - 3) { // folded into the caller's fused kernel: not launched
+            *prev = A;
+            continue;
         }
         if (launch)
             if (int rc = launch_level(A, a->batch, s)) return rc;

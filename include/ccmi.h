@@ -175,7 +175,10 @@ typedef struct ccmi_decode_args {
     int64_t out_stride;
     int stages;             /* 0 = all; bit 0: upsampling pyramid down to level 1 (into
                                ups.workspace), bit 1: the fused full-resolution kernel --
-                               lets a caller time the two apart */
+                               lets a caller time the two apart.  bit 3 (opt-in, the 7-grid
+                               48-wide-head decoders): the fused kernel also evaluates the
+                               level-2 -> 1 step and the pyramid stops at level 2 (same values
+                               bit for bit; measured slower) */
     int head;               /* synthesis 1x1 head arithmetic, CCMI_HEAD_*: both are fp32 (the
                                MFMA form's products are exact f32 fmas, summed in another
                                order); MFMA needs 7 inputs, 48 hidden units and >= 1 3x3 layer

@@ -244,14 +244,14 @@ def test_hip_rejects_cpu_tensors(ccmi_lib):
 HEADS = (1, 2)  # ccmi.HEAD_VALU, ccmi.HEAD_MFMA: the fused kernel's two 1x1-head forms
 
 
-def _fused(mps, lats, dev, bitdepth, yuv420, head=0):
+def _fused(mps, lats, dev, bitdepth, yuv420, head=0, fold=False):
     from ccmi import forward as F
     mp0 = mps[0]
     lat = torch.stack([torch.cat([x.reshape(-1) for x in l]) for l in lats]).to(dev)
     ups_p = torch.stack([F.pack_ups(mp.ups_full(), mp.pre_full()) for mp in mps]).to(dev)
     syn_p = torch.stack([F.pack_syn(mp.syn) for mp in mps]).to(dev)
     return F.decode_forward(lat, mp0.sizes, ups_p, mp0.ups_k, len(mp0.ups_half), mp0.pre_k, len(mp0.pre_half),
-                            mp0.layers, syn_p, mp0.gain, True, bitdepth, yuv420, head)
+                            mp0.layers, syn_p, mp0.gain, True, bitdepth, yuv420, head, fold)
 
 
 @pytest.mark.gpu
@@ -294,6 +294,39 @@ def test_unrolled_head_bitwise_generic(path, gpu, ccmi_lib):
     lat = [0.5 * torch.randn(h, w, generator=g) for h, w in mp.sizes]
     assert torch.equal(_fused([mp], [lat], gpu, 0, False, ccmi.HEAD_DEFAULT),
                        _fused([mp], [lat], gpu, 0, False, ccmi.HEAD_GENERIC))
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("H,W,seed", [(720, 1280, 1), (1080, 1920, 11), (37, 53, 2), (1, 1, 3), (2, 130, 4),
+                                      (129, 3, 5), (45, 70, 6), (1365, 2048, 12), (1725, 1145, 13)])
+def test_fused_level2_fold_bitwise_unfolded(H, W, seed, gpu, ccmi_lib):
+    """The level-2 -> 1 upsampling step evaluated inside the fused kernel (opt-in, stages bit 3,
+    for the 7-grid 48-wide-head decoders) against the same kernel reading that level from the
+    pyramid's HBM stack: the fold repeats ups_level_fixed's operation
+    order, so raw synthesis and post-processed 420 output are identical bit for bit, at sizes
+    whose windows clamp at every border (upsampling.py:476-506)."""
+    mp = fo.ModelParams.random(H, W, seed=seed)
+    assert mp.n_grids == 7 and mp.layers[0][0] == 48
+    g = torch.Generator().manual_seed(seed)
+    lat = [0.5 * torch.randn(h, w, generator=g) for h, w in mp.sizes]
+    for bd, yuv in ((0, False), (8, True)):
+        a = _fused([mp], [lat], gpu, bd, yuv, 1, True)
+        b = _fused([mp], [lat], gpu, bd, yuv, 1, False)
+        assert torch.equal(a, b), (H, W, bd)
+
+
+@pytest.mark.gpu
+def test_fused_level2_fold_batch_own_weights(gpu, ccmi_lib):
+    """Per-frame parameter blocks and latents in one folded launch: frame b's output equals a
+    batch-of-1 unfolded run of frame b."""
+    mps = [fo.ModelParams.random(96, 160, seed=40 + i) for i in range(3)]
+    lats = []
+    for i, mp in enumerate(mps):
+        g = torch.Generator().manual_seed(400 + i)
+        lats.append([0.5 * torch.randn(h, w, generator=g) for h, w in mp.sizes])
+    both = _fused(mps, lats, gpu, 8, True, 1, True)
+    for i in range(3):
+        assert torch.equal(both[i], _fused([mps[i]], [lats[i]], gpu, 8, True, 1, False)[0]), i
 
 
 @pytest.mark.gpu
