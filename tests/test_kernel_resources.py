@@ -22,9 +22,10 @@ BUDGET = {
     # tools/occ_probe.sh); no spills since the lane indices are re-derived after the head and
     # per 3x3 layer (round 2 held them across: 5 spilled VGPRs, ~190 MB of scratch writes
     # per 32-frame launch)
-    "syn_fused_kernel<7, 3, true, false, 0>": (80, 0, 0),   # any head width
-    "syn_fused_kernel<7, 3, true, false, 48>": (80, 0, 0),  # headline (hop): unrolled head
-    "syn_fused_kernel<7, 4, true, false, 0>": (128, 0, 0),   # 4-channel tail: 2 workgroups
+    "syn_fused_kernel<7, 3, true, false, 0, false>": (80, 0, 0),   # any head width
+    "syn_fused_kernel<7, 3, true, false, 48, false>": (80, 0, 0),  # headline (hop): unrolled head
+    "syn_fused_kernel<7, 3, true, false, 48, true>": (80, 0, 0),   # the same + the level-2 -> 1 fold (opt-in)
+    "syn_fused_kernel<7, 4, true, false, 0, false>": (128, 0, 0),   # 4-channel tail: 2 workgroups
     "arm_fwd_kernel<16, 2>": (128, 0, 0),                   # path A ARM + rate (hop: 2 hidden layers)
     "arm_fwd_kernel<16, -1>": (128, 0, 0),                  # any hidden-layer count
     "ups_level_fixed<8, 7>": (64, 0, 0),                    # upsampling pyramid
