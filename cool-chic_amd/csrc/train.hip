@@ -1284,14 +1284,17 @@ __global__ void t_sp_gpre(float *__restrict__ gout, const float *__restrict__ ou
 // registers of v_mfma_f32_4x4x1_16b_f32 (+ 3 bias sums), so one launch reads every tile once.
 // (Measured and dropped: the input gradient one channel per iteration with 27 scalar weights
 // each instead of all 81 at once -- 74 vs 40 us, the scalar-load waits per channel.)
+// MODE 7 = MODE 3 over a persistent grid (one resident round of workgroups per frame): the next
+// tile's ring (X, and G with the ReLU mask already applied) is loaded into registers while the
+// current tile computes, and a workgroup flushes its weight gradients once for all its tiles.
 constexpr int kSY = 16, kSX = 64;
 template <int MODE>
-__global__ __launch_bounds__(kT) __attribute__((amdgpu_waves_per_eu(MODE == 2 ? 4 : MODE == 3 ? 5 : 1))) void t_sp_bwd(const float *__restrict__ gout, const float *__restrict__ outp,
+__global__ __launch_bounds__(kT) __attribute__((amdgpu_waves_per_eu(MODE == 2 || MODE == 7 ? 4 : MODE == 3 ? 5 : 1))) void t_sp_bwd(const float *__restrict__ gout, const float *__restrict__ outp,
                                                const float *__restrict__ in, Geo g, const float *__restrict__ th,
                                                int64_t ps, int wo, int bo, int res, float *__restrict__ gin,
                                                float *__restrict__ gth, int64_t gstride)
 {
-    constexpr bool DX = (MODE & 1) != 0, DW = (MODE & 2) != 0;
+    constexpr bool DX = (MODE & 1) != 0, DW = (MODE & 2) != 0, PF = (MODE & 4) != 0;
     constexpr int RH = kSY + 2, RW = kSX + 2;
     // ring images at row pitch kRP = 67 and plane pitch kPP = 1225 (== 3 and 9 mod 32 banks): the 27
     // taps (i, ky, kx) of one pixel sit on 27 distinct banks (9 i + 3 ky + kx), so the weight-
@@ -1322,12 +1325,49 @@ __global__ __launch_bounds__(kT) __attribute__((amdgpu_waves_per_eu(MODE == 2 ? 
     for (int e = 0; e < (VW ? 84 : 1); ++e) acc[e] = 0.f;
     v4f dacc = {0.f, 0.f, 0.f, 0.f}; // MODE 3: the MFMA blocks
     float bacc[3] = {0.f, 0.f, 0.f};  // MODE 3: bias sums
+    // PF: the ring of tile tt in registers: X and the masked G of NU elements per thread
+    constexpr int kPU = (RH * RW + kT - 1) / kT;
+    float px_[PF ? kPU : 1][3], pg_[PF ? kPU : 1][3], po_[PF ? kPU : 1][3]; // raw: the mask is applied at the LDS store (a select here would wait for the loads)
+    auto prefetch = [&](int tt) __attribute__((always_inline)) {
+        const int py0 = (tt / tx) * kSY, px0 = (tt % tx) * kSX;
+#pragma unroll
+        for (int u = 0; u < kPU; ++u) {
+            const int i = threadIdx.x + u * kT;
+            const int r = i / RW, q = i - r * RW;
+            const int y = py0 - 1 + r, x = px0 - 1 + q;
+            const int64_t cl = (int64_t)clampi(y, H - 1) * W + clampi(x, W - 1);
+            const bool inb = y >= 0 && y < H && x >= 0 && x < W, live = i < RH * RW;
+#pragma unroll
+            for (int ch = 0; ch < 3; ++ch) {
+                px_[u][ch] = live ? Xb[ch * npx + cl] : 0.f;
+                pg_[u][ch] = (live && inb) ? Gb[ch * npx + cl] : 0.f;
+                po_[u][ch] = (Ob && live && inb) ? Ob[ch * npx + cl] : 1.f;
+            }
+        }
+    };
+    if constexpr (PF)
+        if ((int)blockIdx.x < ntile) prefetch(blockIdx.x);
     for (int t = blockIdx.x; t < ntile; t += gridDim.x) {
         const int y0 = (t / tx) * kSY, x0 = (t % tx) * kSX;
         __syncthreads();
+        if constexpr (PF) {
+#pragma unroll
+            for (int u = 0; u < kPU; ++u) {
+                const int i = threadIdx.x + u * kT;
+                if (i >= RH * RW) continue;
+                const int r = i / RW, q = i - r * RW;
+#pragma unroll
+                for (int ch = 0; ch < 3; ++ch) {
+                    SX(ch, r, q) = px_[u][ch];
+                    SG(ch, r, q) = po_[u][ch] <= 0.f ? 0.f : pg_[u][ch];
+                }
+            }
+            if (t + (int)gridDim.x < ntile) prefetch(t + gridDim.x); // in flight behind this tile's work
+        } else
         // the ring in batches of UN elements per thread: a batch's loads are all in flight
         // before its LDS stores (the input-gradient kernel, with few registers, takes the
         // whole ring in one batch; the weight-gradient kernel two per batch)
+        {
         constexpr int NU = (RH * RW + kT - 1) / kT, UN = VW ? 2 : NU;
 #pragma unroll
         for (int u0 = 0; u0 < NU; u0 += UN) {
@@ -1366,9 +1406,10 @@ __global__ __launch_bounds__(kT) __attribute__((amdgpu_waves_per_eu(MODE == 2 ? 
                 }
             }
         }
+        }
         __syncthreads();
 #if !defined(CCMI_DIAG_SPB_NODW)
-        if constexpr (MODE == 3) {
+        if constexpr ((MODE & 3) == 3) {
             // dW[oc][n = (i, ky, kx)] += sum_q G[oc][q] X[i][q + (ky - 1, kx - 1)] over the wave's 4 x 64
             // pixels: block bk = lane >> 2 < 14 is (column quad nq = bk % 7, pixel stream bk / 7;
             // stream s takes rows rb + 2 s, rb + 2 s + 1), A = G[oc = lane & 3], B = X at tap column
@@ -1397,7 +1438,7 @@ __global__ __launch_bounds__(kT) __attribute__((amdgpu_waves_per_eu(MODE == 2 ? 
             float gp[3];
 #pragma unroll
             for (int ch = 0; ch < 3; ++ch) gp[ch] = SG(ch, ry + 1, c + 1);
-            if constexpr (MODE == 3) {
+            if constexpr ((MODE & 3) == 3) {
 #pragma unroll
                 for (int oc = 0; oc < 3; ++oc) bacc[oc] += gp[oc];
             }
@@ -2848,6 +2889,17 @@ static int resident_wgs(const void *fn, int threads, size_t lds, int max_per_cu)
     return cache[key] = std::min(per, max_per_cu) * cus;
 }
 // grid of a persistent kernel over `units` work units per frame, B frames
+// the 3x3 backward as a persistent prefetching grid (t_sp_bwd<7>) or one tile per workgroup
+// (t_sp_bwd<3>); CCMI_SP_BWD_PF=0 selects the latter (A/B)
+static bool sp_bwd_persistent()
+{
+    static const bool on = [] {
+        const char *e = getenv("CCMI_SP_BWD_PF");
+        return !(e && *e == '0');
+    }();
+    return on;
+}
+
 static dim3 resident_grid(const void *fn, int threads, size_t lds, int64_t units, int B, int max_per_cu = 1 << 20)
 {
     const int64_t per_frame = std::max<int64_t>(1, resident_wgs(fn, threads, lds, max_per_cu) / B);
@@ -3186,8 +3238,12 @@ extern "C" int ccmi_train_step(const ccmi_train_args *a, void *stream)
 #else
         (void)nb;
         // both halves, one tile per workgroup: each tile's X / G / out read once
-        hipLaunchKernelGGL(t_sp_bwd<3>, dim3((unsigned)ntile, B), dim3(kT), 0, s, gcur, outp, F(pl.z[i]), g, a->params,
-                           a->param_stride, g.sp_w[i], g.sp_b[i], g.sp_res[i], gin, slots, g.P);
+        if (sp_bwd_persistent())
+            hipLaunchKernelGGL(t_sp_bwd<7>, resident_grid((const void *)t_sp_bwd<7>, kT, 0, ntile, B), dim3(kT), 0, s, gcur,
+                               outp, F(pl.z[i]), g, a->params, a->param_stride, g.sp_w[i], g.sp_b[i], g.sp_res[i], gin, slots, g.P);
+        else
+            hipLaunchKernelGGL(t_sp_bwd<3>, dim3((unsigned)ntile, B), dim3(kT), 0, s, gcur, outp, F(pl.z[i]), g, a->params,
+                               a->param_stride, g.sp_w[i], g.sp_b[i], g.sp_res[i], gin, slots, g.P);
 #endif
         gcur = gin;
     }

@@ -161,14 +161,81 @@ def test_debug_preset_default_arch_matches_reference_rd(image, gpu):
     prev = json.loads(f.read_text()) if f.exists() else {}
     prev[image] = [r.as_dict() for r in recs]
     f.write_text(json.dumps(prev, indent=1))
-    # 120 iterations of a 40-wide head and a dim-24 ARM land far apart from seed to seed: the
-    # reference's own seed 1 is +18 % BD-rate against its seed 0 on kodim01 (hop: -0.45 %), so
-    # the band is that spread + 5 %
-    spread = abs(_ref_seed_bd(ref, image))
-    bd = _check(image, recs, ref, bd_band=(-(spread + BD_KODAK), spread + BD_KODAK) if image == "kodim01_768x512" else False)
+    # 120 iterations of a 40-wide head and a dim-24 ARM land far apart from seed to seed (the
+    # reference's seed 1 against its seed 0: +18 % BD-rate on kodim01), so two reference seeds
+    # could not pin it: since round 6 the fixture holds 6 seeds per lambda and the bands are the
+    # pooled-sigma form of the c3x test (per lambda) plus a BD-rate band from the reference's own
+    # seed-curve scatter (_check_pooled)
+    bd = _check_pooled(image, recs, ref, "debug default")
     for r in recs:
         assert r.cool_bpp == r.cool_bpp and r.cool_bpp > 0
     assert np.isfinite(bd)
+
+
+# pooled-sigma bands of the debug preset (round 6): per lambda the GPU mean within
+# 3 sigma sqrt(1 / n_ref + 1 / n_gpu) + DEBUG_PSNR_MARGIN_DB / + DEBUG_RATE_MARGIN of the reference
+# mean (sigma pooled over the image's four lambdas).  On the Kodak-geometry image also the BD-rate of
+# the GPU's mean curve against the reference's mean curve: within 3 sd_half sqrt((1 / n_ref +
+# 1 / n_gpu) / (2 / h)) + DEBUG_BD_MARGIN %, sd_half the scatter of the BD-rate between the mean
+# curves of complementary halves (h seeds each) of the reference's own seeds.  (The 192 x 128 image's
+# 120-iteration curves are too irregular for a cubic BD fit: its half-split BD-rates reach +1,000 %.)
+DEBUG_PSNR_MARGIN_DB = 0.1
+DEBUG_RATE_MARGIN = 0.03
+DEBUG_BD_MARGIN = 2.0
+
+
+def _half_split_bd_sd(ref):
+    """Standard deviation of the BD-rate between the mean curves of complementary halves of the
+    reference seeds (every split with seed 0 in the first half), and the half size."""
+    import itertools
+    from ccmi import rd
+    seeds = sorted({r["seed"] for r in ref})
+    h = len(seeds) // 2
+    out = []
+    for A in itertools.combinations(seeds, h):
+        if seeds[0] not in A:
+            continue
+        B = [x for x in seeds if x not in A][:h]
+        R1, P1, _ = rd.curve([r for r in ref if r["seed"] in A])
+        R2, P2, _ = rd.curve([r for r in ref if r["seed"] in B])
+        out.append(rd.bd_rate(R1, P1, R2, P2))
+    return float(np.std(out, ddof=1)), h, out
+
+
+def _check_pooled(image, recs, ref, tag):
+    from ccmi import rd
+    by_lm = {lm: [x for x in ref if x["lmbda"] == lm] for lm in LAMBDAS}
+    assert all(len(v) >= 4 for v in by_lm.values()), "pooled bands need >= 4 reference seeds per lambda"
+    sd_p = _pooled_sd([[x["psnr_db"] for x in r] for r in by_lm.values()])
+    sd_r = _pooled_sd([[x["rate_bpp"] for x in r] for r in by_lm.values()], rel=True)
+    lines = []
+    for lm in LAMBDAS:
+        r = by_lm[lm]
+        rp, rr = [x["psnr_db"] for x in r], [x["rate_bpp"] for x in r]
+        o = [x for x in recs if x.lmbda == lm]
+        op, orr = np.mean([x.psnr_db for x in o]), np.mean([x.rate_bpp for x in o])
+        k = 3.0 * np.sqrt(1.0 / len(r) + 1.0 / len(o))
+        tol_p, tol_r = DEBUG_PSNR_MARGIN_DB + k * sd_p, DEBUG_RATE_MARGIN + k * sd_r
+        lines.append(f"{image} {tag} lambda {lm}: PSNR ref {np.mean(rp):.3f} ({len(rp)} seeds, {min(rp):.3f}..{max(rp):.3f}) "
+                     f"gpu {op:.3f} (tol {tol_p:.2f}), rate ref {np.mean(rr):.4f} gpu {orr:.4f} (tol {tol_r:.3f})")
+        assert abs(op - np.mean(rp)) <= tol_p, lines[-1]
+        assert abs(orr / np.mean(rr) - 1) <= tol_r, lines[-1]
+    R1, P1, _ = rd.curve(ref)
+    R2, P2, _ = rd.curve(recs)
+    bd = rd.bd_rate(R1, P1, R2, P2)
+    if image == "kodim01_768x512":
+        sd_h, h, splits = _half_split_bd_sd(ref)
+        n_ref = min(len(v) for v in by_lm.values())
+        n_gpu = len({x.seed for x in recs})
+        band = 3.0 * sd_h * np.sqrt((1.0 / n_ref + 1.0 / n_gpu) / (2.0 / h)) + DEBUG_BD_MARGIN
+        lines.append(f"{image} {tag}: BD-rate GPU vs reference {bd:+.2f} % (band +-{band:.1f}: reference half-split "
+                     f"BD-rates {', '.join(f'{v:+.1f}' for v in splits)} %, sd {sd_h:.1f})")
+        print("\n" + "\n".join(lines))
+        assert abs(bd) <= band, lines[-1]
+    else:
+        lines.append(f"{image} {tag}: BD-rate GPU vs reference {bd:+.2f} % (reported, not banded)")
+        print("\n" + "\n".join(lines))
+    return bd
 
 
 # c3x preset (preset_cfg/c3x.yaml) with every phase / warm-up / patience scaled by 0.1, as
