@@ -166,7 +166,11 @@ def test_debug_preset_default_arch_matches_reference_rd(image, gpu):
     # could not pin it: since round 6 the fixture holds 6 seeds per lambda and the bands are the
     # pooled-sigma form of the c3x test (per lambda) plus a BD-rate band from the reference's own
     # seed-curve scatter (_check_pooled)
-    bd = _check_pooled(image, recs, ref, "debug default")
+    if min(sum(1 for x in ref if x["lmbda"] == lm) for lm in LAMBDAS) >= 4:
+        bd = _check_pooled(image, recs, ref, "debug default")
+    else:  # the round-5 form (2 reference seeds): spread of the reference's two seed curves + 5 %
+        spread = abs(_ref_seed_bd(ref, image))
+        bd = _check(image, recs, ref, bd_band=(-(spread + BD_KODAK), spread + BD_KODAK) if image == "kodim01_768x512" else False)
     for r in recs:
         assert r.cool_bpp == r.cool_bpp and r.cool_bpp > 0
     assert np.isfinite(bd)
