@@ -252,11 +252,22 @@ __device__ __forceinline__ void ctx_off(int i, int &dy, int &dx)
 // reads are in flight together (as `if (inside) v += s_g[..]` they compiled to D + 1
 // exec-mask branches with one LDS round trip each).
 // Summation order as before (own value, then k = 0 .. D - 1).
-template <int D>
+// t_arm16's order of its 16 context inputs (input slot -> context index) and its inverse.  A
+// wave's four 16-lane groups read slots 4 lk + s of the same instruction s: with s_y's pitch
+// kYP16 = 81 (17 mod 32 banks) the contexts paired in a 32-lane half are (dy, dx) and
+// (dy + 1, dx - 1), 16 banks apart -- seven of the eight pairs conflict-free (the natural order
+// at pitch 72 conflicted in all eight: 2.0 M of t_arm16's 16.5 M conflict cycles per dispatch)
+constexpr int kYP16 = 81;
+__device__ constexpr signed char kPi16[16] = {0, 1, 2, 5, 3, 4, 7, 10, 6, 8, 9, 12, 11, 13, 14, 15};
+__device__ constexpr signed char kSlot16[16] = {0, 1, 2, 4, 5, 3, 8, 6, 9, 10, 7, 12, 11, 13, 14, 15};
+
+// RP: the LDS distance of two tile rows of gradient rows (t_arm: kATX rows of pitch D + 1, one
+// block for the tile; t_arm16: one 2048-float block per wave); PERM: columns are t_arm16's slots
+template <int D, int RP = kATX * (D + 1), bool PERM = false>
 __device__ __forceinline__ float gather_ctx(const float *s_g, const float *s_zero, int r, int c)
 {
     const int ly0 = r - kAH, lx0 = c - kAH;
-    const int base = (ly0 * kATX + lx0) * (D + 1);
+    const int base = ly0 * RP + lx0 * (D + 1);
     auto inside = [](int ly, int lx) { return (unsigned)ly < (unsigned)kATY && (unsigned)lx < (unsigned)kATX; };
     float t[D + 1];
     t[D] = *(inside(ly0, lx0) ? s_g + base + D : s_zero);
@@ -264,7 +275,8 @@ __device__ __forceinline__ float gather_ctx(const float *s_g, const float *s_zer
     for (int k = 0; k < D; ++k) {
         int dy, dx;
         ctx_off<D>(k, dy, dx);
-        t[k] = *(inside(ly0 - dy, lx0 - dx) ? s_g + base + (-dy * kATX - dx) * (D + 1) + k : s_zero);
+        const int col = PERM ? kSlot16[k] : k;
+        t[k] = *(inside(ly0 - dy, lx0 - dx) ? s_g + base - dy * RP - dx * (D + 1) + col : s_zero);
     }
     // all reads issued before the first add (the scheduler otherwise sinks each read to its
     // add: one LDS round trip per term again)
@@ -1856,6 +1868,173 @@ __global__ __launch_bounds__(kHeadT) void t_head_bwd(const float *__restrict__ d
 // the dW0 tile 8 of 16 columns, 1,024 MFMA cycles per tile and wave; now 128 + 256.
 // The output layer must be linear (g.r1 == 0, every reference architecture's "X-1-linear-none"):
 // then g_out needs no pass over all units first, and a tile's units are computed just in time.
+// Register form (the one launched for a linear output layer): no LDS round trip between the
+// hidden layer and the matrix cores.  Per 16-pixel block a wave evaluates the hidden layer TWICE
+// on v_mfma_f32_16x16x4_f32 (K = the CIN inputs + the constant 1 of the bias, two K-steps), with
+// the same operand registers in swapped roles:
+//   layout B: Z^T = W0 X, accumulator register r of lane l = unit 16 t + 4 (l >> 4) + r of pixel
+//     l & 15 -- g_h in this layout is exactly the A operand of g_x = g_h W0 with the K order
+//     permuted (K-step r takes units 16 t + 4 g + r from lane group g), so g_x comes out of the
+//     matrix cores with no data movement;
+//   layout A: Z = X^T W0^T, register r of lane l = pixel 4 (l >> 4) + r of unit 16 t + (l & 15) --
+//     g_h here is the A operand of dW0 = g_h^T [x | 1] with K = the pixels (K-step r takes
+//     pixel 4 g + r from lane group g), and dW1 = g_out h^T is 12 VALU FMAs into per-lane
+//     partial sums (3 outputs: a matrix core would be 13/16 padding).
+// Two hidden-layer evaluations cost 4 MFMA per 16-unit tile; what they replace is the LDS staging
+// of every tile (WAIT_INST_LDS 17 % of the tiled form's wave cycles, profiles/r5zk_train_pmc.txt).
+template <int CIN, int NT>
+__global__ __launch_bounds__(256) void t_head_bwd_m(const float *__restrict__ dense, const float *__restrict__ gz0, Geo g,
+                                                    const float *__restrict__ th, int64_t ps, float *__restrict__ gdense,
+                                                    float *__restrict__ gth, int64_t gstride)
+{
+    static_assert(CIN + 1 <= 8, "inputs + bias in two K-steps of 4");
+    constexpr int kU = 16 * NT, kRedN = kU * (CIN + 4) + 3;
+    __shared__ __attribute__((aligned(16))) float s_w1[3][kU];
+    __shared__ float s_red[4][kRedN];
+    const int b = blockIdx.y, t = threadIdx.x, lane = t & 63, w = t >> 6, i = lane & 15, gq = lane >> 4;
+    const int hid = g.hid;
+    const int64_t npx = (int64_t)g.H * g.W;
+    const cfloat_ptr P = (cfloat_ptr)(size_t)(th + (int64_t)b * ps);
+    for (int e = t; e < 3 * kU; e += 256) {
+        const int k = e / kU, u = e - k * kU;
+        s_w1[k][u] = u < hid ? P[g.w1 + k * hid + u] : 0.f;
+    }
+    // per-lane constants: aB[tt][s] = W0|b0 [unit 16 tt + i][input 4 s + gq] (A of layout B, B of
+    // layout A); bG[tt][r] = W0[unit 16 tt + 4 gq + r][input i] (B of g_x); w1A[tt][k] = W1[k][16 tt + i]
+    float aB[NT][2], bG[NT][4], w1A[NT][3];
+#pragma unroll
+    for (int tt = 0; tt < NT; ++tt) {
+        const int u = 16 * tt + i;
+#pragma unroll
+        for (int s = 0; s < 2; ++s) {
+            const int c = 4 * s + gq;
+            aB[tt][s] = u < hid ? (c < CIN ? P[g.w0 + u * CIN + c] : c == CIN ? P[g.b0 + u] : 0.f) : 0.f;
+        }
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            const int ur = 16 * tt + 4 * gq + r;
+            bG[tt][r] = (ur < hid && i < CIN) ? P[g.w0 + ur * CIN + i] : 0.f;
+        }
+#pragma unroll
+        for (int k = 0; k < 3; ++k) w1A[tt][k] = u < hid ? P[g.w1 + k * hid + u] : 0.f;
+    }
+    const bool relu = g.r0 != 0;
+    v4f dw0[NT];
+    float acc1[NT][3], db1[3] = {0.f, 0.f, 0.f};
+#pragma unroll
+    for (int tt = 0; tt < NT; ++tt) {
+        dw0[tt] = v4f{0.f, 0.f, 0.f, 0.f};
+        acc1[tt][0] = acc1[tt][1] = acc1[tt][2] = 0.f;
+    }
+    __syncthreads(); // s_w1 staged
+    const float *xg = dense + (int64_t)b * CIN * npx;
+    const float *gpg = gz0 + (int64_t)b * 3 * npx;
+    float *gdb = gdense + (int64_t)b * CIN * npx;
+    const int64_t nblk = (npx + 15) >> 4, wstride = (int64_t)gridDim.x * 4;
+    for (int64_t blk = (int64_t)blockIdx.x * 4 + w; blk < nblk; blk += wstride) {
+        const int64_t p0 = blk << 4, pi = p0 + i, pa = p0 + 4 * gq;
+        // X[input 4 s + gq][pixel p0 + i] (0 past the frame, bias input included)
+        float xb[2];
+#pragma unroll
+        for (int s = 0; s < 2; ++s) {
+            const int c = 4 * s + gq;
+            xb[s] = pi >= npx ? 0.f : c < CIN ? xg[c * npx + pi] : c == CIN ? 1.f : 0.f;
+        }
+        float gpT[3], gpA[3][4], xA[4];
+#pragma unroll
+        for (int k = 0; k < 3; ++k) gpT[k] = pi < npx ? gpg[k * npx + pi] : 0.f;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            const bool v = pa + r < npx;
+#pragma unroll
+            for (int k = 0; k < 3; ++k) gpA[k][r] = v ? gpg[k * npx + pa + r] : 0.f;
+            xA[r] = !v ? 0.f : i < CIN ? xg[i * npx + pa + r] : i == CIN ? 1.f : 0.f;
+        }
+        if (gq == 0) {
+#pragma unroll
+            for (int k = 0; k < 3; ++k) db1[k] += gpT[k];
+        }
+        v4f gx = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int tt = 0; tt < NT; ++tt) {
+            v4f zT = mfma4(aB[tt][0], xb[0], v4f{0.f, 0.f, 0.f, 0.f});
+            zT = mfma4(aB[tt][1], xb[1], zT);
+            v4f zA = mfma4(xb[0], aB[tt][0], v4f{0.f, 0.f, 0.f, 0.f});
+            zA = mfma4(xb[1], aB[tt][1], zA);
+            // layout B: g_h of units 16 tt + 4 gq + r at pixel i, then g_x += g_h W0
+            const v4f wk0 = *reinterpret_cast<const v4f *>(&s_w1[0][16 * tt + 4 * gq]);
+            const v4f wk1 = *reinterpret_cast<const v4f *>(&s_w1[1][16 * tt + 4 * gq]);
+            const v4f wk2 = *reinterpret_cast<const v4f *>(&s_w1[2][16 * tt + 4 * gq]);
+            float ghT[4];
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                const float sgh = fmaf(wk2[r], gpT[2], fmaf(wk1[r], gpT[1], wk0[r] * gpT[0]));
+                ghT[r] = (!relu || zT[r] > 0.f) ? sgh : 0.f;
+            }
+#pragma unroll
+            for (int r = 0; r < 4; ++r) gx = mfma4(ghT[r], bG[tt][r], gx);
+            // layout A: h and g_h of unit 16 tt + i at pixels 4 gq + r; dW1 partials, dW0 += g_h^T [x | 1]
+            float ghA[4];
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                const float h = relu ? fmaxf(zA[r], 0.f) : zA[r];
+#pragma unroll
+                for (int k = 0; k < 3; ++k) acc1[tt][k] = fmaf(gpA[k][r], h, acc1[tt][k]);
+                const float sgh = fmaf(w1A[tt][2], gpA[2][r], fmaf(w1A[tt][1], gpA[1][r], w1A[tt][0] * gpA[0][r]));
+                ghA[r] = (!relu || zA[r] > 0.f) ? sgh : 0.f;
+            }
+#pragma unroll
+            for (int r = 0; r < 4; ++r) dw0[tt] = mfma4(ghA[r], xA[r], dw0[tt]);
+        }
+        // g_x: register r of lane l = pixel 4 gq + r, input i
+        if (i < CIN) {
+#pragma unroll
+            for (int r = 0; r < 4; ++r)
+                if (pa + r < npx) gdb[i * npx + pa + r] = gx[r];
+        }
+    }
+    // ---- flush: this wave's partial row (w0 [hid][CIN] | b0 [hid] | w1 [3][hid] | b1 [3]), the
+    // four waves summed in LDS, one atomic per value per workgroup into its slot row
+    float *red = s_red[w];
+    const int nred = hid * (CIN + 4) + 3;
+    for (int e = lane; e < nred; e += 64) red[e] = 0.f;
+    __builtin_amdgcn_wave_barrier();
+#pragma unroll
+    for (int tt = 0; tt < NT; ++tt) {
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            const int u = 16 * tt + 4 * gq + r; // dW0[u][c = i]
+            if (u < hid) {
+                if (i < CIN) red[u * CIN + i] = dw0[tt][r];
+                else if (i == CIN) red[hid * CIN + u] = dw0[tt][r];
+            }
+        }
+#pragma unroll
+        for (int k = 0; k < 3; ++k) {
+            float v = acc1[tt][k];
+            v += __shfl_xor(v, 16);
+            v += __shfl_xor(v, 32);
+            const int u = 16 * tt + i;
+            if (gq == 0 && u < hid) red[hid * (CIN + 1) + k * hid + u] = v;
+        }
+    }
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {
+        const float v = wave_sum(db1[k]);
+        if (lane == 0) red[hid * (CIN + 4) + k] = v;
+    }
+    __syncthreads();
+    float *Gp = gth + ((int64_t)b * kDwSlots + blockIdx.x % kDwSlots) * gstride; // this workgroup's slot row
+    for (int e = t; e < nred; e += 256) {
+        const float v = (s_red[0][e] + s_red[1][e]) + (s_red[2][e] + s_red[3][e]);
+        const int dst = e < hid * CIN ? g.w0 + e
+                        : e < hid * (CIN + 1) ? g.b0 + (e - hid * CIN)
+                        : e < hid * (CIN + 4) ? g.w1 + (e - hid * (CIN + 1))
+                                              : g.b1 + (e - hid * (CIN + 4));
+        atomicAdd(&Gp[dst], v);
+    }
+}
+
 constexpr int kHbXP = 68;
 constexpr int head_bwd_t_wave_floats(int cin) { return (16 + 4 + cin + 1) * kHbXP; }
 
@@ -2888,7 +3067,22 @@ static int resident_wgs(const void *fn, int threads, size_t lds, int max_per_cu)
     if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, fn, threads, lds) != hipSuccess || per < 1) per = 1;
     return cache[key] = std::min(per, max_per_cu) * cus;
 }
-// grid of a persistent kernel over `units` work units per frame, B frames
+
+// the 1x1 head backward in the register form (t_head_bwd_m, opt-in: CCMI_HEAD_BWD_REGS=1) or the
+// LDS-tiled form (t_head_bwd_t, the default).  The register form is bit-for-bit a different
+// summation but passes every gradient test; it measured 273 us per launch against the tiled
+// form's 190 us (step 0.842 -> 0.910 ms, profiles/r6h_head_bwd_regs_ab.txt): its 36 16x16x4
+// MFMAs per 16 pixels are half padding (N = 8 of 16 inputs for g_x and dW0), and at 180 VGPRs it
+// runs 2 waves / SIMD with no prefetch of the next block's 25 small loads.
+static bool head_bwd_regs()
+{
+    static const bool on = [] {
+        const char *e = getenv("CCMI_HEAD_BWD_REGS");
+        return e && *e == '1';
+    }();
+    return on;
+}
+
 // the 3x3 backward as a persistent prefetching grid (t_sp_bwd<7>) or one tile per workgroup
 // (t_sp_bwd<3>); CCMI_SP_BWD_PF=0 selects the latter (A/B)
 static bool sp_bwd_persistent()
@@ -2900,6 +3094,7 @@ static bool sp_bwd_persistent()
     return on;
 }
 
+// grid of a persistent kernel over `units` work units per frame, B frames
 static dim3 resident_grid(const void *fn, int threads, size_t lds, int64_t units, int B, int max_per_cu = 1 << 20)
 {
     const int64_t per_frame = std::max<int64_t>(1, resident_wgs(fn, threads, lds, max_per_cu) / B);
@@ -2957,7 +3152,12 @@ void launch_head(bool bwd, dim3 grid, hipStream_t s, const float *dense, const f
         // fit: 399 us against 286 us capped at 4; profiles/r4n_*, r4o_*, r4y_*)
         const int64_t nchunk = ((int64_t)g.H * g.W + kHeadT - 1) / kHeadT;
 #define CCMI_HB(N)                                                                                                     \
-    if (tiled)                                                                                                         \
+    if (tiled && head_bwd_regs() && CIN + 1 <= 8)                                                                      \
+        hipLaunchKernelGGL((t_head_bwd_m<(CIN + 1 <= 8 ? CIN : 7), N>),                                               \
+                           resident_grid((const void *)t_head_bwd_m<(CIN + 1 <= 8 ? CIN : 7), N>, 256, 0,                \
+                                         ((int64_t)g.H * g.W + 63) / 64, (int)grid.y),                                  \
+                           dim3(256), 0, s, dense, gz0, g, th, ps, z0_or_gdense, gth, gstride);                         \
+    else if (tiled)                                                                                                    \
         hipLaunchKernelGGL((t_head_bwd_t<CIN, N>), resident_grid((const void *)t_head_bwd_t<CIN, N>, kHeadT, lds, nchunk, (int)grid.y), \
                            dim3(kHeadT), lds, s, dense, gz0, g, th, ps, z0_or_gdense, gth, gstride);                    \
     else                                                                                                               \
