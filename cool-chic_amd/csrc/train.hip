@@ -252,22 +252,11 @@ __device__ __forceinline__ void ctx_off(int i, int &dy, int &dx)
 // reads are in flight together (as `if (inside) v += s_g[..]` they compiled to D + 1
 // exec-mask branches with one LDS round trip each).
 // Summation order as before (own value, then k = 0 .. D - 1).
-// t_arm16's order of its 16 context inputs (input slot -> context index) and its inverse.  A
-// wave's four 16-lane groups read slots 4 lk + s of the same instruction s: with s_y's pitch
-// kYP16 = 81 (17 mod 32 banks) the contexts paired in a 32-lane half are (dy, dx) and
-// (dy + 1, dx - 1), 16 banks apart -- seven of the eight pairs conflict-free (the natural order
-// at pitch 72 conflicted in all eight: 2.0 M of t_arm16's 16.5 M conflict cycles per dispatch)
-constexpr int kYP16 = 81;
-__device__ constexpr signed char kPi16[16] = {0, 1, 2, 5, 3, 4, 7, 10, 6, 8, 9, 12, 11, 13, 14, 15};
-__device__ constexpr signed char kSlot16[16] = {0, 1, 2, 4, 5, 3, 8, 6, 9, 10, 7, 12, 11, 13, 14, 15};
-
-// RP: the LDS distance of two tile rows of gradient rows (t_arm: kATX rows of pitch D + 1, one
-// block for the tile; t_arm16: one 2048-float block per wave); PERM: columns are t_arm16's slots
-template <int D, int RP = kATX * (D + 1), bool PERM = false>
+template <int D>
 __device__ __forceinline__ float gather_ctx(const float *s_g, const float *s_zero, int r, int c)
 {
     const int ly0 = r - kAH, lx0 = c - kAH;
-    const int base = ly0 * RP + lx0 * (D + 1);
+    const int base = (ly0 * kATX + lx0) * (D + 1);
     auto inside = [](int ly, int lx) { return (unsigned)ly < (unsigned)kATY && (unsigned)lx < (unsigned)kATX; };
     float t[D + 1];
     t[D] = *(inside(ly0, lx0) ? s_g + base + D : s_zero);
@@ -275,8 +264,7 @@ __device__ __forceinline__ float gather_ctx(const float *s_g, const float *s_zer
     for (int k = 0; k < D; ++k) {
         int dy, dx;
         ctx_off<D>(k, dy, dx);
-        const int col = PERM ? kSlot16[k] : k;
-        t[k] = *(inside(ly0 - dy, lx0 - dx) ? s_g + base - dy * RP - dx * (D + 1) + col : s_zero);
+        t[k] = *(inside(ly0 - dy, lx0 - dx) ? s_g + base + (-dy * kATX - dx) * (D + 1) + k : s_zero);
     }
     // all reads issued before the first add (the scheduler otherwise sinks each read to its
     // add: one LDS round trip per term again)
@@ -772,7 +760,11 @@ __global__ __launch_bounds__(kT) __attribute__((amdgpu_waves_per_eu(t_arm16_wpe(
         tile_geo(t, l, y0, x0);
         const int H = g.h[l], W = g.w[l];
         const float *src = yq + (int64_t)b * g.N + g.off[l];
-        const int tid = threadIdx.x;
+        // the staging indices from an opaque thread index, re-derived per tile: hoisted, two
+        // of them were spilled and their reloads' vmcnt(0) inside this prefetch waited for the
+        // previous tile's gather atomics (measured neutral, 232 us either way: r6k)
+        int tid = threadIdx.x;
+        asm volatile("" : "+v"(tid));
 #pragma unroll
         for (int u = 0; u < kSU; ++u) {
             const int i = tid + u * kT;

@@ -40,10 +40,11 @@ BUDGET = {
     # training step (3 waves / SIMD).  t_arm16<2>: round 3 spilled 13 VGPRs across its tile
     # loop (their reloads' vmcnt(0) waited for the previous tile's gradient atomics); since
     # round 4 all weights sit in LDS, the ReLU masks in lane masks and the tile-invariant
-    # indices are re-derived per tile: 4 waves / SIMD (<= 128 VGPRs), with 2 spilled values
-    # that live only in the prologue / epilogue, outside the tile loop (477 -> 448 us per
-    # launch against the 3-wave build, profiles/r4j_train_ab.txt)
-    "t_arm16<2>": (128, 2, 12),
+    # indices are re-derived per tile: 4 waves / SIMD (<= 128 VGPRs) (477 -> 448 us per launch
+    # against the 3-wave build, profiles/r4j_train_ab.txt).  Round 6: the prefetch's staging
+    # indices too (two of them were spilled, reloaded with a vmcnt(0) inside the tile loop):
+    # one spilled value left, live only in the prologue / epilogue
+    "t_arm16<2>": (128, 1, 8),
     "t_head_bwd<7, 3, true>": (168, 0, 0),  # unit-pair packed form (output-ReLU architectures)
     # the tiled form (linear output layer, every reference architecture): 4 waves / SIMD
     "t_head_bwd_t<7, 3>": (128, 0, 0),

@@ -4,7 +4,7 @@
 #   gpurun -- 'source tools/gpu_lib.sh gpurun_out/r6a && run tests 600 $PT tests/test_decode_gpu.py && ab 3 lat ...'
 # run NAME SECONDS CMD...   runs CMD from /tmp under its own time limit, output in $OUT/NAME.log;
 #                           a failing step prints its tail and ends the session (no retries)
-# ab N NAME SECONDS CMD...  N interleaved pairs: CMD against tools/ablib/libccmi_base.so (CCMI_LIB)
+# ab N NAME SECONDS CMD...  N interleaved pairs: CMD against $ABLIB (tools/ablib/libccmi_base.so by default, as CCMI_LIB)
 #                           and against the in-tree library -> NAME_base_i / NAME_new_i
 # PT                        the GPU pytest command line (thread timeouts, stops at the first failure)
 ROOT=$(pwd)
@@ -26,7 +26,7 @@ ab() {
     local n=$1 name=$2 secs=$3
     shift 3
     for i in $(seq 1 "$n"); do
-        run "${name}_base_$i" "$secs" env CCMI_LIB="$ROOT/tools/ablib/libccmi_base.so" "$@"
+        run "${name}_base_$i" "$secs" env CCMI_LIB="${ABLIB:-$ROOT/tools/ablib/libccmi_base.so}" "$@"
         run "${name}_new_$i" "$secs" "$@"
     done
 }
