@@ -3066,24 +3066,20 @@ static int resident_wgs(const void *fn, int threads, size_t lds, int max_per_cu)
 // form's 190 us (step 0.842 -> 0.910 ms, profiles/r6h_head_bwd_regs_ab.txt): its 36 16x16x4
 // MFMAs per 16 pixels are half padding (N = 8 of 16 inputs for g_x and dW0), and at 180 VGPRs it
 // runs 2 waves / SIMD with no prefetch of the next block's 25 small loads.
+// (read per call, like CCMI_SP_BWD_PF below, so a test can select either form within one
+// process: a getenv per launch against a ~1 ms step)
 static bool head_bwd_regs()
 {
-    static const bool on = [] {
-        const char *e = getenv("CCMI_HEAD_BWD_REGS");
-        return e && *e == '1';
-    }();
-    return on;
+    const char *e = getenv("CCMI_HEAD_BWD_REGS");
+    return e && *e == '1';
 }
 
 // the 3x3 backward as a persistent prefetching grid (t_sp_bwd<7>) or one tile per workgroup
 // (t_sp_bwd<3>); CCMI_SP_BWD_PF=0 selects the latter (A/B)
 static bool sp_bwd_persistent()
 {
-    static const bool on = [] {
-        const char *e = getenv("CCMI_SP_BWD_PF");
-        return !(e && *e == '0');
-    }();
-    return on;
+    const char *e = getenv("CCMI_SP_BWD_PF");
+    return !(e && *e == '0');
 }
 
 // grid of a persistent kernel over `units` work units per frame, B frames

@@ -88,6 +88,20 @@ def _check_grads(got, st, names):
 
 @pytest.mark.parametrize("f", FILES, ids=lambda f: f.stem)
 def test_gpu_gradients_match_reference(f, gpu):
+    _gradients_match_reference(f, gpu)
+
+
+# the opt-in kernel forms the library ships next to the defaults (train.hip head_bwd_regs /
+# sp_bwd_persistent, read per launch): the register-form head backward (t_head_bwd_m) and the
+# one-tile-per-workgroup 3x3 backward (t_sp_bwd<3>)
+@pytest.mark.parametrize("env", [("CCMI_HEAD_BWD_REGS", "1"), ("CCMI_SP_BWD_PF", "0")], ids=lambda e: f"{e[0]}={e[1]}")
+def test_gpu_gradients_opt_in_kernel_forms(env, gpu, monkeypatch):
+    monkeypatch.setenv(*env)
+    for f in FILES:
+        _gradients_match_reference(f, gpu)
+
+
+def _gradients_match_reference(f, gpu):
     import train_oracle as to
     z = np.load(f)
     of, st, target, meta = _setup(z, gpu)
