@@ -1293,12 +1293,17 @@ __global__ void t_sp_gpre(float *__restrict__ gout, const float *__restrict__ ou
 // current tile computes, and a workgroup flushes its weight gradients once for all its tiles.
 constexpr int kSY = 16, kSX = 64;
 template <int MODE>
-__global__ __launch_bounds__(kT) __attribute__((amdgpu_waves_per_eu(MODE == 2 || MODE == 7 ? 4 : MODE == 3 ? 5 : 1))) void t_sp_bwd(const float *__restrict__ gout, const float *__restrict__ outp,
+__global__ __launch_bounds__(kT) __attribute__((amdgpu_waves_per_eu((MODE & 7) == 2 || (MODE & 7) == 7 ? 4 : (MODE & 7) == 3 ? 5 : 1))) void t_sp_bwd(const float *__restrict__ gout, const float *__restrict__ outp,
                                                const float *__restrict__ in, Geo g, const float *__restrict__ th,
                                                int64_t ps, int wo, int bo, int res, float *__restrict__ gin,
                                                float *__restrict__ gth, int64_t gstride)
 {
     constexpr bool DX = (MODE & 1) != 0, DW = (MODE & 2) != 0, PF = (MODE & 4) != 0;
+    // MODE bit 8: the previous layer's ReLU applied to the input gradient written here, where its
+    // output (this layer's input X) is staged -- that layer's backward then loads no output planes
+    // (a compile-time bit: as a run-time flag the border pass's select spilled ~50 VGPRs)
+    constexpr bool mask_in = (MODE & 8) != 0;
+    static_assert(!mask_in || DW, "the mask reads the staged X");
     constexpr int RH = kSY + 2, RW = kSX + 2;
     // ring images at row pitch kRP = 67 and plane pitch kPP = 1225 (== 3 and 9 mod 32 banks): the 27
     // taps (i, ky, kx) of one pixel sit on 27 distinct banks (9 i + 3 ky + kx), so the weight-
@@ -1475,8 +1480,12 @@ __global__ __launch_bounds__(kT) __attribute__((amdgpu_waves_per_eu(MODE == 2 ||
             }
 #endif
             const int64_t pi = (int64_t)py * W + px;
+            // mask_in (MODE bit 8): the previous layer's ReLU
 #pragma unroll
-            for (int i = 0; i < 3; ++i) Ib[i * npx + pi] = gi[i] + (res ? gp[i] : 0.f);
+            for (int i = 0; i < 3; ++i) {
+                const float v = gi[i] + (res ? gp[i] : 0.f);
+                Ib[i * npx + pi] = (mask_in && SX(i, ry + 1, c + 1) <= 0.f) ? 0.f : v;
+            }
         }
 #if !defined(CCMI_DIAG_SPB_NODX) && !defined(CCMI_DIAG_SPB_NOBORDER)
         // What the replicate padding clamps onto a border pixel -- the padded-domain adjoint at the
@@ -1531,7 +1540,8 @@ __global__ __launch_bounds__(kT) __attribute__((amdgpu_waves_per_eu(MODE == 2 ||
                     }
                     const int64_t pi = (int64_t)by * W + bx;
 #pragma unroll
-                    for (int i = 0; i < 3; ++i) Ib[i * npx + pi] += e[i];
+                    for (int i = 0; i < 3; ++i) // a masked pixel was written 0 and stays 0
+                        Ib[i * npx + pi] += (mask_in && SX(i, ry + 1, cx + 1) <= 0.f) ? 0.f : e[i];
                 }
             }
         }
@@ -3414,9 +3424,13 @@ extern "C" int ccmi_train_step(const ccmi_train_args *a, void *stream)
         // weight gradients: grid-stride over <= 1024 / B workgroups per frame (measured fastest
         // against 32 .. 512 per frame)
         const unsigned nb = (unsigned)std::max(1, std::min(ntile, 1024 / B));
-        const float *outp = g.sp_relu[i] ? F(pl.z[i + 1]) : nullptr;
+        // a ReLU layer's mask comes from its output planes only for the last layer (its output
+        // gradient is the loss's); for the others the next layer's backward applied it (mask_in)
+        const float *outp = g.sp_relu[i] && i == g.n_sp - 1 ? F(pl.z[i + 1]) : nullptr;
+        const int mask_in = i >= 1 && g.sp_relu[i - 1];
 #if defined(CCMI_SP_BWD_SPLIT) // A/B builds: the round-4 pair of launches
         {
+            const float *outp = g.sp_relu[i] ? F(pl.z[i + 1]) : nullptr; // no mask bit: MODE 1 stages no X
             // input gradient: one tile per workgroup; weight gradients: grid-stride as before
             hipLaunchKernelGGL(t_sp_bwd<1>, dim3((unsigned)ntile, B), dim3(kT), 0, s, gcur, outp, F(pl.z[i]), g, a->params,
                                a->param_stride, g.sp_w[i], g.sp_b[i], g.sp_res[i], gin, slots, g.P);
@@ -3426,9 +3440,15 @@ extern "C" int ccmi_train_step(const ccmi_train_args *a, void *stream)
 #else
         (void)nb;
         // both halves, one tile per workgroup: each tile's X / G / out read once
-        if (sp_bwd_persistent())
+        if (sp_bwd_persistent() && mask_in)
+            hipLaunchKernelGGL(t_sp_bwd<15>, resident_grid((const void *)t_sp_bwd<15>, kT, 0, ntile, B), dim3(kT), 0, s, gcur,
+                               outp, F(pl.z[i]), g, a->params, a->param_stride, g.sp_w[i], g.sp_b[i], g.sp_res[i], gin, slots, g.P);
+        else if (sp_bwd_persistent())
             hipLaunchKernelGGL(t_sp_bwd<7>, resident_grid((const void *)t_sp_bwd<7>, kT, 0, ntile, B), dim3(kT), 0, s, gcur,
                                outp, F(pl.z[i]), g, a->params, a->param_stride, g.sp_w[i], g.sp_b[i], g.sp_res[i], gin, slots, g.P);
+        else if (mask_in)
+            hipLaunchKernelGGL(t_sp_bwd<11>, dim3((unsigned)ntile, B), dim3(kT), 0, s, gcur, outp, F(pl.z[i]), g, a->params,
+                               a->param_stride, g.sp_w[i], g.sp_b[i], g.sp_res[i], gin, slots, g.P);
         else
             hipLaunchKernelGGL(t_sp_bwd<3>, dim3((unsigned)ntile, B), dim3(kT), 0, s, gcur, outp, F(pl.z[i]), g, a->params,
                                a->param_stride, g.sp_w[i], g.sp_b[i], g.sp_res[i], gin, slots, g.P);

@@ -52,6 +52,11 @@ BUDGET = {
     # with the 31 KB of LDS five workgroups per CU; profiles/r5zf_*: with the border weights in
     # LDS, 74.6 -> 69.1 us per layer)
     "t_sp_bwd<3>": (96, 0, 0),
+    "t_sp_bwd<11>": (96, 0, 0),   # the same + the previous layer's ReLU mask on the written gradient
+    # persistent form with the next tile's ring in registers: 4 waves / SIMD (one spilled value in
+    # the prologue); with the mask bit none
+    "t_sp_bwd<7>": (128, 1, 8),
+    "t_sp_bwd<15>": (128, 0, 0),
 }
 
 
