@@ -618,7 +618,7 @@ def encoder_shard(rank: int, lambdas=None):
 # hop, c3x; one launch per iteration each).  A HISTORICAL profile, not this run: its sidecar
 # <csv>.sources.json records the sha256 of the kernel sources it was measured on, and the
 # bench line says whether today's sources still match (profile_provenance).
-TRAIN_PROFILE = "profiles/r6g_train_iso_kernel_stats.csv"
+TRAIN_PROFILE = "profiles/r6m_train_iso_kernel_stats.csv"
 TRAIN_FRAMES, TRAIN_H, TRAIN_W = 8, 512, 768
 
 
