@@ -284,8 +284,13 @@ C3X_PHASES = [
 ]
 
 
-# preset "debug" (enc/training/presets.py:380-432): the schedule of the reference's sanity check
-DEBUG_WARMUP = [(3, Phase(max_itr=10)), (2, Phase(max_itr=10))]
+# preset "debug" (preset_cfg/debug.yaml, the file the reference's encoder loads with --preset and
+# tools/gen_golden_rd.py ran the R-D fixtures from): the schedule of the reference's sanity check.
+# Its warm-up trains with kumaraswamy noise parameter 2.0, freq_valid 400, patience 100000 -- the
+# legacy class enc/training/presets.py:380-432 (PresetDebug) leaves the TrainerPhase defaults
+# (noise 1.0), which this schedule followed until round 6.
+DEBUG_WARMUP = [(3, Phase(lr=1e-2, max_itr=10, freq_valid=400, patience=100000, noise_parameter=(2.0, 2.0))),
+                (2, Phase(lr=1e-2, max_itr=10, freq_valid=400, patience=100000, noise_parameter=(2.0, 2.0)))]
 DEBUG_PHASES = [
     Phase(lr=1e-2, max_itr=50, patience=100000, schedule_lr=True, quantizer_noise_type="gaussian",
           softround_temperature=(0.3, 0.1), noise_parameter=(0.25, 0.1)),

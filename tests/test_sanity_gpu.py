@@ -2,8 +2,9 @@
 
 The reference's own test image (test/data/192x128_kodim15.png, kept as
 tests/golden/192x128_kodim15.png) is encoded on the GPU with the debug preset
-(presets.py:380-432: warm-up 3 x 10 then 2 x 10 candidate iterations, phases 50 / 10 / 10,
-network quantisation after the second) and the vlop decoder (cfg/dec/vlop.cfg: ARM 8 x 1,
+(preset_cfg/debug.yaml, which enc/utils/manager.py loads -- its AVAILABLE_PRESETS lookup of the
+class presets.py:380-432 is commented out: warm-up 3 x 10 then 2 x 10 candidate iterations with
+kumaraswamy noise 2.0, phases 50 / 10 / 10, network quantisation after the second) and the vlop decoder (cfg/dec/vlop.cfg: ARM 8 x 1,
 synthesis 8-1-linear-relu / X-1-linear-none / X-3-residual-none, upsampling 8 / 7), written as
 a .cool stream and decoded by the bit-exact HIP decoder to a PPM.  The encoder's estimates
 (results_best.tsv: eval-mode PSNR, latent + network rate) must match the decoded file with
@@ -22,6 +23,8 @@ def test_debug_preset_is_the_reference_schedule():
     from ccmi import train
     assert [c for c, _ in train.DEBUG_WARMUP] == [3, 2]
     assert [p.max_itr for _, p in train.DEBUG_WARMUP] == [10, 10]
+    assert all(p.noise_parameter == (2.0, 2.0) and p.quantizer_noise_type == "kumaraswamy"
+               and p.freq_valid == 400 and p.patience == 100000 for _, p in train.DEBUG_WARMUP)
     assert [p.max_itr for p in train.DEBUG_PHASES] == [50, 10, 10]
     assert [p.quantize_model for p in train.DEBUG_PHASES] == [False, True, False]
     assert train.DEBUG_PHASES[2].optimized_module == "latent"
