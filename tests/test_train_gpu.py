@@ -327,6 +327,17 @@ def test_gpu_gradients_synthesis_and_grid_variants(n_grids, layers, yuv420, gpu)
     _random_arch_vs_oracle(gpu, 42, 66, n_grids, n_grids=n_grids, layers=fo.parse_layers(layers), yuv420=yuv420)
 
 
+@pytest.mark.parametrize("H,W", [(128, 192), (97, 161)])
+def test_gpu_gradients_reference_default_decoder(H, W, gpu):
+    """The reference's default decoder exactly (coolchic/utils/types.py:120-143: ARM 24,2, 7 grids,
+    40-1-linear-relu|3-1-linear-none|3-3-residual-relu|3-3-residual-none) at sizes of several
+    ARM tiles, 3x3-backward tiles and pyramid tiles per level: the VALU ARM t_arm<24, 2> with its
+    4-rows-up contexts, and the next 3x3 layer applying the previous one's ReLU mask."""
+    import forward_oracle as fo
+    _random_arch_vs_oracle(gpu, H, W, 24, dim_arm=24, n_hidden=2, n_grids=7,
+                           layers=fo.parse_layers("40-1-linear-relu|3-1-linear-none|3-3-residual-relu|3-3-residual-none"))
+
+
 @pytest.mark.parametrize("H,W", [(33, 65), (17, 1), (1, 70), (2, 1), (81, 129)])
 def test_gpu_gradients_border_tile_shapes(H, W, gpu):
     """Sizes whose last image row / column is the first of a 16 x 64 backward tile (H = 1 mod
